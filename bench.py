@@ -1,0 +1,261 @@
+#!/usr/bin/env python3
+"""Training-step throughput of the MI355X deformable-Gaussian path (BASELINE.json metric).
+
+One step = one camera/timestep of train_baseline.py:104-182: fused deformation MLP forward ->
+HIP rasterizer forward -> 0.8*L1 + 0.2*(1-SSIM) -> backward (raster + MLP) -> [RCCL grad
+all-reduce when N>1] -> Adam on the Gaussians and the MLP. Workload: synth-100k:
+100k Gaussians, 800x800, blender deformation network (timenet on), SH degree 3, synthetic
+(random-init weights, random target image). Inputs are resident in HBM before timing starts.
+
+Run: python bench.py [--gpus N --steps K --warmup W]; N>1 under torch.distributed.run (one rank per
+GPU, RCCL). Rank 0 prints ONE JSON line (value = whole-job iters/s = world * K / max-rank time).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "deformable-3d-gaussians_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense FP32 matrix peak (spec)
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak (spec)
+
+# algorithmic multiply-accumulates per point of the blender network
+MLP_FWD_MAC = 519936            # every weight once
+MLP_DX_MAC = 484352             # W^T products whose input gradient is needed
+MLP_DW_MAC = 519936             # every weight once
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=100_000)
+    ap.add_argument("--res", type=int, default=800)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--no-adam", action="store_true", help="time only the reference's span (fwd+bwd)")
+    ap.add_argument("--raw-init", action="store_true",
+                    help="keep nn.Linear's default init on the deformation heads (the iteration-3000 transient: "
+                         "deltas O(0.3) make every Gaussian hundreds of pixels wide)")
+    return ap.parse_args()
+
+
+def kernel_algorithmic(name, N, P, HW):
+    """(amount, unit, bound) per launch for the roofline of a kernel class."""
+    if name == "mlp_fwd":
+        return 2.0 * MLP_FWD_MAC * N, "flop", "mfma"
+    if name == "mlp_bwd":
+        return 2.0 * MLP_DX_MAC * N, "flop", "mfma"
+    if name == "mlp_dw":
+        return 2.0 * MLP_DW_MAC * N, "flop", "mfma"
+    if name == "preprocess_fwd":
+        return 327.0 * N, "byte", "hbm"
+    if name == "preprocess_bwd":
+        return 600.0 * N, "byte", "hbm"
+    if name == "blend_fwd":
+        return 44.0 * P + 24.0 * HW, "byte", "hbm"
+    if name == "blend_bwd":
+        return 44.0 * P + 24.0 * HW + 48.0 * N, "byte", "hbm"
+    if name == "sort":
+        return 24.0 * P, "byte", "hbm"
+    if name == "duplicate":
+        return 20.0 * N + 12.0 * P, "byte", "hbm"
+    if name == "ranges":
+        return 8.0 * P, "byte", "hbm"
+    return None
+
+
+KERNEL_CLASSES = ["mlp_fwd", "mlp_bwd", "mlp_dw", "mlp_dw_reduce", "preprocess_fwd", "duplicate", "sort", "ranges",
+                  "blend_fwd", "blend_bwd", "preprocess_bwd"]
+
+
+def cpu_baseline(N, res, steps):
+    """The oracle (oracle/mlp_ref.py float64 numpy MLP + oracle/raster_ref.c OpenMP rasterizer + torch-CPU
+    L1/SSIM) timed on the host for `steps` full steps of the same workload."""
+    from deformgs.synthetic import synth_camera, synth_gaussians
+    from oracle import mlp_ref
+    from oracle.raster import OracleRaster, make_settings
+    from deformgs.loss import l1_loss, ssim
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from weights import mlp_weights
+    threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
+    torch.set_num_threads(threads)
+    g = synth_gaussians(N, seed=0, device="cpu")
+    cam = synth_camera(res, res, index=0, fid=0.5, device="cpu")
+    p = mlp_weights(mlp_ref.param_shapes(True, False), seed=1)
+    gt = torch.rand((3, res, res), generator=torch.Generator().manual_seed(7))
+    s = make_settings(res, res, math.tan(cam.FoVx / 2), math.tan(cam.FoVy / 2), [0, 0, 0], 1.0,
+                      cam.world_view_transform.numpy(), cam.full_proj_transform.numpy(), 3, cam.camera_center.numpy())
+    xyz = g["xyz"].numpy()
+    shs = torch.cat([g["features_dc"], g["features_rest"]], 1).numpy()
+    times = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        t = np.full((N, 1), 0.5, np.float32)
+        out, c = mlp_ref.forward(p, xyz, t, True, False)
+        means = (xyz + out["d_xyz"]).astype(np.float32)
+        scales = (np.exp(g["scaling"].numpy()) + out["d_scale"]).astype(np.float32)
+        rq = g["rotation"].numpy()
+        rots = (rq / np.linalg.norm(rq, axis=1, keepdims=True) + out["d_rot"]).astype(np.float32)
+        op = torch.sigmoid(g["opacity"]).numpy()
+        o = OracleRaster(s, means, shs=shs, opacities=op, scales=scales, rotations=rots)
+        img = torch.from_numpy(o.color).requires_grad_(True)
+        loss = 0.8 * l1_loss(img, gt) + 0.2 * (1.0 - ssim(img, gt))
+        loss.backward()
+        gr = o.backward(img.grad.numpy())
+        gout = {"d_xyz": gr["means3D"], "d_rot": gr["rotations"], "d_scale": gr["scales"]}
+        mlp_ref.backward(p, c, out, gout, True, False)
+        times.append(time.perf_counter() - t0)
+    return dict(value=1.0 / float(np.median(times)), unit="iters/s", cores=threads, kind="port",
+                sample=f"{steps} full step(s) of synth-100k at N={N}, {res}x{res} (median); float64 numpy MLP "
+                       f"(BLAS threads={threads}) + C raster oracle (OpenMP forward, serial backward) + torch-CPU SSIM")
+
+
+def main():
+    args = parse()
+    from deformgs import _lib
+    from deformgs.dist import GradAllReduce, init_from_env
+    from deformgs.deform_model import DeformModelBaseline
+    from deformgs.gaussian_model import GaussianModel
+    from deformgs.arguments import OptimizationParams, PipelineParams
+    from deformgs.synthetic import synth_camera, synth_gaussians
+    from deformgs.train_step import forward_backward, optimizer_step
+    import torch.distributed as dist
+
+    rank, world, local = init_from_env()
+    if world != args.gpus and rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    lib = _lib.load()
+    N, R = args.n, args.res
+    torch.manual_seed(0)
+    g = synth_gaussians(N, seed=0, device=dev)
+    gaussians = GaussianModel(3)
+    gaussians.from_tensors(g["xyz"], g["features_dc"], g["features_rest"], g["scaling"], g["rotation"], g["opacity"])
+    opt = OptimizationParams()
+    gaussians.training_setup(opt)
+    torch.manual_seed(0)
+    deform = DeformModelBaseline(is_blender=True, is_6dof=False, device=dev)
+    if not args.raw_init:
+        # steady-state training: the learned deltas are small (O(1e-3)); scale the random heads so the
+        # rasterizer sees the Gaussians' own footprint, as in every iteration after the first few
+        with torch.no_grad():
+            for head in (deform.deform.gaussian_warp, deform.deform.gaussian_rotation, deform.deform.gaussian_scaling):
+                head.weight.mul_(0.01)
+                head.bias.mul_(0.01)
+    deform.train_setting(opt)
+    pipe = PipelineParams()
+    bg = torch.zeros(3, device=dev)
+    cams = [synth_camera(R, R, index=rank * 97 + k, fid=((rank * 97 + k) % 30) / 30.0, device=dev) for k in range(8)]
+    gt = torch.rand((3, R, R), device=dev, generator=torch.Generator(device=dev).manual_seed(100 + rank))
+    allreduce = GradAllReduce(lambda: list(deform.deform.parameters()) + [
+        gaussians._xyz, gaussians._features_dc, gaussians._features_rest, gaussians._scaling, gaussians._rotation,
+        gaussians._opacity])
+
+    state = {"it": 3000, "P": 0}
+
+    def step(k):
+        cam = cams[k % len(cams)]
+        loss, pkg = forward_backward(gaussians, deform, cam, gt, pipe, bg)
+        allreduce()
+        if not args.no_adam:
+            optimizer_step(gaussians, deform, state["it"])
+        state["it"] += 1
+
+    for k in range(args.warmup):
+        step(k)
+    torch.cuda.synchronize()
+    lib.dgs_timing_reset()
+    lib.dgs_timing_enable(1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    lib.dgs_timing_enable(0)
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+
+    # pair count of one render (for the raster rooflines), measured once outside the timed region
+    from deformgs.renderer import render
+    with torch.no_grad():
+        d = deform.step(gaussians.get_xyz.detach(), cams[0].fid.unsqueeze(0).expand(N, -1))
+    import diff_gaussian_rasterization as dgr
+    # count pairs: rerun one forward through the autograd function to read ctx.num_rendered
+    pk = render(cams[0], gaussians, pipe, bg, d[0], d[1], d[2])
+    P_pairs = int(pk["render"].grad_fn.num_rendered) if hasattr(pk["render"].grad_fn, "num_rendered") else 0
+    del pk
+
+    kernels = {}
+    for name in KERNEL_CLASSES:
+        n_l = _lib.I(0)
+        ms = lib.dgs_timing_query(name.encode(), n_l)
+        if n_l.value:
+            kernels[name] = (ms, n_l.value)
+    HW = R * R
+    best = None
+    for name, (ms, n) in kernels.items():
+        info = kernel_algorithmic(name, N, P_pairs, HW)
+        if info is None:
+            continue
+        if best is None or ms > best[1]:
+            best = (name, ms, n, info)
+    roofline = None
+    if best:
+        name, ms, n, (amount, unit, bound) = best
+        avg_s = ms / 1000.0 / n
+        if bound == "mfma":
+            achieved = amount / avg_s / 1e12
+            roofline = {"bound": "mfma", "kernel": name, "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS,
+                        "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
+                        "avg_launch_ms": avg_s * 1e3, "launches": n}
+        else:
+            achieved = amount / avg_s / 1e9
+            roofline = {"bound": "hbm", "kernel": name, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": None, "avg_launch_ms": avg_s * 1e3,
+                        "launches": n}
+    value = world * args.steps / elapsed
+    result = {
+        "metric": "train iters/s (deform+raster fwd+bwd), 100k Gaussians @ 800x800",
+        "value": value, "unit": "iters/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "fp32", "data": "synthetic (synth-100k, random-init weights)",
+        "config": {"workload": f"synth-100k: {N} Gaussians, {R}x{R}, blender DeformNetworkBaseline, SH3"
+                   + (" (raw-init heads)" if args.raw_init else " (heads at 1/100 init: steady-state deltas)"),
+                   "global_batch": world, "includes_adam": not args.no_adam, "pairs_per_render": P_pairs,
+                   "parallelism": f"dp{world} (frame-parallel, RCCL grad all-reduce)"},
+        "roofline": roofline,
+        "kernels_ms_per_step": {k: v[0] / args.steps for k, v in kernels.items()},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            result["cpu_baseline"] = cpu_baseline(N, R, args.cpu_steps)
+        except Exception as e:  # report, never hide
+            result["cpu_baseline"] = {"error": repr(e)}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,95 @@
+// Error reporting, version and the kernel-timing hooks of libdgs_hip.so.
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "dgs_common.h"
+
+namespace dgs {
+namespace {
+thread_local std::string g_err;
+std::mutex g_tmu;
+bool g_timing = false;
+struct Pending {
+    std::string name;
+    hipEvent_t a, b;
+};
+std::vector<Pending> g_pending;
+std::vector<hipEvent_t> g_free_events;
+std::map<std::string, std::pair<double, int>> g_acc;
+
+hipEvent_t take_event() {
+    if (!g_free_events.empty()) {
+        hipEvent_t e = g_free_events.back();
+        g_free_events.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+void drain_locked() {
+    for (auto &p : g_pending) {
+        float ms = 0.f;
+        if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+            auto &a = g_acc[p.name];
+            a.first += ms;
+            a.second += 1;
+        }
+        g_free_events.push_back(p.a);
+        g_free_events.push_back(p.b);
+    }
+    g_pending.clear();
+}
+}  // namespace
+
+void set_error(const std::string &msg) { g_err = msg; }
+
+ScopedTimer::ScopedTimer(const char *n, hipStream_t s) : name(n), stream(s), ev0(nullptr) {
+    if (!g_timing) return;
+    std::lock_guard<std::mutex> lk(g_tmu);
+    hipEvent_t e = take_event();
+    (void)hipEventRecord(e, stream);
+    ev0 = (void *)e;
+}
+
+ScopedTimer::~ScopedTimer() {
+    if (!ev0) return;
+    std::lock_guard<std::mutex> lk(g_tmu);
+    hipEvent_t e = take_event();
+    (void)hipEventRecord(e, stream);
+    g_pending.push_back({name, (hipEvent_t)ev0, e});
+    if (g_pending.size() > 4096) drain_locked();
+}
+
+}  // namespace dgs
+
+extern "C" const char *dgs_last_error(void) { return dgs::g_err.c_str(); }
+extern "C" const char *dgs_version(void) { return "libdgs_hip 0.1 (gfx950)"; }
+
+extern "C" void dgs_timing_enable(int on) {
+    std::lock_guard<std::mutex> lk(dgs::g_tmu);
+    dgs::g_timing = on != 0;
+}
+
+extern "C" double dgs_timing_query(const char *name, int *launches) {
+    std::lock_guard<std::mutex> lk(dgs::g_tmu);
+    dgs::drain_locked();
+    auto it = dgs::g_acc.find(name);
+    if (it == dgs::g_acc.end()) {
+        if (launches) *launches = 0;
+        return 0.0;
+    }
+    if (launches) *launches = it->second.second;
+    return it->second.first;
+}
+
+extern "C" void dgs_timing_reset(void) {
+    std::lock_guard<std::mutex> lk(dgs::g_tmu);
+    dgs::drain_locked();
+    dgs::g_acc.clear();
+}

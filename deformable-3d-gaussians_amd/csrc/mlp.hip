@@ -1,0 +1,941 @@
+// Fused deformation MLP (positional encoding + timenet + 8x256 trunk with skip + heads) on fp32
+// MFMA (v_mfma_f32_32x32x2_f32: exact fp32 fma chains) for MI355X / gfx950.
+//
+// Replaces DeformNetworkBaseline.forward and its autograd backward (utils/time_utils.py:56-127;
+// DeformNetwork :129-201 via DGS_MLP_NO_ROTSCALE; 6-DoF heads :114-121 emitted raw, exp_se3 stays
+// in the host glue). Default and only supported shape: D=8, W=256, multires=10, skips=[4]
+// (arguments/__init__.py:65-68 and every arguments/*.py config).
+//
+// Layout ("transposed" formulation, Y^T = W X^T): features on MFMA rows, points on MFMA columns.
+// One workgroup = 64 points (two 32-point m-tiles) x 8 waves; wave w owns output n-tile w of a
+// 256-wide layer for both m-tiles, so every weight fragment is read once per workgroup.
+//  * Activations live in LDS as [feature/4][64 points][4] (16-byte groups): the B operand of a
+//    k-step is one ds_read_b128 per lane, and the 32x32 accumulator rows (8j + 4h + 0..3) of a
+//    layer are exactly one ds_write_b128 into the next layer's input image (no shuffles).
+//    LDS regions (groups of 4 features): XE 0-15 | TE 16-23 | H 24-87 | TIN 88-91 | PART 92-123;
+//    XE|TE|H contiguous makes cat(x_emb, t_emb) and cat(x_emb, t_emb, h) plain ranges.
+//  * Weights are re-packed every call (they change every optimizer step) into MFMA A-fragment
+//    order [n-tile][8-feature chunk][64 lanes][4] so each wave-load is 1 KiB contiguous.
+//  * Narrow layers (timenet.2, heads, and the t_emb slices of the backward) split K over the 8
+//    waves and sum their partials in a fixed order (deterministic, no LDS atomics).
+//  * Forward saves every layer's input activations feature-major [F][Ns] (coalesced from the
+//    accumulator layout); backward dX saves every dZ the same way; dW = dZ X^T is a separate
+//    split-N MFMA GEMM + fixed-order slab reduction (deterministic).
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <mutex>
+#include <vector>
+
+#include "dgs_common.h"
+
+namespace dgs {
+namespace mlp {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int BM = 64;          // points per workgroup
+constexpr int NWAVE = 8;
+constexpr int NTHR = NWAVE * 64;
+// LDS group offsets (1 group = 64 points x 4 features = 1 KiB)
+constexpr int G_XE = 0, G_TE = 16, G_H = 24, G_TIN = 88, G_PART = 92, G_TOTAL = 124;
+// padded feature offsets of the concatenated layer input (XE|TE|H)
+constexpr int F_XE = 0, F_TE = 64, F_H = 96;
+
+// saved-activation row offsets ([rows][Ns], feature-major); order keeps each layer input contiguous
+constexpr int S_H0 = 0, S_XE = 1024, S_TE = 1088, S_H4 = 1120, S_TIN = 2144, S_TH = 2160;
+__host__ __device__ constexpr int s_h(int i) { return i < 4 ? S_H0 + 256 * i : S_H4 + 256 * (i - 4); }
+// dZ scratch rows
+constexpr int Z_L0 = 0, Z_G = 2048, Z_TE = 2080, Z_T1 = 2112;
+
+struct Flags {
+    bool blender, sixdof, norotscale;
+    int nout;     // head outputs: 10 or 13
+    int tin;      // raw t PE channels: 13 (L=6) or 21 (L=10)
+    int nsaved;   // saved rows
+    int nz;       // dZ rows
+};
+
+__host__ __device__ inline Flags make_flags(int f) {
+    Flags F;
+    F.blender = f & DGS_MLP_BLENDER;
+    F.sixdof = f & DGS_MLP_6DOF;
+    F.norotscale = f & DGS_MLP_NO_ROTSCALE;
+    F.nout = F.sixdof ? 13 : 10;
+    F.tin = F.blender ? 13 : 21;
+    F.nsaved = F.blender ? 2416 : 2144;
+    F.nz = F.blender ? 2368 : 2080;
+    return F;
+}
+
+// ------------------------------------------------------------------------------------------------
+// packing plan (host): which A-operand images exist and where
+// ------------------------------------------------------------------------------------------------
+struct Seg {  // padded index range [p0, p0+len) <- source index s0 + (p - p0)
+    int p0, len, s0;
+};
+struct PackJob {
+    int src;            // parameter index (weight)
+    int transpose;      // 0: A[n][f] = W[n][f]; 1: A[n][f] = W[f][n] (n over input features)
+    int ntiles, nchunks;
+    int nseg_n, nseg_f;
+    Seg segn[3], segf[3];
+    int off;            // float offset in packed buffer
+};
+struct BiasJob {
+    int src;            // parameter index (bias)
+    int npad;
+    int nseg;
+    Seg seg[3];
+    int off;
+};
+
+struct Plan {
+    Flags F;
+    int nparams;
+    // parameter indices (state_dict order)
+    int pT0w = -1, pT0b = -1, pT2w = -1, pT2b = -1, pLw[8], pLb[8];
+    int nheads;               // number of head linears (3 or 4)
+    int pHw[4], pHb[4], hrows[4];
+    std::vector<PackJob> jobs;
+    std::vector<BiasJob> biases;
+    // forward A images
+    int fT1, fT2, fL[8], fHd;
+    // forward biases (padded)
+    int bT1, bT2, bL[8], bHd;
+    // backward A images (transposed)
+    int tHd, tL[8], tT2;
+    int total;
+};
+
+inline Seg seg(int p0, int len, int s0) { return Seg{p0, len, s0}; }
+
+// input-feature segments of the concatenated trunk inputs
+inline int layer_in_segs(const Flags &F, int layer, Seg *s) {
+    const int te = F.blender ? 30 : F.tin;
+    if (layer == 0) {
+        s[0] = seg(F_XE, 63, 0);
+        s[1] = seg(F_TE, te, 63);
+        return 2;
+    }
+    if (layer == 5) {
+        s[0] = seg(F_XE, 63, 0);
+        s[1] = seg(F_TE, te, 63);
+        s[2] = seg(F_H, 256, 63 + te);
+        return 3;
+    }
+    s[0] = seg(0, 256, 0);
+    return 1;
+}
+
+__host__ __device__ inline int layer_kpad(int layer) { return layer == 0 ? 96 : layer == 5 ? 352 : 256; }
+
+Plan make_plan(int flags) {
+    Plan P;
+    P.F = make_flags(flags);
+    const Flags &F = P.F;
+    int k = 0;
+    if (F.blender) {
+        P.pT0w = k++; P.pT0b = k++; P.pT2w = k++; P.pT2b = k++;
+    }
+    for (int i = 0; i < 8; i++) {
+        P.pLw[i] = k++;
+        P.pLb[i] = k++;
+    }
+    P.nheads = F.sixdof ? 4 : 3;
+    int hr[4] = {3, 3, 4, 3};
+    int hr3[3] = {3, 4, 3};
+    for (int h = 0; h < P.nheads; h++) {
+        P.pHw[h] = k++;
+        P.pHb[h] = k++;
+        P.hrows[h] = F.sixdof ? hr[h] : hr3[h];
+    }
+    P.nparams = k;
+    int off = 0;
+    auto add_job = [&](int src, int tr, int ntiles, int nchunks, int nsn, const Seg *sn, int nsf, const Seg *sf) {
+        PackJob j{};
+        j.src = src; j.transpose = tr; j.ntiles = ntiles; j.nchunks = nchunks;
+        j.nseg_n = nsn; j.nseg_f = nsf;
+        for (int q = 0; q < nsn; q++) j.segn[q] = sn[q];
+        for (int q = 0; q < nsf; q++) j.segf[q] = sf[q];
+        j.off = off;
+        off += ntiles * nchunks * 256;
+        P.jobs.push_back(j);
+        return j.off;
+    };
+    auto add_bias = [&](int src, int npad, int ns, const Seg *s) {
+        BiasJob b{};
+        b.src = src; b.npad = npad; b.nseg = ns;
+        for (int q = 0; q < ns; q++) b.seg[q] = s[q];
+        b.off = off;
+        off += npad;
+        P.biases.push_back(b);
+        return b.off;
+    };
+    Seg full256 = seg(0, 256, 0);
+    if (F.blender) {
+        Seg sf = seg(0, F.tin, 0);
+        P.fT1 = add_job(P.pT0w, 0, 8, 2, 1, &full256, 1, &sf);
+        Seg sn = seg(0, 30, 0);
+        P.fT2 = add_job(P.pT2w, 0, 1, 32, 1, &sn, 1, &full256);
+        P.bT1 = add_bias(P.pT0b, 256, 1, &full256);
+        P.bT2 = add_bias(P.pT2b, 32, 1, &sn);
+        // backward: A[n = TH feature][f = TE feature] = W_T2[f][n]
+        P.tT2 = add_job(P.pT2w, 1, 8, 4, 1, &full256, 1, &sn);
+    } else {
+        P.fT1 = P.fT2 = P.bT1 = P.bT2 = P.tT2 = -1;
+    }
+    for (int i = 0; i < 8; i++) {
+        Seg s[3];
+        int ns = layer_in_segs(F, i, s);
+        int kp = layer_kpad(i);
+        P.fL[i] = add_job(P.pLw[i], 0, 8, kp / 8, 1, &full256, ns, s);
+        P.bL[i] = add_bias(P.pLb[i], 256, 1, &full256);
+        // backward image: rows = padded input features (kp), contraction over the 256 outputs
+        P.tL[i] = add_job(P.pLw[i], 1, kp / 32, 32, ns, s, 1, &full256);
+    }
+    // heads: rows stacked in output order
+    {
+        // one job per head linear writing into row ranges of one 32-row tile: emulate by segments
+        // on n with distinct sources is not expressible (different src params) -> pack per head.
+        int base = off;
+        off += 1 * 32 * 256;  // forward image, 1 n-tile x 32 chunks
+        int tbase = off;
+        off += 8 * 4 * 256;   // transposed image, 8 tiles x 4 chunks
+        int bbase = off;
+        off += 32;
+        int r0 = 0;
+        for (int h = 0; h < P.nheads; h++) {
+            PackJob j{};
+            j.src = P.pHw[h]; j.transpose = 0; j.ntiles = 1; j.nchunks = 32;
+            j.nseg_n = 1; j.segn[0] = seg(r0, P.hrows[h], 0);
+            j.nseg_f = 1; j.segf[0] = full256;
+            j.off = base;
+            P.jobs.push_back(j);
+            PackJob t{};
+            t.src = P.pHw[h]; t.transpose = 1; t.ntiles = 8; t.nchunks = 4;
+            t.nseg_n = 1; t.segn[0] = full256;
+            t.nseg_f = 1; t.segf[0] = seg(r0, P.hrows[h], 0);
+            t.off = tbase;
+            P.jobs.push_back(t);
+            BiasJob b{};
+            b.src = P.pHb[h]; b.npad = 32; b.nseg = 1; b.seg[0] = seg(r0, P.hrows[h], 0);
+            b.off = bbase;
+            P.biases.push_back(b);
+            r0 += P.hrows[h];
+        }
+        P.fHd = base;
+        P.tHd = tbase;
+        P.bHd = bbase;
+    }
+    P.total = off;
+    return P;
+}
+
+// source index of padded index p under segments (or -1 = zero padding)
+__host__ __device__ inline int seg_lookup(const Seg *s, int ns, int p) {
+    for (int q = 0; q < ns; q++)
+        if (p >= s[q].p0 && p < s[q].p0 + s[q].len) return s[q].s0 + (p - s[q].p0);
+    return -1;
+}
+
+struct ParamDesc {
+    const float *ptr;
+    int rows, cols;
+};
+
+// One thread per packed float. Heads jobs share an image: only write where the n-segment matches.
+__global__ void k_pack(PackJob job, ParamDesc src, float *__restrict__ packed, bool zero_fill) {
+    int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    int total = job.ntiles * job.nchunks * 256;
+    if (idx >= total) return;
+    int t = idx & 3;
+    int lane = (idx >> 2) & 63;
+    int rest = idx >> 8;
+    int chunk = rest % job.nchunks;
+    int ntile = rest / job.nchunks;
+    int n = ntile * 32 + (lane & 31);
+    int f = chunk * 8 + 4 * (lane >> 5) + t;
+    int sn = seg_lookup(job.segn, job.nseg_n, n);
+    int sf = seg_lookup(job.segf, job.nseg_f, f);
+    float v = 0.f;
+    bool mine = job.transpose ? (sf >= 0) : (sn >= 0);
+    if (sn >= 0 && sf >= 0) v = job.transpose ? src.ptr[sf * src.cols + sn] : src.ptr[sn * src.cols + sf];
+    if (mine || zero_fill) packed[job.off + idx] = v;
+}
+
+__global__ void k_pack_bias(BiasJob job, ParamDesc src, float *__restrict__ packed, bool zero_fill) {
+    int n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= job.npad) return;
+    int s = seg_lookup(job.seg, job.nseg, n);
+    if (s >= 0)
+        packed[job.off + n] = src.ptr[s];
+    else if (zero_fill)
+        packed[job.off + n] = 0.f;
+}
+
+// ------------------------------------------------------------------------------------------------
+// device GEMM pieces
+// ------------------------------------------------------------------------------------------------
+__device__ inline f32x16 zero16() {
+    f32x16 z;
+#pragma unroll
+    for (int i = 0; i < 16; i++) z[i] = 0.f;
+    return z;
+}
+
+#define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_32x32x2f32((a), (b), (c), 0, 0, 0)
+
+// acc0/acc1 (m-tiles 0/1) += A[ntile] . X over chunks [c0, c1) of the LDS image starting at group g0
+__device__ inline void gemm_2m(const float4 *__restrict__ Apk, int c0, int c1, const float4 *lds, int g0, int lane,
+                               f32x16 &acc0, f32x16 &acc1) {
+    const int h = lane >> 5, m = lane & 31;
+    float4 a_next = (c0 < c1) ? Apk[c0 * 64 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int c = c0; c < c1; c++) {
+        float4 a = a_next;
+        if (c + 1 < c1) a_next = Apk[(c + 1) * 64 + lane];
+        const float4 *grp = lds + (g0 + 2 * c + h) * BM;
+        float4 b0 = grp[m];
+        float4 b1 = grp[32 + m];
+        acc0 = MFMA(a.x, b0.x, acc0);
+        acc1 = MFMA(a.x, b1.x, acc1);
+        acc0 = MFMA(a.y, b0.y, acc0);
+        acc1 = MFMA(a.y, b1.y, acc1);
+        acc0 = MFMA(a.z, b0.z, acc0);
+        acc1 = MFMA(a.z, b1.z, acc1);
+        acc0 = MFMA(a.w, b0.w, acc0);
+        acc1 = MFMA(a.w, b1.w, acc1);
+    }
+}
+
+// single m-tile variant (narrow K-split layers)
+__device__ inline void gemm_1m(const float4 *__restrict__ Apk, int c0, int c1, const float4 *lds, int g0, int mt,
+                               int lane, f32x16 &acc) {
+    const int h = lane >> 5, m = lane & 31;
+    float4 a_next = (c0 < c1) ? Apk[c0 * 64 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int c = c0; c < c1; c++) {
+        float4 a = a_next;
+        if (c + 1 < c1) a_next = Apk[(c + 1) * 64 + lane];
+        float4 b = lds[(g0 + 2 * c + h) * BM + mt * 32 + m];
+        acc = MFMA(a.x, b.x, acc);
+        acc = MFMA(a.y, b.y, acc);
+        acc = MFMA(a.z, b.z, acc);
+        acc = MFMA(a.w, b.w, acc);
+    }
+}
+
+// accumulator (n-tile base n0, m-tile mt) -> LDS groups starting at gout, with bias/relu
+__device__ inline void acc_to_lds(const f32x16 &acc, float4 *lds, int gout, int n0, int mt, int lane,
+                                  const float *bias, bool relu) {
+    const int h = lane >> 5, m = lane & 31;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        int f = n0 + 8 * j + 4 * h;
+        float4 v = make_float4(acc[4 * j], acc[4 * j + 1], acc[4 * j + 2], acc[4 * j + 3]);
+        if (bias) {
+            float4 b = *reinterpret_cast<const float4 *>(bias + f);
+            v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+        }
+        if (relu) {
+            v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+        }
+        lds[(gout + f / 4) * BM + mt * 32 + m] = v;
+    }
+}
+
+// LDS groups [g0, g0+ng) (features 4*ng) -> global rows [row0, row0 + 4ng) of a [rows][Ns] array
+__device__ inline void lds_to_global(const float4 *lds, int g0, int ng, float *__restrict__ dst, int row0, size_t Ns,
+                                     int p0, int tid) {
+    // thread -> (feature, point): consecutive threads = consecutive points (coalesced)
+    for (int e = tid; e < ng * 4 * BM; e += NTHR) {
+        int m = e % BM;
+        int f = e / BM;
+        const float *src = reinterpret_cast<const float *>(lds + (g0 + f / 4) * BM + m);
+        dst[(size_t)(row0 + f) * Ns + p0 + m] = src[f & 3];
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// forward
+// ------------------------------------------------------------------------------------------------
+struct FwdArgs {
+    int N;
+    size_t Ns;
+    const float *xyz, *t;
+    const float *packed;
+    float *out;
+    float *saved;
+    int fT1, fT2, fL[8], fHd, bT1, bT2, bL[8], bHd;
+    int flags;
+};
+
+// narrow layer: 1 output n-tile, K split over 8 waves (4 quarters x 2 m-tiles), fixed-order sum,
+// result (+bias) written to LDS groups gout..gout+7 (32 features)
+__device__ inline void narrow_layer(const float4 *Apk, int nchunks, float4 *lds, int g0, int gout, const float *bias,
+                                    int wave, int lane, int tid) {
+    const int mt = wave & 1, q = wave >> 1;
+    const int per = nchunks / 4;
+    f32x16 acc = zero16();
+    gemm_1m(Apk, q * per, (q + 1) * per, lds, g0, mt, lane, acc);
+    // partial -> PART region slot q (8 groups per slot)
+    acc_to_lds(acc, lds, G_PART + 8 * q, 0, mt, lane, nullptr, false);
+    __syncthreads();
+    for (int e = tid; e < 8 * BM; e += NTHR) {
+        int gi = e / BM, m = e % BM;
+        float4 s0 = lds[(G_PART + gi) * BM + m];
+        float4 s1 = lds[(G_PART + 8 + gi) * BM + m];
+        float4 s2 = lds[(G_PART + 16 + gi) * BM + m];
+        float4 s3 = lds[(G_PART + 24 + gi) * BM + m];
+        float4 r;
+        r.x = ((s0.x + s1.x) + s2.x) + s3.x;
+        r.y = ((s0.y + s1.y) + s2.y) + s3.y;
+        r.z = ((s0.z + s1.z) + s2.z) + s3.z;
+        r.w = ((s0.w + s1.w) + s2.w) + s3.w;
+        if (bias) {
+            float4 b = *reinterpret_cast<const float4 *>(bias + 4 * gi);
+            r.x += b.x; r.y += b.y; r.z += b.z; r.w += b.w;
+        }
+        lds[(gout + gi) * BM + m] = r;
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(NTHR) void k_mlp_fwd(FwdArgs a) {
+    __shared__ float4 lds[G_TOTAL * BM];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int p0 = blockIdx.x * BM;
+    const Flags F = make_flags(a.flags);
+    const float4 *pk = reinterpret_cast<const float4 *>(a.packed);
+    float *lf = reinterpret_cast<float *>(lds);
+    // ---- positional encodings (utils/time_utils.py:42-54) ----
+    for (int e = tid; e < 64 * BM; e += NTHR) {
+        int m = e % BM, f = e / BM;
+        int p = p0 + m;
+        float v = 0.f;
+        if (p < a.N && f < 63) {
+            int d = f % 3, band = f / 3;  // band 0: identity; then (sin, cos) per frequency
+            float x = a.xyz[3 * p + d];
+            if (band == 0) {
+                v = x;
+            } else {
+                int fi = (band - 1) >> 1;
+                float arg = x * (float)(1 << fi);
+                v = ((band - 1) & 1) ? cosf(arg) : sinf(arg);
+            }
+        }
+        lf[((G_XE + f / 4) * BM + m) * 4 + (f & 3)] = v;
+    }
+    {
+        const int tg = F.blender ? G_TIN : G_TE;
+        const int ng = F.blender ? 4 : 8;
+        for (int e = tid; e < ng * 4 * BM; e += NTHR) {
+            int m = e % BM, f = e / BM;
+            int p = p0 + m;
+            float v = 0.f;
+            if (p < a.N && f < F.tin) {
+                float x = a.t[p];
+                if (f == 0) {
+                    v = x;
+                } else {
+                    int fi = (f - 1) >> 1;
+                    float arg = x * (float)(1 << fi);
+                    v = ((f - 1) & 1) ? cosf(arg) : sinf(arg);
+                }
+            }
+            lf[((tg + f / 4) * BM + m) * 4 + (f & 3)] = v;
+        }
+    }
+    __syncthreads();
+    if (a.saved) {
+        lds_to_global(lds, G_XE, 16, a.saved, S_XE, a.Ns, p0, tid);
+        if (F.blender) lds_to_global(lds, G_TIN, 4, a.saved, S_TIN, a.Ns, p0, tid);
+        else lds_to_global(lds, G_TE, 8, a.saved, S_TE, a.Ns, p0, tid);
+    }
+    const float *bias = a.packed;
+    // ---- timenet (blender): Linear(13,256) + ReLU -> H ; Linear(256,30) -> TE ----
+    if (F.blender) {
+        f32x16 c0 = zero16(), c1 = zero16();
+        gemm_2m(pk + a.fT1 / 4 + wave * 2 * 64, 0, 2, lds, G_TIN, lane, c0, c1);
+        acc_to_lds(c0, lds, G_H, wave * 32, 0, lane, bias + a.bT1, true);
+        acc_to_lds(c1, lds, G_H, wave * 32, 1, lane, bias + a.bT1, true);
+        __syncthreads();
+        if (a.saved) lds_to_global(lds, G_H, 64, a.saved, S_TH, a.Ns, p0, tid);
+        narrow_layer(pk + a.fT2 / 4, 32, lds, G_H, G_TE, bias + a.bT2, wave, lane, tid);
+        if (a.saved) lds_to_global(lds, G_TE, 8, a.saved, S_TE, a.Ns, p0, tid);
+    }
+    // ---- trunk: 8 x (Linear + ReLU), skip cat after layer 4 (time_utils.py:107-112) ----
+    for (int L = 0; L < 8; L++) {
+        const int g0 = (L == 0 || L == 5) ? G_XE : G_H;
+        const int nch = layer_kpad(L) / 8;
+        f32x16 c0 = zero16(), c1 = zero16();
+        gemm_2m(pk + a.fL[L] / 4 + wave * nch * 64, 0, nch, lds, g0, lane, c0, c1);
+        __syncthreads();  // all waves finished reading H before it is overwritten
+        acc_to_lds(c0, lds, G_H, wave * 32, 0, lane, bias + a.bL[L], true);
+        acc_to_lds(c1, lds, G_H, wave * 32, 1, lane, bias + a.bL[L], true);
+        __syncthreads();
+        if (a.saved) lds_to_global(lds, G_H, 64, a.saved, s_h(L), a.Ns, p0, tid);
+    }
+    // ---- heads (no activation): [warp | branch_w, branch_v], rotation, scaling -> TE region ----
+    narrow_layer(pk + a.fHd / 4, 32, lds, G_H, G_TE, bias + a.bHd, wave, lane, tid);
+    for (int e = tid; e < F.nout * BM; e += NTHR) {
+        int c = e % F.nout, m = e / F.nout;
+        int p = p0 + m;
+        if (p < a.N) a.out[(size_t)p * F.nout + c] = lf[((G_TE + c / 4) * BM + m) * 4 + (c & 3)];
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// backward (dX chain): dZ_i for every layer -> scratch; deterministic
+// ------------------------------------------------------------------------------------------------
+struct BwdArgs {
+    int N;
+    size_t Ns;
+    const float *packed;
+    const float *saved;
+    const float *dout;
+    float *dz;
+    int tHd, tL[8], tT2;
+    int flags;
+};
+
+// wide transposed layer: out n-tile = wave (rows [32w, 32w+32) of the 256-feature output),
+// reading K from LDS groups g0.., masked by saved activations (relu'), written to LDS H + global dZ
+__device__ inline void mask_store(f32x16 &acc, const float *__restrict__ saved_rows, float *__restrict__ dz_rows,
+                                  size_t Ns, int p0, int mt, int lane, int n0) {
+    const int h = lane >> 5, m = lane & 31;
+    const size_t base = (size_t)(n0 + 4 * h) * Ns + p0 + mt * 32 + m;
+    const float *sv = saved_rows + base;
+    float *dz = dz_rows + base;
+    const int ns = (int)Ns;  // a 32-row tile spans < 2^31 floats
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        const int o = (8 * (r >> 2) + (r & 3)) * ns;
+        float v = sv[o] > 0.f ? acc[r] : 0.f;
+        acc[r] = v;
+        dz[o] = v;
+    }
+}
+
+__global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
+    __shared__ float4 lds[G_TOTAL * BM];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int p0 = blockIdx.x * BM;
+    const Flags F = make_flags(a.flags);
+    const float4 *pk = reinterpret_cast<const float4 *>(a.packed);
+    float *lf = reinterpret_cast<float *>(lds);
+    // dOut -> LDS TIN..(use PART slot 0 region? no: TE region is the head-gradient image G)
+    for (int e = tid; e < 32 * BM; e += NTHR) {
+        int m = e % BM, c = e / BM;
+        int p = p0 + m;
+        float v = (p < a.N && c < F.nout) ? a.dout[(size_t)p * F.nout + c] : 0.f;
+        lf[((G_TE + c / 4) * BM + m) * 4 + (c & 3)] = v;
+        a.dz[(size_t)(Z_G + c) * a.Ns + p] = v;
+    }
+    __syncthreads();
+    // heads^T: dH7 = W_h^T dOut (K = 32 from TE region) -> mask H7 -> dZ7
+    {
+        f32x16 c0 = zero16(), c1 = zero16();
+        gemm_2m(pk + a.tHd / 4 + wave * 4 * 64, 0, 4, lds, G_TE, lane, c0, c1);
+        mask_store(c0, a.saved + (size_t)s_h(7) * a.Ns, a.dz + (size_t)(Z_L0 + 7 * 256) * a.Ns, a.Ns, p0, 0, lane, wave * 32);
+        mask_store(c1, a.saved + (size_t)s_h(7) * a.Ns, a.dz + (size_t)(Z_L0 + 7 * 256) * a.Ns, a.Ns, p0, 1, lane, wave * 32);
+        __syncthreads();  // TE (dOut image) reads done before TE is reused for dTE
+        acc_to_lds(c0, lds, G_H, wave * 32, 0, lane, nullptr, false);
+        acc_to_lds(c1, lds, G_H, wave * 32, 1, lane, nullptr, false);
+    }
+    // zero the dTE accumulator (TE region holds dL/dt_emb from layers 5 and 0)
+    for (int e = tid; e < 8 * BM; e += NTHR) lds[G_TE * BM + e] = make_float4(0.f, 0.f, 0.f, 0.f);
+    __syncthreads();
+    for (int L = 7; L >= 1; L--) {
+        // dX_L = W_L^T dZ_L ; H-part rows of the padded input live at tiles (F_H/32 + w) for L=5
+        const int tile0 = (L == 5) ? F_H / 32 : 0;
+        if (L == 5 && F.blender) {
+            // t_emb slice (padded rows 64..95 = tile 2): narrow K-split partials -> PART
+            const int mt = wave & 1, q = wave >> 1;
+            f32x16 ct = zero16();
+            gemm_1m(pk + a.tL[5] / 4 + (F_TE / 32) * 32 * 64, q * 8, q * 8 + 8, lds, G_H, mt, lane, ct);
+            acc_to_lds(ct, lds, G_PART + 8 * q, 0, mt, lane, nullptr, false);
+        }
+        f32x16 c0 = zero16(), c1 = zero16();
+        gemm_2m(pk + a.tL[L] / 4 + (tile0 + wave) * 32 * 64, 0, 32, lds, G_H, lane, c0, c1);
+        mask_store(c0, a.saved + (size_t)s_h(L - 1) * a.Ns, a.dz + (size_t)(Z_L0 + (L - 1) * 256) * a.Ns, a.Ns, p0, 0, lane, wave * 32);
+        mask_store(c1, a.saved + (size_t)s_h(L - 1) * a.Ns, a.dz + (size_t)(Z_L0 + (L - 1) * 256) * a.Ns, a.Ns, p0, 1, lane, wave * 32);
+        __syncthreads();
+        if (L == 5 && F.blender) {
+            for (int e = tid; e < 8 * BM; e += NTHR) {
+                int gi = e / BM, m = e % BM;
+                float4 s0 = lds[(G_PART + gi) * BM + m], s1 = lds[(G_PART + 8 + gi) * BM + m];
+                float4 s2 = lds[(G_PART + 16 + gi) * BM + m], s3 = lds[(G_PART + 24 + gi) * BM + m];
+                float4 &d = lds[(G_TE + gi) * BM + m];
+                d.x += ((s0.x + s1.x) + s2.x) + s3.x;
+                d.y += ((s0.y + s1.y) + s2.y) + s3.y;
+                d.z += ((s0.z + s1.z) + s2.z) + s3.z;
+                d.w += ((s0.w + s1.w) + s2.w) + s3.w;
+            }
+        }
+        acc_to_lds(c0, lds, G_H, wave * 32, 0, lane, nullptr, false);
+        acc_to_lds(c1, lds, G_H, wave * 32, 1, lane, nullptr, false);
+        __syncthreads();
+    }
+    if (!F.blender) return;  // raw t PE has no parameters upstream of it
+    // layer 0: t_emb slice of W_0^T dZ_0 (narrow)
+    {
+        const int mt = wave & 1, q = wave >> 1;
+        f32x16 ct = zero16();
+        gemm_1m(pk + a.tL[0] / 4 + (F_TE / 32) * 32 * 64, q * 8, q * 8 + 8, lds, G_H, mt, lane, ct);
+        acc_to_lds(ct, lds, G_PART + 8 * q, 0, mt, lane, nullptr, false);
+        __syncthreads();
+        for (int e = tid; e < 8 * BM; e += NTHR) {
+            int gi = e / BM, m = e % BM;
+            float4 s0 = lds[(G_PART + gi) * BM + m], s1 = lds[(G_PART + 8 + gi) * BM + m];
+            float4 s2 = lds[(G_PART + 16 + gi) * BM + m], s3 = lds[(G_PART + 24 + gi) * BM + m];
+            float4 &d = lds[(G_TE + gi) * BM + m];
+            d.x += ((s0.x + s1.x) + s2.x) + s3.x;
+            d.y += ((s0.y + s1.y) + s2.y) + s3.y;
+            d.z += ((s0.z + s1.z) + s2.z) + s3.z;
+            d.w += ((s0.w + s1.w) + s2.w) + s3.w;
+        }
+        __syncthreads();
+    }
+    // dTE (30 real rows) -> global (dW of timenet.2)
+    lds_to_global(lds, G_TE, 8, a.dz, Z_TE, a.Ns, p0, tid);
+    // timenet.2^T: dTH = W_T2^T dTE (K = 32) -> mask TH -> dZ_T1
+    {
+        f32x16 c0 = zero16(), c1 = zero16();
+        gemm_2m(pk + a.tT2 / 4 + wave * 4 * 64, 0, 4, lds, G_TE, lane, c0, c1);
+        mask_store(c0, a.saved + (size_t)S_TH * a.Ns, a.dz + (size_t)Z_T1 * a.Ns, a.Ns, p0, 0, lane, wave * 32);
+        mask_store(c1, a.saved + (size_t)S_TH * a.Ns, a.dz + (size_t)Z_T1 * a.Ns, a.Ns, p0, 1, lane, wave * 32);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// dW = dZ X^T over all points (split-N MFMA GEMM into slabs) + fixed-order reduction
+// ------------------------------------------------------------------------------------------------
+struct WJob {
+    int zrow, nrows;   // dZ rows [zrow, zrow + nrows) (padded layer outputs)
+    int xrow, krows;   // X rows in saved
+    int tn, tk;        // tile index (128 x 128)
+    int slab;          // float offset of this tile's slab block (splits x (128*128 + 128))
+};
+
+constexpr int WT = 128;
+constexpr int SLAB = WT * WT + WT;
+
+__global__ __launch_bounds__(256) void k_dw(const WJob *__restrict__ jobs, int nsplit, size_t Ns, int pts_per_split,
+                                            const float *__restrict__ dz, const float *__restrict__ saved,
+                                            float *__restrict__ slabs) {
+    const WJob J = jobs[blockIdx.x / nsplit];
+    const int split = blockIdx.x % nsplit;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int wn = wave >> 1, wk = wave & 1;
+    const int h = lane >> 5, i = lane & 31;
+    const int pbeg = split * pts_per_split;
+    const int pend = min((int)Ns, pbeg + pts_per_split);
+    // rows handled by this lane
+    const int nA0 = J.tn * WT + wn * 64 + i, nA1 = nA0 + 32;
+    const int kB0 = J.tk * WT + wk * 64 + i, kB1 = kB0 + 32;
+    const bool vA0 = nA0 < J.nrows, vA1 = nA1 < J.nrows, vB0 = kB0 < J.krows, vB1 = kB1 < J.krows;
+    const float *A0 = dz + (size_t)(J.zrow + (vA0 ? nA0 : 0)) * Ns;
+    const float *A1 = dz + (size_t)(J.zrow + (vA1 ? nA1 : 0)) * Ns;
+    const float *B0 = saved + (size_t)(J.xrow + (vB0 ? kB0 : 0)) * Ns;
+    const float *B1 = saved + (size_t)(J.xrow + (vB1 ? kB1 : 0)) * Ns;
+    f32x16 c00 = zero16(), c01 = zero16(), c10 = zero16(), c11 = zero16();
+    float bs0 = 0.f, bs1 = 0.f;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int niter = (pend - pbeg) / 8;  // uniform across the wave (MFMA needs every lane)
+    for (int it = 0; it < niter; it++) {
+        const int p = pbeg + 8 * it + 4 * h;
+        float4 a0 = vA0 ? *reinterpret_cast<const float4 *>(A0 + p) : z4;
+        float4 a1 = vA1 ? *reinterpret_cast<const float4 *>(A1 + p) : z4;
+        float4 b0 = vB0 ? *reinterpret_cast<const float4 *>(B0 + p) : z4;
+        float4 b1 = vB1 ? *reinterpret_cast<const float4 *>(B1 + p) : z4;
+        bs0 += (a0.x + a0.y) + (a0.z + a0.w);
+        bs1 += (a1.x + a1.y) + (a1.z + a1.w);
+        c00 = MFMA(a0.x, b0.x, c00); c01 = MFMA(a0.x, b1.x, c01); c10 = MFMA(a1.x, b0.x, c10); c11 = MFMA(a1.x, b1.x, c11);
+        c00 = MFMA(a0.y, b0.y, c00); c01 = MFMA(a0.y, b1.y, c01); c10 = MFMA(a1.y, b0.y, c10); c11 = MFMA(a1.y, b1.y, c11);
+        c00 = MFMA(a0.z, b0.z, c00); c01 = MFMA(a0.z, b1.z, c01); c10 = MFMA(a1.z, b0.z, c10); c11 = MFMA(a1.z, b1.z, c11);
+        c00 = MFMA(a0.w, b0.w, c00); c01 = MFMA(a0.w, b1.w, c01); c10 = MFMA(a1.w, b0.w, c10); c11 = MFMA(a1.w, b1.w, c11);
+    }
+    float *slab = slabs + J.slab + (size_t)split * SLAB;
+    auto store = [&](const f32x16 &c, int nb, int kb) {
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            int n = nb + 8 * (r >> 2) + 4 * h + (r & 3);
+            slab[n * WT + kb + i] = c[r];
+        }
+    };
+    store(c00, wn * 64, wk * 64);
+    store(c01, wn * 64, wk * 64 + 32);
+    store(c10, wn * 64 + 32, wk * 64);
+    store(c11, wn * 64 + 32, wk * 64 + 32);
+    if (wk == 0) {
+        // lanes l and l+32 hold the same row: combine halves, lane < 32 writes
+        bs0 += __shfl_xor(bs0, 32);
+        bs1 += __shfl_xor(bs1, 32);
+        if (h == 0) {
+            slab[WT * WT + wn * 64 + i] = bs0;
+            slab[WT * WT + wn * 64 + 32 + i] = bs1;
+        }
+    }
+}
+
+struct RJob {
+    float *dst;        // parameter gradient (rows x cols) or bias (rows)
+    int rows, cols;    // cols == 0 -> bias
+    int rowpad0;       // padded output row of source row 0 (head stacking)
+    int nseg;
+    Seg seg[3];        // source col -> padded feature (inverse used via lookup on source side)
+    int slab_base;     // slab offset of tile (0,0) of the layer
+    int ktiles;        // number of k tiles of the layer
+};
+
+// one thread per gradient element; sums the splits in order
+__global__ void k_dw_reduce(RJob J, int nsplit, const float *__restrict__ slabs) {
+    int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    int total = J.cols ? J.rows * J.cols : J.rows;
+    if (idx >= total) return;
+    int r = J.cols ? idx / J.cols : idx;
+    int n = J.rowpad0 + r;
+    int tn = n / WT, nl = n % WT;
+    float s = 0.f;
+    if (J.cols) {
+        int c = idx % J.cols;
+        // padded feature of source column c
+        int f = -1;
+        for (int q = 0; q < J.nseg; q++)
+            if (c >= J.seg[q].s0 && c < J.seg[q].s0 + J.seg[q].len) f = J.seg[q].p0 + (c - J.seg[q].s0);
+        int tk = f / WT, kl = f % WT;
+        const float *sl = slabs + J.slab_base + (size_t)(tn * J.ktiles + tk) * nsplit * SLAB + nl * WT + kl;
+        for (int sp = 0; sp < nsplit; sp++) s += sl[(size_t)sp * SLAB];
+    } else {
+        const float *sl = slabs + J.slab_base + (size_t)(tn * J.ktiles) * nsplit * SLAB + WT * WT + nl;
+        for (int sp = 0; sp < nsplit; sp++) s += sl[(size_t)sp * SLAB];
+    }
+    J.dst[idx] = s;
+}
+
+// dW job list for the flags (host)
+struct WPlan {
+    std::vector<WJob> jobs;
+    struct Layer {
+        int zrow, nrows, xrow, krows, ntiles, ktiles, slab_base;
+    };
+    std::vector<Layer> layers;  // order: L0..L7, heads, T1, T2
+    int slab_floats;
+};
+
+inline WPlan make_wplan(const Flags &F, int nsplit) {
+    WPlan W;
+    int off = 0;
+    auto add = [&](int zrow, int nrows, int xrow, int krows) {
+        WPlan::Layer L{zrow, nrows, xrow, krows, div_up(nrows, WT), div_up(krows, WT), off};
+        for (int tn = 0; tn < L.ntiles; tn++)
+            for (int tk = 0; tk < L.ktiles; tk++) {
+                W.jobs.push_back(WJob{zrow, nrows, xrow, krows, tn, tk, off});
+                off += nsplit * SLAB;
+            }
+        W.layers.push_back(L);
+    };
+    for (int i = 0; i < 8; i++) {
+        int xrow = (i == 0 || i == 5) ? S_XE : s_h(i - 1);
+        add(Z_L0 + 256 * i, 256, xrow, layer_kpad(i));
+    }
+    add(Z_G, 32, s_h(7), 256);
+    if (F.blender) {
+        add(Z_T1, 256, S_TIN, 16);
+        add(Z_TE, 32, S_TH, 256);
+    }
+    W.slab_floats = off;
+    return W;
+}
+
+constexpr int NSPLIT = 32;
+
+}  // namespace mlp
+}  // namespace dgs
+
+using namespace dgs;
+using namespace dgs::mlp;
+
+extern "C" int dgs_deform_outputs(int flags) { return make_flags(flags).nout; }
+extern "C" int dgs_deform_num_params(int flags) { return make_plan(flags).nparams; }
+extern "C" size_t dgs_deform_packed_floats(int flags) { return (size_t)make_plan(flags).total; }
+static size_t padded_points(int N) { return (size_t)div_up(N, BM) * BM; }
+extern "C" size_t dgs_deform_saved_floats(int flags, int N) { return (size_t)make_flags(flags).nsaved * padded_points(N); }
+
+// constant dW job table per (device, flags), uploaded once
+static int job_table(int flags, const WPlan &W, WJob **out) {
+    static std::mutex mu;
+    static std::map<std::pair<int, int>, WJob *> tables;
+    int dev = 0;
+    DGS_HIP_CHECK(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(mu);
+    auto key = std::make_pair(dev, flags);
+    auto it = tables.find(key);
+    if (it != tables.end()) {
+        *out = it->second;
+        return DGS_OK;
+    }
+    WJob *d = nullptr;
+    DGS_HIP_CHECK(hipMalloc(&d, sizeof(WJob) * W.jobs.size()));
+    DGS_HIP_CHECK(hipMemcpy(d, W.jobs.data(), sizeof(WJob) * W.jobs.size(), hipMemcpyHostToDevice));
+    tables[key] = d;
+    *out = d;
+    return DGS_OK;
+}
+
+extern "C" size_t dgs_deform_scratch_floats(int flags, int N) {
+    Flags F = make_flags(flags);
+    WPlan W = make_wplan(F, NSPLIT);
+    return (size_t)F.nz * padded_points(N) + (size_t)W.slab_floats;
+}
+
+static int param_shape(const Plan &P, int idx, int &rows, int &cols) {
+    const Flags &F = P.F;
+    rows = cols = 0;
+    if (F.blender) {
+        if (idx == P.pT0w) { rows = 256; cols = F.tin; return 0; }
+        if (idx == P.pT0b) { rows = 256; return 0; }
+        if (idx == P.pT2w) { rows = 30; cols = 256; return 0; }
+        if (idx == P.pT2b) { rows = 30; return 0; }
+    }
+    const int te = F.blender ? 30 : F.tin;
+    for (int i = 0; i < 8; i++) {
+        if (idx == P.pLw[i]) { rows = 256; cols = i == 0 ? 63 + te : i == 5 ? 256 + 63 + te : 256; return 0; }
+        if (idx == P.pLb[i]) { rows = 256; return 0; }
+    }
+    for (int h = 0; h < P.nheads; h++) {
+        if (idx == P.pHw[h]) { rows = P.hrows[h]; cols = 256; return 0; }
+        if (idx == P.pHb[h]) { rows = P.hrows[h]; return 0; }
+    }
+    return -1;
+}
+
+extern "C" int dgs_deform_pack(int flags, const float *const *params, float *packed, void *stream_) {
+    hipStream_t stream = (hipStream_t)stream_;
+    Plan P = make_plan(flags);
+    for (int k = 0; k < P.nparams; k++)
+        if (!params[k]) {
+            set_error("dgs_deform_pack: null parameter pointer");
+            return DGS_ERR_ARGS;
+        }
+    // head images are shared by several jobs: zero them once, then each job writes its rows
+    DGS_HIP_CHECK(hipMemsetAsync(packed + P.fHd, 0, sizeof(float) * (32 * 256 + 8 * 4 * 256 + 32), stream));
+    for (const PackJob &j : P.jobs) {
+        int r, c;
+        param_shape(P, j.src, r, c);
+        ParamDesc d{params[j.src], r, c};
+        bool head = (j.off == P.fHd || j.off == P.tHd);
+        int total = j.ntiles * j.nchunks * 256;
+        hipLaunchKernelGGL(k_pack, dim3(div_up(total, 256)), dim3(256), 0, stream, j, d, packed, !head);
+    }
+    for (const BiasJob &b : P.biases) {
+        int r, c;
+        param_shape(P, b.src, r, c);
+        ParamDesc d{params[b.src], r, 0};
+        bool head = (b.off == P.bHd);
+        hipLaunchKernelGGL(k_pack_bias, dim3(div_up(b.npad, 64)), dim3(64), 0, stream, b, d, packed, !head);
+    }
+    DGS_LAUNCH_CHECK("k_pack", false, stream);
+    return DGS_OK;
+}
+
+extern "C" int dgs_deform_forward(int flags, int N, const float *xyz, const float *t, const float *packed, float *out,
+                                  float *saved, void *stream_) {
+    hipStream_t stream = (hipStream_t)stream_;
+    if (N < 0 || (N > 0 && (!xyz || !t || !packed || !out))) {
+        set_error("dgs_deform_forward: null argument");
+        return DGS_ERR_ARGS;
+    }
+    if (N == 0) return DGS_OK;
+    Plan P = make_plan(flags);
+    FwdArgs a{};
+    a.N = N;
+    a.Ns = padded_points(N);
+    a.xyz = xyz; a.t = t; a.packed = packed; a.out = out; a.saved = saved;
+    a.fT1 = P.fT1; a.fT2 = P.fT2; a.fHd = P.fHd; a.bT1 = P.bT1; a.bT2 = P.bT2; a.bHd = P.bHd;
+    for (int i = 0; i < 8; i++) { a.fL[i] = P.fL[i]; a.bL[i] = P.bL[i]; }
+    a.flags = flags;
+    {
+        ScopedTimer tm("mlp_fwd", stream);
+        hipLaunchKernelGGL(k_mlp_fwd, dim3(div_up(N, BM)), dim3(NTHR), 0, stream, a);
+    }
+    DGS_LAUNCH_CHECK("k_mlp_fwd", false, stream);
+    return DGS_OK;
+}
+
+extern "C" int dgs_deform_backward(int flags, int N, const float *packed, const float *saved, const float *dout,
+                                   float *scratch, float *const *grads, void *stream_) {
+    hipStream_t stream = (hipStream_t)stream_;
+    if (N < 0 || (N > 0 && (!packed || !saved || !dout || !scratch || !grads))) {
+        set_error("dgs_deform_backward: null argument");
+        return DGS_ERR_ARGS;
+    }
+    Plan P = make_plan(flags);
+    const Flags &F = P.F;
+    if (N == 0) {
+        for (int k = 0; k < P.nparams; k++) {
+            int r, c;
+            param_shape(P, k, r, c);
+            DGS_HIP_CHECK(hipMemsetAsync(grads[k], 0, sizeof(float) * r * (c ? c : 1), stream));
+        }
+        return DGS_OK;
+    }
+    const size_t Ns = padded_points(N);
+    float *dz = scratch;
+    float *slabs = scratch + (size_t)F.nz * Ns;
+    BwdArgs b{};
+    b.N = N; b.Ns = Ns; b.packed = packed; b.saved = saved; b.dout = dout; b.dz = dz;
+    b.tHd = P.tHd; b.tT2 = P.tT2;
+    for (int i = 0; i < 8; i++) b.tL[i] = P.tL[i];
+    b.flags = flags;
+    {
+        ScopedTimer tm("mlp_bwd", stream);
+        hipLaunchKernelGGL(k_mlp_bwd, dim3(div_up(N, BM)), dim3(NTHR), 0, stream, b);
+    }
+    DGS_LAUNCH_CHECK("k_mlp_bwd", false, stream);
+    WPlan W = make_wplan(F, NSPLIT);
+    WJob *djobs = nullptr;
+    if (int rc = job_table(flags, W, &djobs)) return rc;
+    const int pps = div_up((int)(Ns / 8), NSPLIT) * 8;
+    {
+        ScopedTimer tm("mlp_dw", stream);
+        hipLaunchKernelGGL(k_dw, dim3((unsigned)W.jobs.size() * NSPLIT), dim3(256), 0, stream, djobs, NSPLIT, Ns, pps, dz,
+                           saved, slabs);
+    }
+    DGS_LAUNCH_CHECK("k_dw", false, stream);
+    // reductions into the parameter gradients
+    auto reduce = [&](int pw, int pb, const WPlan::Layer &L, int rowpad0, int ns, const Seg *s) -> int {
+        int r, c;
+        param_shape(P, pw, r, c);
+        RJob J{};
+        J.dst = grads[pw]; J.rows = r; J.cols = c; J.rowpad0 = rowpad0; J.nseg = ns;
+        for (int q = 0; q < ns; q++) J.seg[q] = s[q];
+        J.slab_base = L.slab_base; J.ktiles = L.ktiles;
+        hipLaunchKernelGGL(k_dw_reduce, dim3(div_up(r * c, 256)), dim3(256), 0, stream, J, NSPLIT, slabs);
+        RJob B = J;
+        B.dst = grads[pb]; B.cols = 0;
+        hipLaunchKernelGGL(k_dw_reduce, dim3(div_up(r, 256)), dim3(256), 0, stream, B, NSPLIT, slabs);
+        return 0;
+    };
+    {
+        ScopedTimer tm("mlp_dw_reduce", stream);
+        for (int i = 0; i < 8; i++) {
+            Seg s[3];
+            int ns = layer_in_segs(F, i, s);
+            reduce(P.pLw[i], P.pLb[i], W.layers[i], 0, ns, s);
+        }
+        Seg full = seg(0, 256, 0);
+        int r0 = 0;
+        for (int h = 0; h < P.nheads; h++) {
+            reduce(P.pHw[h], P.pHb[h], W.layers[8], r0, 1, &full);
+            r0 += P.hrows[h];
+        }
+        if (F.blender) {
+            Seg st = seg(0, F.tin, 0);
+            reduce(P.pT0w, P.pT0b, W.layers[9], 0, 1, &st);
+            reduce(P.pT2w, P.pT2b, W.layers[10], 0, 1, &full);
+        }
+    }
+    DGS_LAUNCH_CHECK("k_dw_reduce", false, stream);
+    return DGS_OK;
+}

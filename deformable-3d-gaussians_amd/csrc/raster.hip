@@ -1,0 +1,885 @@
+// Differentiable tile rasterizer for MI355X (gfx950): forward + backward kernels and the C ABI
+// entry points dgs_raster_forward / dgs_raster_backward / dgs_raster_ctx_free / dgs_mark_visible.
+//
+// Replaces diff_gaussian_rasterization._C (un-vendored submodule, .gitmodules:4-7) behind the call
+// contract of gaussian_renderer/__init__.py:53-124.
+//
+// Pipeline (one HIP stream, all buffers in HBM, SoA per-Gaussian geometry):
+//   k_preprocess   1 thread / Gaussian: cull, Sigma3D, EWA Sigma2D, conic, radius, tile rect, SH->RGB
+//   scan           hipcub inclusive sum of tiles_touched -> pair offsets (P_pairs read back to host)
+//   k_duplicate    emit (tile<<32 | depth_bits, id) pairs, Gaussian-index order
+//   radix sort     hipcub onesweep over bits [0, 32+bits(tiles)) (stable: ties stay in index order)
+//   k_ranges       [start,end) per tile
+//   k_blend_fwd    1 workgroup (4 waves) / 16x16 tile, LDS-staged 256-Gaussian batches, block-wide
+//                  early exit; writes colour, depth, final T, last contributor
+//   k_blend_bwd    back-to-front replay from the block's max contributor; per-Gaussian gradients
+//                  summed across the wave with DPP (row_shr / row_bcast) and added with ONE atomic
+//                  wave-instruction of 12 contiguous floats per (wave, Gaussian)
+//   k_preprocess_bwd 1 thread / Gaussian: conic->Sigma2D->(Sigma3D, mean), projection, SH, Sigma3D->(s,q)
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <mutex>
+#include <vector>
+
+#include "raster_kernels.h"
+
+namespace dgs {
+
+// ------------------------------------------------------------------------------------------------
+// forward kernels
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_preprocess(
+    int P, int D, int M, const float *__restrict__ means3D, const float *__restrict__ scales, float mod,
+    const float *__restrict__ rots, const float *__restrict__ cov_pre, const float *__restrict__ opac,
+    const float *__restrict__ shs, const float *__restrict__ colors_pre, const float *view,
+    const float *proj, const float *campos, int W, int H, float tanx, float tany, float fx, float fy,
+    int gx, int gy, int *__restrict__ radii, float2 *__restrict__ xy, float4 *__restrict__ conic_o,
+    float4 *__restrict__ rgbd, uint32_t *__restrict__ tiles, uint8_t *__restrict__ clamped) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    Cam cam;
+    load_cam(cam, view, proj, campos);
+    radii[i] = 0;
+    tiles[i] = 0;
+    float3 p = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
+    float3 pv = xform43(cam.v, p);
+    if (pv.z <= 0.2f) return;
+    float c3[6];
+    if (cov_pre) {
+#pragma unroll
+        for (int k = 0; k < 6; k++) c3[k] = cov_pre[6 * i + k];
+    } else {
+        float3 s = make_float3(scales[3 * i], scales[3 * i + 1], scales[3 * i + 2]);
+        float4 q = *reinterpret_cast<const float4 *>(rots + 4 * i);
+        cov3d(s, mod, q, c3);
+    }
+    Ewa e;
+    ewa_T(pv, fx, fy, tanx, tany, cam.v, e);
+    float3 c2 = cov2d(e, c3);
+    float det = c2.x * c2.z - c2.y * c2.y;
+    if (det == 0.f) return;
+    float di = 1.f / det;
+    float3 con = make_float3(c2.z * di, -c2.y * di, c2.x * di);
+    float mid = 0.5f * (c2.x + c2.z);
+    float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+    float l2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+    int rad = (int)ceilf(3.f * sqrtf(fmaxf(l1, l2)));
+    float4 ph = xform44(cam.p, p);
+    float pw = 1.f / (ph.w + 0.0000001f);
+    float px = ((ph.x * pw + 1.f) * W - 1.f) * 0.5f;
+    float py = ((ph.y * pw + 1.f) * H - 1.f) * 0.5f;
+    int x0, y0, x1, y1;
+    tile_rect(px, py, rad, gx, gy, x0, y0, x1, y1);
+    int area = (x1 - x0) * (y1 - y0);
+    if (area == 0) return;
+    float3 rgb;
+    uint8_t cl = 0;
+    if (colors_pre) {
+        rgb = make_float3(colors_pre[3 * i], colors_pre[3 * i + 1], colors_pre[3 * i + 2]);
+    } else {
+        float dx = p.x - cam.c[0], dy = p.y - cam.c[1], dz = p.z - cam.c[2];
+        float n = sqrtf(dx * dx + dy * dy + dz * dz);
+        float x = dx / n, y = dy / n, z = dz / n;
+        const float *sh = shs + (size_t)i * M * 3;
+        float r[3];
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            float v = SH_C0 * sh[c];
+            if (D > 0) {
+                v = v - SH_C1 * y * sh[3 + c] + SH_C1 * z * sh[6 + c] - SH_C1 * x * sh[9 + c];
+                if (D > 1) {
+                    float xx = x * x, yy = y * y, zz = z * z, xy_ = x * y, yz = y * z, xz = x * z;
+                    v = v + SH_C2_0 * xy_ * sh[12 + c] + SH_C2_1 * yz * sh[15 + c] +
+                        SH_C2_2 * (2.f * zz - xx - yy) * sh[18 + c] + SH_C2_3 * xz * sh[21 + c] +
+                        SH_C2_4 * (xx - yy) * sh[24 + c];
+                    if (D > 2) {
+                        v = v + SH_C3_0 * y * (3.f * xx - yy) * sh[27 + c] + SH_C3_1 * xy_ * z * sh[30 + c] +
+                            SH_C3_2 * y * (4.f * zz - xx - yy) * sh[33 + c] +
+                            SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy) * sh[36 + c] +
+                            SH_C3_4 * x * (4.f * zz - xx - yy) * sh[39 + c] +
+                            SH_C3_5 * z * (xx - yy) * sh[42 + c] + SH_C3_6 * x * (xx - 3.f * yy) * sh[45 + c];
+                    }
+                }
+            }
+            v += 0.5f;
+            cl |= (v < 0.f) << c;
+            r[c] = v < 0.f ? 0.f : v;
+        }
+        rgb = make_float3(r[0], r[1], r[2]);
+    }
+    radii[i] = rad;
+    xy[i] = make_float2(px, py);
+    conic_o[i] = make_float4(con.x, con.y, con.z, opac[i]);
+    rgbd[i] = make_float4(rgb.x, rgb.y, rgb.z, pv.z);
+    tiles[i] = (uint32_t)area;
+    clamped[i] = cl;
+}
+
+__global__ __launch_bounds__(256) void k_duplicate(int P, const float2 *__restrict__ xy,
+                                                   const int *__restrict__ radii,
+                                                   const float4 *__restrict__ rgbd,
+                                                   const uint32_t *__restrict__ offsets, int gx, int gy,
+                                                   uint64_t *__restrict__ keys,
+                                                   uint32_t *__restrict__ vals) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    int r = radii[i];
+    if (r <= 0) return;
+    uint32_t off = (i == 0) ? 0u : offsets[i - 1];
+    float2 c = xy[i];
+    int x0, y0, x1, y1;
+    tile_rect(c.x, c.y, r, gx, gy, x0, y0, x1, y1);
+    uint64_t db = (uint64_t)__float_as_uint(rgbd[i].w);
+    for (int y = y0; y < y1; y++)
+        for (int x = x0; x < x1; x++) {
+            keys[off] = ((uint64_t)(y * gx + x) << 32) | db;
+            vals[off] = (uint32_t)i;
+            off++;
+        }
+}
+
+__global__ __launch_bounds__(256) void k_ranges(int L, const uint64_t *__restrict__ keys, uint2 *__restrict__ ranges) {
+    int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= L) return;
+    uint32_t t = (uint32_t)(keys[idx] >> 32);
+    if (idx == 0) {
+        ranges[t].x = 0;
+    } else {
+        uint32_t prev = (uint32_t)(keys[idx - 1] >> 32);
+        if (t != prev) {
+            ranges[prev].y = idx;
+            ranges[t].x = idx;
+        }
+    }
+    if (idx == L - 1) ranges[t].y = L;
+}
+
+__global__ __launch_bounds__(256) void k_blend_fwd(const uint2 *__restrict__ ranges, const uint32_t *__restrict__ vals,
+                                                   int W, int H, int gx, const float2 *__restrict__ xy,
+                                                   const float4 *__restrict__ conic_o, const float4 *__restrict__ rgbd,
+                                                   const float *bg, float *__restrict__ final_T,
+                                                   uint32_t *__restrict__ n_contrib, float *__restrict__ out_color,
+                                                   float *__restrict__ out_depth) {
+    __shared__ float2 s_xy[TILE_PIX];
+    __shared__ float4 s_co[TILE_PIX];
+    __shared__ float4 s_cd[TILE_PIX];
+    const int tile = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int px = (tile % gx) * TILE_X + (tid % TILE_X);
+    const int py = (tile / gx) * TILE_Y + (tid / TILE_X);
+    const bool inside = px < W && py < H;
+    const float pfx = (float)px, pfy = (float)py;
+    uint2 range = ranges[tile];
+    const int todo_total = (int)(range.y - range.x);
+    const int rounds = div_up(todo_total, TILE_PIX);
+    bool done = !inside;
+    float T = 1.f, C0 = 0.f, C1 = 0.f, C2 = 0.f, Dd = 0.f;
+    uint32_t contributor = 0, last = 0;
+    for (int r = 0; r < rounds; r++) {
+        if (__syncthreads_count(done) == TILE_PIX) break;
+        int prog = r * TILE_PIX + tid;
+        if ((int)range.x + prog < (int)range.y) {
+            uint32_t id = vals[range.x + prog];
+            s_xy[tid] = xy[id];
+            s_co[tid] = conic_o[id];
+            s_cd[tid] = rgbd[id];
+        }
+        __syncthreads();
+        int n = min(TILE_PIX, todo_total - r * TILE_PIX);
+        for (int j = 0; !done && j < n; j++) {
+            contributor++;
+            float2 g = s_xy[j];
+            float4 co = s_co[j];
+            float dx = g.x - pfx, dy = g.y - pfy;
+            float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+            if (power > 0.f) continue;
+            float alpha = fminf(0.99f, co.w * __expf(power));
+            if (alpha < 1.f / 255.f) continue;
+            float testT = T * (1.f - alpha);
+            if (testT < 0.0001f) {
+                done = true;
+                continue;
+            }
+            float4 cd = s_cd[j];
+            float w = alpha * T;
+            C0 += cd.x * w;
+            C1 += cd.y * w;
+            C2 += cd.z * w;
+            Dd += cd.w * w;
+            T = testT;
+            last = contributor;
+        }
+    }
+    if (inside) {
+        int pid = py * W + px;
+        final_T[pid] = T;
+        n_contrib[pid] = last;
+        int HW = H * W;
+        out_color[pid] = C0 + T * bg[0];
+        out_color[HW + pid] = C1 + T * bg[1];
+        out_color[2 * HW + pid] = C2 + T * bg[2];
+        out_depth[pid] = Dd;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// backward kernels
+// ------------------------------------------------------------------------------------------------
+// Sum over the 64 lanes, result valid in lane 63 (gfx9 DPP: row_shr 1/2/4/8, row_bcast 15/31).
+__device__ inline float wave_sum63(float v) {
+    int x = __float_as_int(v);
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true));
+    x = __float_as_int(v);
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true));
+    x = __float_as_int(v);
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true));
+    x = __float_as_int(v);
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true));
+    x = __float_as_int(v);
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false));
+    x = __float_as_int(v);
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false));
+    return v;
+}
+
+__device__ inline float lane63(float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63)); }
+
+__global__ __launch_bounds__(256) void k_blend_bwd(const uint2 *__restrict__ ranges, const uint32_t *__restrict__ vals,
+                                                   int W, int H, int gx, const float *bg,
+                                                   const float2 *__restrict__ xy, const float4 *__restrict__ conic_o,
+                                                   const float4 *__restrict__ rgbd, const float *__restrict__ final_T,
+                                                   const uint32_t *__restrict__ n_contrib,
+                                                   const float *__restrict__ dL_dpix, const float *__restrict__ dL_ddepth,
+                                                   float *__restrict__ acc) {
+    __shared__ float2 s_xy[TILE_PIX];
+    __shared__ float4 s_co[TILE_PIX];
+    __shared__ float4 s_cd[TILE_PIX];
+    __shared__ uint32_t s_id[TILE_PIX];
+    __shared__ uint32_t s_maxlast;
+    const int tile = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int px = (tile % gx) * TILE_X + (tid % TILE_X);
+    const int py = (tile / gx) * TILE_Y + (tid / TILE_X);
+    const bool inside = px < W && py < H;
+    const float pfx = (float)px, pfy = (float)py;
+    const uint2 range = ranges[tile];
+    const int pid = py * W + px;
+    const int HW = H * W;
+    float Tfinal = 1.f, dp0 = 0.f, dp1 = 0.f, dp2 = 0.f, ddep = 0.f;
+    uint32_t last = 0;
+    if (inside) {
+        Tfinal = final_T[pid];
+        last = n_contrib[pid];
+        dp0 = dL_dpix[pid];
+        dp1 = dL_dpix[HW + pid];
+        dp2 = dL_dpix[2 * HW + pid];
+        ddep = dL_ddepth ? dL_ddepth[pid] : 0.f;
+    }
+    if (tid == 0) s_maxlast = 0;
+    __syncthreads();
+    atomicMax(&s_maxlast, last);
+    __syncthreads();
+    const int todo_total = (int)s_maxlast;  // Gaussians past every pixel's last contributor are skipped
+    const float b0 = bg[0], b1 = bg[1], b2 = bg[2];
+    const float bgdot = b0 * dp0 + b1 * dp1 + b2 * dp2;
+    const float hx = 0.5f * W, hy = 0.5f * H;
+    float T = Tfinal;
+    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, accd = 0.f;
+    float lc0 = 0.f, lc1 = 0.f, lc2 = 0.f, lcd = 0.f, last_alpha = 0.f;
+    int contributor = todo_total;
+    const int rounds = div_up(todo_total, TILE_PIX);
+    const int end = (int)range.x + todo_total;
+    for (int r = 0; r < rounds; r++) {
+        __syncthreads();
+        int prog = r * TILE_PIX + tid;
+        if (prog < todo_total) {
+            uint32_t id = vals[end - prog - 1];
+            s_id[tid] = id;
+            s_xy[tid] = xy[id];
+            s_co[tid] = conic_o[id];
+            s_cd[tid] = rgbd[id];
+        }
+        __syncthreads();
+        int n = min(TILE_PIX, todo_total - r * TILE_PIX);
+        for (int j = 0; j < n; j++) {
+            contributor--;
+            float2 g = s_xy[j];
+            float4 co = s_co[j];
+            float dx = g.x - pfx, dy = g.y - pfy;
+            float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+            float G = __expf(power);
+            float alpha = fminf(0.99f, co.w * G);
+            bool act = inside && (uint32_t)contributor < last && power <= 0.f && alpha >= 1.f / 255.f;
+            if (__ballot(act) == 0ull) continue;  // wave-uniform
+            float v_mx = 0.f, v_my = 0.f, v_cx = 0.f, v_cy = 0.f, v_cz = 0.f, v_op = 0.f;
+            float v_r = 0.f, v_g = 0.f, v_b = 0.f, v_d = 0.f;
+            if (act) {
+                float4 cd = s_cd[j];
+                T = T / (1.f - alpha);
+                float w = alpha * T;
+                acc0 = last_alpha * lc0 + (1.f - last_alpha) * acc0;
+                acc1 = last_alpha * lc1 + (1.f - last_alpha) * acc1;
+                acc2 = last_alpha * lc2 + (1.f - last_alpha) * acc2;
+                accd = last_alpha * lcd + (1.f - last_alpha) * accd;
+                lc0 = cd.x; lc1 = cd.y; lc2 = cd.z; lcd = cd.w;
+                float dLda = (cd.x - acc0) * dp0 + (cd.y - acc1) * dp1 + (cd.z - acc2) * dp2 + (cd.w - accd) * ddep;
+                v_r = w * dp0;
+                v_g = w * dp1;
+                v_b = w * dp2;
+                v_d = w * ddep;
+                dLda *= T;
+                last_alpha = alpha;
+                dLda += (-Tfinal / (1.f - alpha)) * bgdot;
+                float dLdG = co.w * dLda;
+                float gdx = G * dx, gdy = G * dy;
+                float dGdx = -gdx * co.x - gdy * co.y;
+                float dGdy = -gdy * co.z - gdx * co.y;
+                v_mx = dLdG * dGdx * hx;
+                v_my = dLdG * dGdy * hy;
+                v_cx = -0.5f * gdx * dx * dLdG;
+                v_cy = -0.5f * gdx * dy * dLdG;
+                v_cz = -0.5f * gdy * dy * dLdG;
+                v_op = G * dLda;
+            }
+            float s_mx = lane63(wave_sum63(v_mx));
+            float s_my = lane63(wave_sum63(v_my));
+            float s_cx = lane63(wave_sum63(v_cx));
+            float s_cy = lane63(wave_sum63(v_cy));
+            float s_cz = lane63(wave_sum63(v_cz));
+            float s_op = lane63(wave_sum63(v_op));
+            float s_r = lane63(wave_sum63(v_r));
+            float s_g = lane63(wave_sum63(v_g));
+            float s_b = lane63(wave_sum63(v_b));
+            float s_d = lane63(wave_sum63(v_d));
+            float s_ax = lane63(wave_sum63(fabsf(v_mx)));
+            float s_ay = lane63(wave_sum63(fabsf(v_my)));
+            // spread the 12 sums over lanes 0..11 -> one 48-byte atomic wave-instruction
+            float val = lane == 0 ? s_mx : lane == 1 ? s_my : lane == 2 ? s_cx : lane == 3 ? s_cy
+                      : lane == 4 ? s_cz : lane == 5 ? s_op : lane == 6 ? s_r : lane == 7 ? s_g
+                      : lane == 8 ? s_b : lane == 9 ? s_d : lane == 10 ? s_ax : s_ay;
+            if (lane < ACC_STRIDE) atomicAdd(acc + (size_t)s_id[j] * ACC_STRIDE + lane, val);
+        }
+    }
+}
+
+__device__ inline void dR_dq(float4 q, const float dR[9], float4 &dq) {
+    float r = q.x, x = q.y, y = q.z, z = q.w;
+    dq.x = 2.f * (-z * dR[1] + y * dR[2] + z * dR[3] - x * dR[5] - y * dR[6] + x * dR[7]);
+    dq.y = 2.f * (y * dR[1] + z * dR[2] + y * dR[3] - r * dR[5] + z * dR[6] + r * dR[7]) - 4.f * x * (dR[4] + dR[8]);
+    dq.z = 2.f * (x * dR[1] + r * dR[2] + x * dR[3] + z * dR[5] - r * dR[6] + z * dR[7]) - 4.f * y * (dR[0] + dR[8]);
+    dq.w = 2.f * (-r * dR[1] + x * dR[2] + r * dR[3] + y * dR[5] + x * dR[6] + y * dR[7]) - 4.f * z * (dR[0] + dR[4]);
+}
+
+__global__ __launch_bounds__(256) void k_preprocess_bwd(
+    int P, int D, int M, const float *__restrict__ means3D, const float *__restrict__ scales, float mod,
+    const float *__restrict__ rots, const float *__restrict__ cov_pre, const float *__restrict__ shs,
+    const float *view, const float *proj, const float *campos, int W, int H, float tanx, float tany,
+    float fx, float fy, const int *__restrict__ radii, const uint8_t *__restrict__ clamped,
+    const float *__restrict__ acc, float *__restrict__ dL_dmeans3D, float *__restrict__ dL_dmeans2D,
+    float *__restrict__ dL_ddens, float *__restrict__ dL_dcolors, float *__restrict__ dL_dopac,
+    float *__restrict__ dL_dcov3D, float *__restrict__ dL_dshs, float *__restrict__ dL_dscales,
+    float *__restrict__ dL_drots) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const float *a = acc + (size_t)i * ACC_STRIDE;
+    float4 a0 = *reinterpret_cast<const float4 *>(a);
+    float4 a1 = *reinterpret_cast<const float4 *>(a + 4);
+    float4 a2 = *reinterpret_cast<const float4 *>(a + 8);
+    // a0 = (mx, my, cx, cy), a1 = (cz, op, r, g), a2 = (b, depth, dx, dy)
+    dL_dmeans2D[3 * i] = a0.x;
+    dL_dmeans2D[3 * i + 1] = a0.y;
+    dL_dmeans2D[3 * i + 2] = 0.f;
+    dL_ddens[3 * i] = a2.z;
+    dL_ddens[3 * i + 1] = a2.w;
+    dL_ddens[3 * i + 2] = 0.f;
+    dL_dopac[i] = a1.y;
+    if (dL_dcolors) {
+        dL_dcolors[3 * i] = a1.z;
+        dL_dcolors[3 * i + 1] = a1.w;
+        dL_dcolors[3 * i + 2] = a2.x;
+    }
+    const bool vis = radii[i] > 0;
+    float3 p = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
+    Cam cam;
+    load_cam(cam, view, proj, campos);
+    float dm0 = 0.f, dm1 = 0.f, dm2 = 0.f;
+    float dcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float c3[6];
+    float3 s3 = make_float3(0.f, 0.f, 0.f);
+    float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (vis) {
+        if (cov_pre) {
+#pragma unroll
+            for (int k = 0; k < 6; k++) c3[k] = cov_pre[6 * i + k];
+        } else {
+            s3 = make_float3(scales[3 * i], scales[3 * i + 1], scales[3 * i + 2]);
+            q = *reinterpret_cast<const float4 *>(rots + 4 * i);
+            cov3d(s3, mod, q, c3);
+        }
+        float3 tv = xform43(cam.v, p);
+        Ewa e;
+        ewa_T(tv, fx, fy, tanx, tany, cam.v, e);
+        const float *Tm = e.T;
+        float3 c2 = cov2d(e, c3);
+        float A = c2.x, B = c2.y, Cc = c2.z;
+        float den = A * Cc - B * B;
+        float d2i = 1.f / (den * den + 0.0000001f);
+        float gcx = a0.z, gcy = a0.w, gcz = a1.x;
+        float dLa = 0.f, dLb = 0.f, dLc = 0.f;
+        if (d2i != 0.f) {
+            dLa = d2i * (-Cc * Cc * gcx + 2.f * B * Cc * gcy + (den - A * Cc) * gcz);
+            dLc = d2i * (-A * A * gcz + 2.f * A * B * gcy + (den - A * Cc) * gcx);
+            dLb = d2i * 2.f * (B * Cc * gcx - (den + 2.f * B * B) * gcy + A * B * gcz);
+        }
+        dcov[0] = Tm[0] * Tm[0] * dLa + Tm[0] * Tm[3] * dLb + Tm[3] * Tm[3] * dLc;
+        dcov[3] = Tm[1] * Tm[1] * dLa + Tm[1] * Tm[4] * dLb + Tm[4] * Tm[4] * dLc;
+        dcov[5] = Tm[2] * Tm[2] * dLa + Tm[2] * Tm[5] * dLb + Tm[5] * Tm[5] * dLc;
+        dcov[1] = 2.f * Tm[0] * Tm[1] * dLa + (Tm[0] * Tm[4] + Tm[1] * Tm[3]) * dLb + 2.f * Tm[3] * Tm[4] * dLc;
+        dcov[2] = 2.f * Tm[0] * Tm[2] * dLa + (Tm[0] * Tm[5] + Tm[2] * Tm[3]) * dLb + 2.f * Tm[3] * Tm[5] * dLc;
+        dcov[4] = 2.f * Tm[2] * Tm[1] * dLa + (Tm[1] * Tm[5] + Tm[2] * Tm[4]) * dLb + 2.f * Tm[4] * Tm[5] * dLc;
+        float V[9] = {c3[0], c3[1], c3[2], c3[1], c3[3], c3[4], c3[2], c3[4], c3[5]};
+        float dT[6];
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            float v0 = V[k * 3] * Tm[0] + V[k * 3 + 1] * Tm[1] + V[k * 3 + 2] * Tm[2];
+            float v1 = V[k * 3] * Tm[3] + V[k * 3 + 1] * Tm[4] + V[k * 3 + 2] * Tm[5];
+            dT[k] = 2.f * v0 * dLa + v1 * dLb;
+            dT[3 + k] = 2.f * v1 * dLc + v0 * dLb;
+        }
+        const float *vm = cam.v;
+        // W rows: W0 = (vm0, vm4, vm8), W1 = (vm1, vm5, vm9), W2 = (vm2, vm6, vm10)
+        float dJ00 = vm[0] * dT[0] + vm[4] * dT[1] + vm[8] * dT[2];
+        float dJ02 = vm[2] * dT[0] + vm[6] * dT[1] + vm[10] * dT[2];
+        float dJ11 = vm[1] * dT[3] + vm[5] * dT[4] + vm[9] * dT[5];
+        float dJ12 = vm[2] * dT[3] + vm[6] * dT[4] + vm[10] * dT[5];
+        float tz = e.tz;
+        float tz2 = 1.f / (tz * tz), tz3 = tz2 / tz;
+        float dtx = e.mx * -fx * tz2 * dJ02;
+        float dty = e.my * -fy * tz2 * dJ12;
+        float dtz = -fx * tz2 * dJ00 - fy * tz2 * dJ11 + (2.f * fx * e.tx) * tz3 * dJ02 + (2.f * fy * e.ty) * tz3 * dJ12;
+        dtz += a2.y;  // depth output: depth = t.z
+        dm0 += vm[0] * dtx + vm[1] * dty + vm[2] * dtz;
+        dm1 += vm[4] * dtx + vm[5] * dty + vm[6] * dtz;
+        dm2 += vm[8] * dtx + vm[9] * dty + vm[10] * dtz;
+        // projection: mean2D (NDC) -> mean3D
+        const float *pj = cam.p;
+        float4 ph = xform44(pj, p);
+        float mw = 1.f / (ph.w + 0.0000001f);
+        float mul1 = ph.x * mw * mw, mul2 = ph.y * mw * mw;
+        float gx_ = a0.x, gy_ = a0.y;
+        dm0 += (pj[0] * mw - pj[3] * mul1) * gx_ + (pj[1] * mw - pj[3] * mul2) * gy_;
+        dm1 += (pj[4] * mw - pj[7] * mul1) * gx_ + (pj[5] * mw - pj[7] * mul2) * gy_;
+        dm2 += (pj[8] * mw - pj[11] * mul1) * gx_ + (pj[9] * mw - pj[11] * mul2) * gy_;
+    }
+    // SH backward (also writes zeros for culled Gaussians)
+    if (shs) {
+        float *dsh = dL_dshs + (size_t)i * M * 3;
+        if (!vis) {
+            for (int k = 0; k < M * 3; k++) dsh[k] = 0.f;
+        } else {
+            const float *sh = shs + (size_t)i * M * 3;
+            float vx = p.x - cam.c[0], vy = p.y - cam.c[1], vz = p.z - cam.c[2];
+            float n = sqrtf(vx * vx + vy * vy + vz * vz);
+            float x = vx / n, y = vy / n, z = vz / n;
+            uint8_t cl = clamped[i];
+            float g3[3] = {(cl & 1) ? 0.f : a1.z, (cl & 2) ? 0.f : a1.w, (cl & 4) ? 0.f : a2.x};
+            float ddx = 0.f, ddy = 0.f, ddz = 0.f;
+            float xx = x * x, yy = y * y, zz = z * z, xy_ = x * y, yz = y * z, xz = x * z;
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                float g = g3[c];
+#define SHV(k) sh[(k) * 3 + c]
+                dsh[c] = SH_C0 * g;
+                float gxx = 0.f, gyy = 0.f, gzz = 0.f;
+                if (D > 0) {
+                    dsh[3 + c] = -SH_C1 * y * g;
+                    dsh[6 + c] = SH_C1 * z * g;
+                    dsh[9 + c] = -SH_C1 * x * g;
+                    gxx = -SH_C1 * SHV(3);
+                    gyy = -SH_C1 * SHV(1);
+                    gzz = SH_C1 * SHV(2);
+                    if (D > 1) {
+                        dsh[12 + c] = SH_C2_0 * xy_ * g;
+                        dsh[15 + c] = SH_C2_1 * yz * g;
+                        dsh[18 + c] = SH_C2_2 * (2.f * zz - xx - yy) * g;
+                        dsh[21 + c] = SH_C2_3 * xz * g;
+                        dsh[24 + c] = SH_C2_4 * (xx - yy) * g;
+                        gxx += SH_C2_0 * y * SHV(4) + SH_C2_2 * 2.f * -x * SHV(6) + SH_C2_3 * z * SHV(7) + SH_C2_4 * 2.f * x * SHV(8);
+                        gyy += SH_C2_0 * x * SHV(4) + SH_C2_1 * z * SHV(5) + SH_C2_2 * 2.f * -y * SHV(6) + SH_C2_4 * 2.f * -y * SHV(8);
+                        gzz += SH_C2_1 * y * SHV(5) + SH_C2_2 * 2.f * 2.f * z * SHV(6) + SH_C2_3 * x * SHV(7);
+                        if (D > 2) {
+                            dsh[27 + c] = SH_C3_0 * y * (3.f * xx - yy) * g;
+                            dsh[30 + c] = SH_C3_1 * xy_ * z * g;
+                            dsh[33 + c] = SH_C3_2 * y * (4.f * zz - xx - yy) * g;
+                            dsh[36 + c] = SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy) * g;
+                            dsh[39 + c] = SH_C3_4 * x * (4.f * zz - xx - yy) * g;
+                            dsh[42 + c] = SH_C3_5 * z * (xx - yy) * g;
+                            dsh[45 + c] = SH_C3_6 * x * (xx - 3.f * yy) * g;
+                            gxx += SH_C3_0 * SHV(9) * 3.f * 2.f * xy_ + SH_C3_1 * SHV(10) * yz + SH_C3_2 * SHV(11) * -2.f * xy_ +
+                                   SH_C3_3 * SHV(12) * -3.f * 2.f * xz + SH_C3_4 * SHV(13) * (-3.f * xx + 4.f * zz - yy) +
+                                   SH_C3_5 * SHV(14) * 2.f * xz + SH_C3_6 * SHV(15) * 3.f * (xx - yy);
+                            gyy += SH_C3_0 * SHV(9) * 3.f * (xx - yy) + SH_C3_1 * SHV(10) * xz +
+                                   SH_C3_2 * SHV(11) * (-3.f * yy + 4.f * zz - xx) + SH_C3_3 * SHV(12) * -3.f * 2.f * yz +
+                                   SH_C3_4 * SHV(13) * -2.f * xy_ + SH_C3_5 * SHV(14) * -2.f * yz + SH_C3_6 * SHV(15) * -3.f * 2.f * xy_;
+                            gzz += SH_C3_1 * SHV(10) * xy_ + SH_C3_2 * SHV(11) * 4.f * 2.f * yz +
+                                   SH_C3_3 * SHV(12) * 3.f * (2.f * zz - xx - yy) + SH_C3_4 * SHV(13) * 4.f * 2.f * xz +
+                                   SH_C3_5 * SHV(14) * (xx - yy);
+                        }
+                    }
+                }
+#undef SHV
+                ddx += gxx * g;
+                ddy += gyy * g;
+                ddz += gzz * g;
+            }
+            int kmax = (D + 1) * (D + 1);
+            for (int k = kmax; k < M; k++) {
+                dsh[3 * k] = 0.f;
+                dsh[3 * k + 1] = 0.f;
+                dsh[3 * k + 2] = 0.f;
+            }
+            float s2 = vx * vx + vy * vy + vz * vz;
+            float inv32 = 1.f / sqrtf(s2 * s2 * s2);
+            dm0 += ((s2 - vx * vx) * ddx - vy * vx * ddy - vz * vx * ddz) * inv32;
+            dm1 += (-vx * vy * ddx + (s2 - vy * vy) * ddy - vz * vy * ddz) * inv32;
+            dm2 += (-vx * vz * ddx - vy * vz * ddy + (s2 - vz * vz) * ddz) * inv32;
+        }
+    }
+    dL_dmeans3D[3 * i] = dm0;
+    dL_dmeans3D[3 * i + 1] = dm1;
+    dL_dmeans3D[3 * i + 2] = dm2;
+    if (cov_pre) {
+        if (dL_dcov3D)
+            for (int k = 0; k < 6; k++) dL_dcov3D[6 * i + k] = dcov[k];
+    } else {
+        float ds0 = 0.f, ds1 = 0.f, ds2 = 0.f;
+        float4 dq = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (vis) {
+            float R[9];
+            quat_to_R(q, R);
+            float sp[3] = {mod * s3.x, mod * s3.y, mod * s3.z};
+            float G[9] = {dcov[0], 0.5f * dcov[1], 0.5f * dcov[2], 0.5f * dcov[1], dcov[3], 0.5f * dcov[4],
+                          0.5f * dcov[2], 0.5f * dcov[4], dcov[5]};
+            float L[9];
+#pragma unroll
+            for (int r = 0; r < 3; r++)
+#pragma unroll
+                for (int k = 0; k < 3; k++) L[r * 3 + k] = R[r * 3 + k] * sp[k];
+            float dRm[9];
+            float ds[3];
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                float acc_s = 0.f;
+#pragma unroll
+                for (int r = 0; r < 3; r++) {
+                    float dl = 2.f * (G[r * 3] * L[k] + G[r * 3 + 1] * L[3 + k] + G[r * 3 + 2] * L[6 + k]);
+                    acc_s += dl * R[r * 3 + k];
+                    dRm[r * 3 + k] = dl * sp[k];
+                }
+                ds[k] = acc_s * mod;
+            }
+            ds0 = ds[0]; ds1 = ds[1]; ds2 = ds[2];
+            dR_dq(q, dRm, dq);
+        }
+        dL_dscales[3 * i] = ds0;
+        dL_dscales[3 * i + 1] = ds1;
+        dL_dscales[3 * i + 2] = ds2;
+        *reinterpret_cast<float4 *>(dL_drots + 4 * i) = dq;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_mark_visible(int P, const float *__restrict__ means3D, const float *view,
+                                                      uint8_t *__restrict__ visible) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    float3 p = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
+    float3 pv = make_float3(0.f, 0.f, view[2] * p.x + view[6] * p.y + view[10] * p.z + view[14]);
+    visible[i] = pv.z > 0.2f;
+}
+
+}  // namespace dgs
+
+// ================================================================================================
+// host side: context pool and C ABI
+// ================================================================================================
+using namespace dgs;
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return 0;
+        if (p) DGS_HIP_CHECK(hipFree(p));
+        size_t nb = bytes + bytes / 4 + 4096;
+        p = nullptr;
+        DGS_HIP_CHECK(hipMalloc(&p, nb));
+        cap = nb;
+        return 0;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+struct dgs_raster_ctx {
+    int device = 0;
+    dgs_raster_settings s{};
+    int P = 0, M = 0, H = 0, W = 0, gx = 0, gy = 0, num_rendered = 0;
+    const float *means3D = nullptr, *shs = nullptr, *colors = nullptr, *opac = nullptr, *scales = nullptr,
+                *rots = nullptr, *cov = nullptr;
+    DevBuf geom, bin, img, acc, tmp;
+    // carved views
+    float2 *xy = nullptr;
+    float4 *conic_o = nullptr, *rgbd = nullptr;
+    uint32_t *tiles = nullptr, *offsets = nullptr;
+    uint8_t *clamped = nullptr;
+    uint64_t *keys = nullptr;
+    uint32_t *vals = nullptr;
+    uint2 *ranges = nullptr;
+    float *final_T = nullptr;
+    uint32_t *n_contrib = nullptr;
+    int *radii = nullptr;
+    hipEvent_t released = nullptr;
+    hipStream_t last_stream = nullptr;
+    bool pending_release = false;
+};
+
+namespace {
+std::mutex g_pool_mu;
+std::vector<dgs_raster_ctx *> g_pool;
+
+size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
+
+int bits_for(uint32_t n) {
+    int b = 0;
+    while (n) {
+        b++;
+        n >>= 1;
+    }
+    return b;
+}
+
+dgs_raster_ctx *ctx_acquire(int device, hipStream_t stream) {
+    dgs_raster_ctx *c = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        for (size_t k = 0; k < g_pool.size(); k++) {
+            if (g_pool[k]->device == device) {
+                c = g_pool[k];
+                g_pool.erase(g_pool.begin() + k);
+                break;
+            }
+        }
+    }
+    if (!c) {
+        c = new dgs_raster_ctx();
+        c->device = device;
+    }
+    if (c->pending_release && c->released) {
+        (void)hipStreamWaitEvent(stream, c->released, 0);
+        c->pending_release = false;
+    }
+    return c;
+}
+}  // namespace
+
+extern "C" int dgs_raster_forward(const dgs_raster_settings *s, int P, int M, const float *means3D,
+                                  const float *shs, const float *colors_precomp, const float *opacities,
+                                  const float *scales, const float *rotations, const float *cov3D_precomp,
+                                  float *out_color, float *out_depth, int *out_radii, dgs_raster_ctx **ctx_out,
+                                  int *num_rendered, void *stream_) {
+    hipStream_t stream = (hipStream_t)stream_;
+    if (!s || !ctx_out || P < 0 || !out_color || !out_depth || !out_radii || (P > 0 && (!means3D || !opacities))) {
+        set_error("dgs_raster_forward: null argument");
+        return DGS_ERR_ARGS;
+    }
+    if ((shs == nullptr) == (colors_precomp == nullptr)) {
+        set_error("Please provide exactly one of either SHs or precomputed colors!");
+        return DGS_ERR_ARGS;
+    }
+    if (cov3D_precomp == nullptr && (scales == nullptr || rotations == nullptr)) {
+        set_error("Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
+        return DGS_ERR_ARGS;
+    }
+    if (shs && (M < 1 || M < (s->sh_degree + 1) * (s->sh_degree + 1) || s->sh_degree > 3)) {
+        set_error("dgs_raster_forward: SH degree/coefficient count unsupported (degree <= 3, M >= (D+1)^2)");
+        return DGS_ERR_ARGS;
+    }
+    if (s->image_height <= 0 || s->image_width <= 0) {
+        set_error("dgs_raster_forward: empty image");
+        return DGS_ERR_ARGS;
+    }
+    int device = 0;
+    DGS_HIP_CHECK(hipGetDevice(&device));
+    dgs_raster_ctx *c = ctx_acquire(device, stream);
+    c->s = *s;
+    c->P = P;
+    c->M = M;
+    c->H = s->image_height;
+    c->W = s->image_width;
+    c->gx = div_up(c->W, TILE_X);
+    c->gy = div_up(c->H, TILE_Y);
+    c->means3D = means3D; c->shs = shs; c->colors = colors_precomp; c->opac = opacities;
+    c->scales = scales; c->rots = rotations; c->cov = cov3D_precomp;
+    c->radii = out_radii;
+    c->last_stream = stream;
+    const int T = c->gx * c->gy;
+    const int HW = c->H * c->W;
+    const bool dbg = s->debug != 0;
+    // geometry
+    size_t off_xy = 0, off_co = align_up(off_xy + 8ull * P), off_cd = align_up(off_co + 16ull * P),
+           off_t = align_up(off_cd + 16ull * P), off_o = align_up(off_t + 4ull * P), off_cl = align_up(off_o + 4ull * P);
+    size_t scan_tmp = 0;
+    if (P > 0) DGS_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, scan_tmp, (uint32_t *)nullptr, (uint32_t *)nullptr, P, stream));
+    size_t off_st = align_up(off_cl + P);
+    if (int rc = c->geom.ensure(off_st + scan_tmp + 256)) { ctx_out[0] = nullptr; delete c; return rc; }
+    char *g = (char *)c->geom.p;
+    c->xy = (float2 *)(g + off_xy);
+    c->conic_o = (float4 *)(g + off_co);
+    c->rgbd = (float4 *)(g + off_cd);
+    c->tiles = (uint32_t *)(g + off_t);
+    c->offsets = (uint32_t *)(g + off_o);
+    c->clamped = (uint8_t *)(g + off_cl);
+    // image state
+    size_t off_r = 0, off_T = align_up(off_r + 8ull * T), off_n = align_up(off_T + 4ull * HW);
+    if (int rc = c->img.ensure(off_n + 4ull * HW)) { delete c; return rc; }
+    char *im = (char *)c->img.p;
+    c->ranges = (uint2 *)(im + off_r);
+    c->final_T = (float *)(im + off_T);
+    c->n_contrib = (uint32_t *)(im + off_n);
+
+    const float fx = c->W / (2.f * s->tanfovx), fy = c->H / (2.f * s->tanfovy);
+    int nr = 0;
+    if (P > 0) {
+        {
+            ScopedTimer tm("preprocess_fwd", stream);
+            hipLaunchKernelGGL(k_preprocess, dim3(div_up(P, 256)), dim3(256), 0, stream, P, s->sh_degree, M, means3D, scales,
+                               s->scale_modifier, rotations, cov3D_precomp, opacities, shs, colors_precomp, s->viewmatrix,
+                               s->projmatrix, s->campos, c->W, c->H, s->tanfovx, s->tanfovy, fx, fy, c->gx, c->gy, out_radii,
+                               c->xy, c->conic_o, c->rgbd, c->tiles, c->clamped);
+        }
+        DGS_LAUNCH_CHECK("k_preprocess", dbg, stream);
+        DGS_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(g + off_st, scan_tmp, c->tiles, c->offsets, P, stream));
+        uint32_t total = 0;
+        DGS_HIP_CHECK(hipMemcpyAsync(&total, c->offsets + (P - 1), 4, hipMemcpyDeviceToHost, stream));
+        DGS_HIP_CHECK(hipStreamSynchronize(stream));
+        nr = (int)total;
+    }
+    c->num_rendered = nr;
+    DGS_HIP_CHECK(hipMemsetAsync(c->ranges, 0, 8ull * T, stream));
+    if (nr > 0) {
+        const int end_bit = 32 + bits_for((uint32_t)T);
+        size_t sort_tmp = 0;
+        hipcub::DoubleBuffer<uint64_t> kb(nullptr, nullptr);
+        hipcub::DoubleBuffer<uint32_t> vb(nullptr, nullptr);
+        DGS_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, kb, vb, nr, 0, end_bit, stream));
+        size_t o_k0 = 0, o_k1 = align_up(8ull * nr), o_v0 = align_up(o_k1 + 8ull * nr), o_v1 = align_up(o_v0 + 4ull * nr),
+               o_t = align_up(o_v1 + 4ull * nr);
+        if (int rc = c->bin.ensure(o_t + sort_tmp + 256)) { delete c; return rc; }
+        char *b = (char *)c->bin.p;
+        uint64_t *k0 = (uint64_t *)(b + o_k0), *k1 = (uint64_t *)(b + o_k1);
+        uint32_t *v0 = (uint32_t *)(b + o_v0), *v1 = (uint32_t *)(b + o_v1);
+        {
+            ScopedTimer tm("duplicate", stream);
+            hipLaunchKernelGGL(k_duplicate, dim3(div_up(P, 256)), dim3(256), 0, stream, P, c->xy, out_radii, c->rgbd,
+                               c->offsets, c->gx, c->gy, k0, v0);
+        }
+        DGS_LAUNCH_CHECK("k_duplicate", dbg, stream);
+        hipcub::DoubleBuffer<uint64_t> kbuf(k0, k1);
+        hipcub::DoubleBuffer<uint32_t> vbuf(v0, v1);
+        {
+            ScopedTimer tm("sort", stream);
+            DGS_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(b + o_t, sort_tmp, kbuf, vbuf, nr, 0, end_bit, stream));
+        }
+        c->keys = kbuf.Current();
+        c->vals = vbuf.Current();
+        {
+            ScopedTimer tm("ranges", stream);
+            hipLaunchKernelGGL(k_ranges, dim3(div_up(nr, 256)), dim3(256), 0, stream, nr, c->keys, c->ranges);
+        }
+        DGS_LAUNCH_CHECK("k_ranges", dbg, stream);
+    } else {
+        c->keys = nullptr;
+        c->vals = nullptr;
+    }
+    {
+        ScopedTimer tm("blend_fwd", stream);
+        hipLaunchKernelGGL(k_blend_fwd, dim3(T), dim3(TILE_PIX), 0, stream, c->ranges, c->vals, c->W, c->H, c->gx, c->xy,
+                           c->conic_o, c->rgbd, s->bg, c->final_T, c->n_contrib, out_color, out_depth);
+    }
+    DGS_LAUNCH_CHECK("k_blend_fwd", dbg, stream);
+    *ctx_out = c;
+    if (num_rendered) *num_rendered = nr;
+    return DGS_OK;
+}
+
+extern "C" int dgs_raster_backward(dgs_raster_ctx *c, const float *dL_dcolor, const float *dL_ddepth,
+                                   float *dL_dmeans3D, float *dL_dmeans2D, float *dL_dmeans2D_densify,
+                                   float *dL_dcolors, float *dL_dopacity, float *dL_dcov3D, float *dL_dshs,
+                                   float *dL_dscales, float *dL_drotations, void *stream_) {
+    hipStream_t stream = (hipStream_t)stream_;
+    if (!c || !dL_dcolor || !dL_dmeans3D || !dL_dmeans2D || !dL_dmeans2D_densify || !dL_dopacity) {
+        set_error("dgs_raster_backward: null argument");
+        return DGS_ERR_ARGS;
+    }
+    if ((c->shs && !dL_dshs) || (c->colors && !dL_dcolors) || (c->cov && !dL_dcov3D) ||
+        (!c->cov && (!dL_dscales || !dL_drotations))) {
+        set_error("dgs_raster_backward: missing gradient buffer for the forward's input combination");
+        return DGS_ERR_ARGS;
+    }
+    const int P = c->P;
+    c->last_stream = stream;
+    if (P == 0) return DGS_OK;
+    const bool dbg = c->s.debug != 0;
+    const int T = c->gx * c->gy;
+    if (int rc = c->acc.ensure(4ull * ACC_STRIDE * P)) return rc;
+    float *acc = (float *)c->acc.p;
+    DGS_HIP_CHECK(hipMemsetAsync(acc, 0, 4ull * ACC_STRIDE * P, stream));
+    if (c->num_rendered > 0) {
+        ScopedTimer tm("blend_bwd", stream);
+        hipLaunchKernelGGL(k_blend_bwd, dim3(T), dim3(TILE_PIX), 0, stream, c->ranges, c->vals, c->W, c->H, c->gx, c->s.bg,
+                           c->xy, c->conic_o, c->rgbd, c->final_T, c->n_contrib, dL_dcolor, dL_ddepth, acc);
+    }
+    DGS_LAUNCH_CHECK("k_blend_bwd", dbg, stream);
+    const float fx = c->W / (2.f * c->s.tanfovx), fy = c->H / (2.f * c->s.tanfovy);
+    {
+        ScopedTimer tm("preprocess_bwd", stream);
+        hipLaunchKernelGGL(k_preprocess_bwd, dim3(div_up(P, 256)), dim3(256), 0, stream, P, c->s.sh_degree, c->M, c->means3D,
+                           c->scales, c->s.scale_modifier, c->rots, c->cov, c->shs, c->s.viewmatrix, c->s.projmatrix,
+                           c->s.campos, c->W, c->H, c->s.tanfovx, c->s.tanfovy, fx, fy, c->radii, c->clamped, acc,
+                           dL_dmeans3D, dL_dmeans2D, dL_dmeans2D_densify, dL_dcolors, dL_dopacity, dL_dcov3D, dL_dshs,
+                           dL_dscales, dL_drotations);
+    }
+    DGS_LAUNCH_CHECK("k_preprocess_bwd", dbg, stream);
+    return DGS_OK;
+}
+
+extern "C" void dgs_raster_ctx_free(dgs_raster_ctx *c) {
+    if (!c) return;
+    // Buffers stay allocated for reuse by the next forward on this device; a later acquirer waits
+    // on this event (recorded on the stream that last used the buffers) before reuse.
+    if (!c->released) (void)hipEventCreateWithFlags(&c->released, hipEventDisableTiming);
+    (void)hipEventRecord(c->released, c->last_stream);
+    c->pending_release = true;
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    if (g_pool.size() < 64) {
+        g_pool.push_back(c);
+    } else {
+        c->geom.release(); c->bin.release(); c->img.release(); c->acc.release(); c->tmp.release();
+        delete c;
+    }
+}
+
+extern "C" int dgs_mark_visible(int P, const float *means3D, const float *viewmatrix, const float *projmatrix,
+                                uint8_t *visible, void *stream_) {
+    (void)projmatrix;
+    if (P <= 0) return DGS_OK;
+    hipStream_t stream = (hipStream_t)stream_;
+    hipLaunchKernelGGL(k_mark_visible, dim3(div_up(P, 256)), dim3(256), 0, stream, P, means3D, viewmatrix, visible);
+    DGS_LAUNCH_CHECK("k_mark_visible", false, stream);
+    return DGS_OK;
+}

@@ -1,0 +1,148 @@
+"""Deformation networks on the fused HIP MLP (libdgs_hip.so: dgs_deform_*).
+
+DeformNetworkBaseline / DeformNetwork keep the reference's module tree, parameter names, shapes
+and init (utils/time_utils.py:56-201), so `state_dict()` / `load_state_dict()` and
+deform/iteration_k/deform.pth files are interchangeable with the reference. forward(x, t) runs
+PE + timenet + 8x256 trunk + heads in one MFMA kernel; backward runs the dX chain kernel and the
+split-N dW GEMM. Only the reference's shape is supported (D=8, W=256, multires=10): other shapes
+raise. Gradients flow to the parameters only — every reference call site detaches x
+(train_baseline.py:115, render*.py) and t never requires grad; asking for d/dx raises.
+"""
+import torch
+import torch.nn as nn
+
+from . import _lib
+from .rigid import screw_from_raw
+
+FLAG_BLENDER = 1
+FLAG_6DOF = 2
+FLAG_NO_ROTSCALE = 4
+
+
+def get_embedder_out_dim(multires, i=1):
+    return i + i * 2 * multires
+
+
+class _FusedDeformMLP(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, flags, x, t, *params):
+        lib = _lib.load()
+        dev = x.device
+        N = x.shape[0]
+        stream = _lib.stream_ptr(dev)
+        packed = torch.empty(lib.dgs_deform_packed_floats(flags), dtype=torch.float32, device=dev)
+        params_c = [p.detach().contiguous() for p in params]
+        _lib.check(lib.dgs_deform_pack(flags, _lib.ptr_array(params_c), _lib.ptr(packed), stream), "deform_pack")
+        nout = lib.dgs_deform_outputs(flags)
+        out = torch.empty((N, nout), dtype=torch.float32, device=dev)
+        need_grad = any(ctx.needs_input_grad[3:])
+        saved = (torch.empty(lib.dgs_deform_saved_floats(flags, N), dtype=torch.float32, device=dev)
+                 if need_grad else None)
+        rc = lib.dgs_deform_forward(flags, N, _lib.ptr(x), _lib.ptr(t), _lib.ptr(packed), _lib.ptr(out),
+                                    _lib.ptr(saved), stream)
+        _lib.check(rc, "deform_forward")
+        ctx.flags = flags
+        ctx.N = N
+        ctx.param_shapes = [p.shape for p in params]
+        if need_grad:
+            ctx.save_for_backward(packed, saved)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        lib = _lib.load()
+        packed, saved = ctx.saved_tensors
+        dev = packed.device
+        flags, N = ctx.flags, ctx.N
+        grads = [torch.empty(s, dtype=torch.float32, device=dev) for s in ctx.param_shapes]
+        scratch = torch.empty(lib.dgs_deform_scratch_floats(flags, N), dtype=torch.float32, device=dev)
+        dout = dout.contiguous().float()
+        rc = lib.dgs_deform_backward(flags, N, _lib.ptr(packed), _lib.ptr(saved), _lib.ptr(dout), _lib.ptr(scratch),
+                                     _lib.ptr_array(grads), _lib.stream_ptr(dev))
+        _lib.check(rc, "deform_backward")
+        return (None, None, None, *grads)
+
+
+class _DeformBase(nn.Module):
+    _rotscale = True
+
+    def __init__(self, D=8, W=256, input_ch=3, output_ch=59, multires=10, is_blender=False, is_6dof=False):
+        super().__init__()
+        if D != 8 or W != 256 or multires != 10:
+            raise NotImplementedError("fused deformation MLP supports the reference shape D=8, W=256, multires=10")
+        self.D, self.W = D, W
+        self.input_ch, self.output_ch = input_ch, output_ch
+        self.t_multires = 6 if is_blender else 10
+        self.skips = [D // 2]
+        time_input_ch = get_embedder_out_dim(self.t_multires, 1)
+        xyz_input_ch = get_embedder_out_dim(multires, 3)
+        self.input_ch = xyz_input_ch + time_input_ch
+        if is_blender:
+            self.time_out = 30
+            self.timenet = nn.Sequential(nn.Linear(time_input_ch, 256), nn.ReLU(inplace=True),
+                                         nn.Linear(256, self.time_out))
+            self.linear = nn.ModuleList(
+                [nn.Linear(xyz_input_ch + self.time_out, W)] + [
+                    nn.Linear(W, W) if i not in self.skips else nn.Linear(W + xyz_input_ch + self.time_out, W)
+                    for i in range(D - 1)])
+        else:
+            self.linear = nn.ModuleList(
+                [nn.Linear(self.input_ch, W)] + [
+                    nn.Linear(W, W) if i not in self.skips else nn.Linear(W + self.input_ch, W)
+                    for i in range(D - 1)])
+        self.is_blender = is_blender
+        self.is_6dof = is_6dof
+        if is_6dof:
+            self.branch_w = nn.Linear(W, 3)
+            self.branch_v = nn.Linear(W, 3)
+        else:
+            self.gaussian_warp = nn.Linear(W, 3)
+        self.gaussian_rotation = nn.Linear(W, 4)
+        self.gaussian_scaling = nn.Linear(W, 3)
+        self.flags = (FLAG_BLENDER if is_blender else 0) | (FLAG_6DOF if is_6dof else 0) | (
+            0 if self._rotscale else FLAG_NO_ROTSCALE)
+
+    def kernel_params(self):
+        """Parameters in the order of the C ABI's table (include/dgs.h)."""
+        ps = []
+        if self.is_blender:
+            ps += [self.timenet[0].weight, self.timenet[0].bias, self.timenet[2].weight, self.timenet[2].bias]
+        for l in self.linear:
+            ps += [l.weight, l.bias]
+        heads = [self.branch_w, self.branch_v] if self.is_6dof else [self.gaussian_warp]
+        heads += [self.gaussian_rotation, self.gaussian_scaling]
+        for h in heads:
+            ps += [h.weight, h.bias]
+        return ps
+
+    def raw(self, x, t):
+        """(N, 10) [d_xyz, d_rot, d_scale] or (N, 13) [w, v, d_rot, d_scale] from the fused kernel."""
+        if (x.requires_grad or t.requires_grad) and torch.is_grad_enabled():
+            raise NotImplementedError("fused deformation MLP does not differentiate w.r.t. its inputs; "
+                                      "detach xyz / t as every reference call site does")
+        _lib.require_cuda(x, t)
+        x = x.detach().float().contiguous()
+        t = t.detach().float().reshape(-1, 1).expand(x.shape[0], 1).contiguous()
+        return _FusedDeformMLP.apply(self.flags, x, t, *self.kernel_params())
+
+    def forward(self, x, t):
+        out = self.raw(x, t)
+        if self.is_6dof:
+            d_xyz = screw_from_raw(out[:, 0:3], out[:, 3:6])
+            rot, scale = out[:, 6:10], out[:, 10:13]
+        else:
+            d_xyz = out[:, 0:3]
+            rot, scale = out[:, 3:7], out[:, 7:10]
+        if not self._rotscale:
+            return d_xyz, 0, 0
+        return d_xyz, rot, scale
+
+
+class DeformNetworkBaseline(_DeformBase):
+    """utils/time_utils.py:56-127."""
+    _rotscale = True
+
+
+class DeformNetwork(_DeformBase):
+    """utils/time_utils.py:129-201 (fork variant: rotation = scaling = 0)."""
+    _rotscale = False

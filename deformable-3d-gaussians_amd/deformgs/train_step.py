@@ -1,0 +1,34 @@
+"""One training iteration of train_baseline.py:104-182 on the HIP path (shared by bench.py and the
+harness): deform -> render -> 0.8*L1 + 0.2*(1-SSIM) -> backward [-> grad all-reduce] -> Adam.
+"""
+import torch
+
+from .loss import l1_loss, ssim
+from .renderer import render
+
+
+def forward_backward(gaussians, deform, cam, gt_image, pipe, background, is_6dof=False, lambda_dssim=0.2,
+                     warm=True, ast_noise=0.0):
+    """train_baseline.py:104-128 (timed span of the reference's iter_start/iter_end events)."""
+    if not warm:
+        d_xyz, d_rotation, d_scaling = 0.0, 0.0, 0.0
+    else:
+        N = gaussians.get_xyz.shape[0]
+        time_input = cam.fid.unsqueeze(0).expand(N, -1)
+        d_xyz, d_rotation, d_scaling = deform.step(gaussians.get_xyz.detach(), time_input + ast_noise)
+    pkg = render(cam, gaussians, pipe, background, d_xyz, d_rotation, d_scaling, is_6dof)
+    image = pkg["render"]
+    Ll1 = l1_loss(image, gt_image)
+    loss = (1.0 - lambda_dssim) * Ll1 + lambda_dssim * (1.0 - ssim(image, gt_image))
+    loss.backward()
+    return loss, pkg
+
+
+def optimizer_step(gaussians, deform, iteration):
+    """train_baseline.py:176-182."""
+    gaussians.optimizer.step()
+    gaussians.update_learning_rate(iteration)
+    deform.optimizer.step()
+    gaussians.optimizer.zero_grad(set_to_none=True)
+    deform.optimizer.zero_grad()
+    deform.update_learning_rate(iteration)

@@ -1,0 +1,125 @@
+/*
+ * dgs.h — C ABI of libdgs_hip.so, the MI355X (gfx950) deformable-Gaussian training path.
+ *
+ * Plain pointers and sizes only: every float / int pointer is a DEVICE pointer (HBM) unless the comment
+ * says "host"; every entry point enqueues on `stream` (a hipStream_t passed as void*) and returns
+ * 0 on success or a negative dgs_status; dgs_last_error() gives the message.
+ *
+ * Reference interfaces replaced (preacherwhite/Deformable-3D-Gaussians):
+ *   dgs_raster_forward   <- diff_gaussian_rasterization._C.rasterize_gaussians, called through
+ *                           GaussianRasterizer.forward at gaussian_renderer/__init__.py:115-124
+ *                           (submodule .gitmodules:4-7, un-vendored; contract: SURVEY.md section 8a R1-R9)
+ *   dgs_raster_backward  <- diff_gaussian_rasterization._C.rasterize_gaussians_backward (autograd
+ *                           of the same call; grads consumed at train_baseline.py:128,163-165)
+ *   dgs_raster_ctx_free  <- release of the geometry/binning/image buffers the upstream op keeps in
+ *                           its autograd ctx
+ *   dgs_mark_visible     <- diff_gaussian_rasterization._C.mark_visible (GaussianRasterizer.markVisible)
+ *   dgs_deform_*         <- DeformNetworkBaseline.forward / autograd backward
+ *                           (utils/time_utils.py:56-127, called via scene/deform_model.py:323-324)
+ *   dgs_knn_dist2        <- simple_knn._C.distCUDA2 (scene/gaussian_model.py:20,105-106)
+ */
+#ifndef DGS_H
+#define DGS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    DGS_OK = 0,
+    DGS_ERR_ARGS = -1,      /* bad argument combination (upstream raises Exception) */
+    DGS_ERR_HIP = -2,       /* a HIP runtime/launch error */
+    DGS_ERR_UNSUPPORTED = -3,
+    DGS_ERR_OOM = -4
+} dgs_status;
+
+/* GaussianRasterizationSettings (gaussian_renderer/__init__.py:53-66). The four tensor fields of
+ * the reference (bg, viewmatrix, projmatrix, campos) are device pointers so no host sync is needed. */
+typedef struct dgs_raster_settings {
+    int image_height;
+    int image_width;
+    float tanfovx;
+    float tanfovy;
+    const float *bg;          /* (3,) device */
+    float scale_modifier;
+    const float *viewmatrix;  /* (4,4) device, world_view_transform (row-vector convention) */
+    const float *projmatrix;  /* (4,4) device, full_proj_transform */
+    int sh_degree;            /* active degree D (0..3) */
+    const float *campos;      /* (3,) device */
+    int prefiltered;
+    int debug;                /* synchronise + check after every kernel */
+} dgs_raster_settings;
+
+typedef struct dgs_raster_ctx dgs_raster_ctx;
+
+const char *dgs_last_error(void);
+const char *dgs_version(void);
+
+/* Forward. Exactly one of {shs, colors_precomp} and one of {(scales, rotations), cov3D_precomp}
+ * must be non-NULL. P Gaussians, M SH coefficients per colour channel (shs is (P, M, 3)).
+ * Outputs: out_color (3,H,W), out_depth (1,H,W), out_radii (P,) int32.
+ * *ctx receives the saved state for dgs_raster_backward; *num_rendered (host) = tile pairs. */
+int dgs_raster_forward(const dgs_raster_settings *s, int P, int M,
+                       const float *means3D, const float *shs, const float *colors_precomp,
+                       const float *opacities, const float *scales, const float *rotations,
+                       const float *cov3D_precomp,
+                       float *out_color, float *out_depth, int *out_radii,
+                       dgs_raster_ctx **ctx, int *num_rendered, void *stream);
+
+/* Backward. dL_ddepth may be NULL. Every output array is fully written (zeros where culled).
+ * dL_dmeans2D / dL_dmeans2D_densify are (P,3) with z = 0 (NDC units, like upstream).
+ * dL_dcolors is written only when forward got colors_precomp; dL_dcov3D only for cov3D_precomp;
+ * dL_dshs / dL_dscales / dL_drotations only in the opposite cases (others may be NULL). */
+int dgs_raster_backward(dgs_raster_ctx *ctx, const float *dL_dcolor, const float *dL_ddepth,
+                        float *dL_dmeans3D, float *dL_dmeans2D, float *dL_dmeans2D_densify,
+                        float *dL_dcolors, float *dL_dopacity, float *dL_dcov3D, float *dL_dshs,
+                        float *dL_dscales, float *dL_drotations, void *stream);
+
+void dgs_raster_ctx_free(dgs_raster_ctx *ctx);
+
+/* Frustum test only (p_view.z > 0.2): visible (P,) uint8. */
+int dgs_mark_visible(int P, const float *means3D, const float *viewmatrix, const float *projmatrix,
+                     uint8_t *visible, void *stream);
+
+/* ---- timing hooks (bench.py): per-kernel-class HIP event accumulation on the launch stream ---- */
+void dgs_timing_enable(int on);
+/* Returns accumulated ms for kernel class `name` and its launch count (host); syncs those events. */
+double dgs_timing_query(const char *name, int *launches);
+void dgs_timing_reset(void);
+
+/* ---- deformation MLP (utils/time_utils.py:56-201), fused PE + 8x256 MLP on fp32 MFMA ---- */
+enum {
+    DGS_MLP_BLENDER = 1,   /* timenet on (t: L=6 -> 256 -> 30); else raw t PE (L=10, 21 ch) */
+    DGS_MLP_6DOF = 2,      /* heads branch_w(3), branch_v(3) instead of gaussian_warp(3) */
+    DGS_MLP_NO_ROTSCALE = 4 /* DeformNetwork fork variant: rotation/scaling heads unused */
+};
+
+/* Parameter table: device pointers in state_dict order of DeformNetworkBaseline
+ * (timenet.0.w, timenet.0.b, timenet.2.w, timenet.2.b [blender only], linear.0.w, linear.0.b, ...,
+ *  linear.7.b, then head weights/biases: warp|branch_w[,branch_v], rotation, scaling). */
+int dgs_deform_num_params(int flags);
+size_t dgs_deform_packed_floats(int flags);
+/* floats of activation storage kept by forward for backward (N points) */
+size_t dgs_deform_saved_floats(int flags, int N);
+size_t dgs_deform_scratch_floats(int flags, int N);
+int dgs_deform_pack(int flags, const float *const *params, float *packed, void *stream);
+/* out: (N, n_out) with n_out = 10 (d_xyz3, d_rot4, d_scale3) or 13 for 6-DoF (w3, v3, rot4, scale3).
+ * t: (N,1) per-point time. saved may be NULL for inference (no backward). */
+int dgs_deform_forward(int flags, int N, const float *xyz, const float *t, const float *packed,
+                       float *out, float *saved, void *stream);
+/* dout: (N, n_out). grads: device pointers in the same order as params (overwritten).
+ * scratch: dgs_deform_scratch_floats(flags, N) floats. */
+int dgs_deform_backward(int flags, int N, const float *packed, const float *saved, const float *dout,
+                        float *scratch, float *const *grads, void *stream);
+int dgs_deform_outputs(int flags);
+
+/* ---- simple-knn replacement: mean squared distance to the 3 nearest neighbours ---- */
+int dgs_knn_dist2(int P, const float *points, float *dist2, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
