@@ -619,41 +619,90 @@ struct WJob {
 
 constexpr int WT = 128;
 constexpr int SLAB = WT * WT + WT;
+constexpr int PC = 32;           // points per LDS chunk
+constexpr int LDA = PC + 4;      // padded LDS row (floats)
 
-__global__ __launch_bounds__(256) void k_dw(const WJob *__restrict__ jobs, int nsplit, size_t Ns, int pts_per_split,
+// One 128x128 tile of dW (+ bias row sums) over a contiguous point range. 4 waves (2x2 of 64x64),
+// chunk of 32 points staged through double-buffered LDS: coalesced 128-B row loads for the next
+// chunk are issued before the MFMAs of the current one (register-staged, written after compute).
+__global__ __launch_bounds__(256) void k_dw(const WJob *__restrict__ jobs, int nsplit, size_t Ns, int chunks_per_split,
                                             const float *__restrict__ dz, const float *__restrict__ saved,
                                             float *__restrict__ slabs) {
+    __shared__ float4 lds4[2 * 2 * WT * LDA / 4];
+    float *ldsf = reinterpret_cast<float *>(lds4);
     const WJob J = jobs[blockIdx.x / nsplit];
     const int split = blockIdx.x % nsplit;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int wn = wave >> 1, wk = wave & 1;
     const int h = lane >> 5, i = lane & 31;
-    const int pbeg = split * pts_per_split;
-    const int pend = min((int)Ns, pbeg + pts_per_split);
-    // rows handled by this lane
-    const int nA0 = J.tn * WT + wn * 64 + i, nA1 = nA0 + 32;
-    const int kB0 = J.tk * WT + wk * 64 + i, kB1 = kB0 + 32;
-    const bool vA0 = nA0 < J.nrows, vA1 = nA1 < J.nrows, vB0 = kB0 < J.krows, vB1 = kB1 < J.krows;
-    const float *A0 = dz + (size_t)(J.zrow + (vA0 ? nA0 : 0)) * Ns;
-    const float *A1 = dz + (size_t)(J.zrow + (vA1 ? nA1 : 0)) * Ns;
-    const float *B0 = saved + (size_t)(J.xrow + (vB0 ? kB0 : 0)) * Ns;
-    const float *B1 = saved + (size_t)(J.xrow + (vB1 ? kB1 : 0)) * Ns;
+    const int nchunks_total = (int)(Ns / PC);
+    const int c0 = split * chunks_per_split;
+    const int c1 = min(nchunks_total, c0 + chunks_per_split);
+    // global staging map: element e = tid + 256*j (j < 4): row = e / 8, float4 column = e % 8
+    const float *srcA[4];
+    const float *srcB[4];
+    bool okA[4], okB[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        int e = tid + 256 * j;
+        int row = e >> 3, col = (e & 7) * 4;
+        int nr = J.tn * WT + row, kr = J.tk * WT + row;
+        okA[j] = nr < J.nrows;
+        okB[j] = kr < J.krows;
+        srcA[j] = dz + (size_t)(J.zrow + (okA[j] ? nr : 0)) * Ns + col;
+        srcB[j] = saved + (size_t)(J.xrow + (okB[j] ? kr : 0)) * Ns + col;
+    }
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 ra[4], rb[4];
+    auto gload = [&](int c) {
+        const size_t po = (size_t)c * PC;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            ra[j] = okA[j] ? *reinterpret_cast<const float4 *>(srcA[j] + po) : z4;
+            rb[j] = okB[j] ? *reinterpret_cast<const float4 *>(srcB[j] + po) : z4;
+        }
+    };
+    auto lstore = [&](int buf) {
+        float *A = ldsf + buf * (2 * WT * LDA);
+        float *B = A + WT * LDA;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            int e = tid + 256 * j;
+            int row = e >> 3, col = (e & 7) * 4;
+            *reinterpret_cast<float4 *>(A + row * LDA + col) = ra[j];
+            *reinterpret_cast<float4 *>(B + row * LDA + col) = rb[j];
+        }
+    };
     f32x16 c00 = zero16(), c01 = zero16(), c10 = zero16(), c11 = zero16();
     float bs0 = 0.f, bs1 = 0.f;
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int niter = (pend - pbeg) / 8;  // uniform across the wave (MFMA needs every lane)
-    for (int it = 0; it < niter; it++) {
-        const int p = pbeg + 8 * it + 4 * h;
-        float4 a0 = vA0 ? *reinterpret_cast<const float4 *>(A0 + p) : z4;
-        float4 a1 = vA1 ? *reinterpret_cast<const float4 *>(A1 + p) : z4;
-        float4 b0 = vB0 ? *reinterpret_cast<const float4 *>(B0 + p) : z4;
-        float4 b1 = vB1 ? *reinterpret_cast<const float4 *>(B1 + p) : z4;
-        bs0 += (a0.x + a0.y) + (a0.z + a0.w);
-        bs1 += (a1.x + a1.y) + (a1.z + a1.w);
-        c00 = MFMA(a0.x, b0.x, c00); c01 = MFMA(a0.x, b1.x, c01); c10 = MFMA(a1.x, b0.x, c10); c11 = MFMA(a1.x, b1.x, c11);
-        c00 = MFMA(a0.y, b0.y, c00); c01 = MFMA(a0.y, b1.y, c01); c10 = MFMA(a1.y, b0.y, c10); c11 = MFMA(a1.y, b1.y, c11);
-        c00 = MFMA(a0.z, b0.z, c00); c01 = MFMA(a0.z, b1.z, c01); c10 = MFMA(a1.z, b0.z, c10); c11 = MFMA(a1.z, b1.z, c11);
-        c00 = MFMA(a0.w, b0.w, c00); c01 = MFMA(a0.w, b1.w, c01); c10 = MFMA(a1.w, b0.w, c10); c11 = MFMA(a1.w, b1.w, c11);
+    if (c0 < c1) {
+        gload(c0);
+        lstore(0);
+    }
+    __syncthreads();
+    const int ra0 = wn * 64 + i, ra1 = ra0 + 32, rb0 = wk * 64 + i, rb1 = rb0 + 32;
+    for (int c = c0; c < c1; c++) {
+        const int buf = (c - c0) & 1;
+        const bool more = c + 1 < c1;
+        if (more) gload(c + 1);
+        const float *A = ldsf + buf * (2 * WT * LDA);
+        const float *B = A + WT * LDA;
+#pragma unroll
+        for (int g = 0; g < PC / 8; g++) {
+            const int o = 8 * g + 4 * h;
+            float4 a0 = *reinterpret_cast<const float4 *>(A + ra0 * LDA + o);
+            float4 a1 = *reinterpret_cast<const float4 *>(A + ra1 * LDA + o);
+            float4 b0 = *reinterpret_cast<const float4 *>(B + rb0 * LDA + o);
+            float4 b1 = *reinterpret_cast<const float4 *>(B + rb1 * LDA + o);
+            bs0 += (a0.x + a0.y) + (a0.z + a0.w);
+            bs1 += (a1.x + a1.y) + (a1.z + a1.w);
+            c00 = MFMA(a0.x, b0.x, c00); c01 = MFMA(a0.x, b1.x, c01); c10 = MFMA(a1.x, b0.x, c10); c11 = MFMA(a1.x, b1.x, c11);
+            c00 = MFMA(a0.y, b0.y, c00); c01 = MFMA(a0.y, b1.y, c01); c10 = MFMA(a1.y, b0.y, c10); c11 = MFMA(a1.y, b1.y, c11);
+            c00 = MFMA(a0.z, b0.z, c00); c01 = MFMA(a0.z, b1.z, c01); c10 = MFMA(a1.z, b0.z, c10); c11 = MFMA(a1.z, b1.z, c11);
+            c00 = MFMA(a0.w, b0.w, c00); c01 = MFMA(a0.w, b1.w, c01); c10 = MFMA(a1.w, b0.w, c10); c11 = MFMA(a1.w, b1.w, c11);
+        }
+        if (more) lstore(buf ^ 1);
+        __syncthreads();
     }
     float *slab = slabs + J.slab + (size_t)split * SLAB;
     auto store = [&](const f32x16 &c, int nb, int kb) {
@@ -683,26 +732,35 @@ struct RJob {
     int rows, cols;    // cols == 0 -> bias
     int rowpad0;       // padded output row of source row 0 (head stacking)
     int nseg;
-    Seg seg[3];        // source col -> padded feature (inverse used via lookup on source side)
+    Seg seg[3];        // source col <-> padded feature
     int slab_base;     // slab offset of tile (0,0) of the layer
     int ktiles;        // number of k tiles of the layer
 };
 
-// one thread per gradient element; sums the splits in order
-__global__ void k_dw_reduce(RJob J, int nsplit, const float *__restrict__ slabs) {
+constexpr int MAXR = 28;
+struct RJobs {
+    RJob j[MAXR];
+    int begin[MAXR + 1];  // element prefix
+    int n;
+};
+
+// one thread per gradient element of every parameter; sums the splits in a fixed order
+__global__ __launch_bounds__(256) void k_dw_reduce(RJobs R, int nsplit, const float *__restrict__ slabs) {
     int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    int total = J.cols ? J.rows * J.cols : J.rows;
-    if (idx >= total) return;
+    if (idx >= R.begin[R.n]) return;
+    int q = 0;
+    while (idx >= R.begin[q + 1]) q++;
+    const RJob &J = R.j[q];
+    idx -= R.begin[q];
     int r = J.cols ? idx / J.cols : idx;
     int n = J.rowpad0 + r;
     int tn = n / WT, nl = n % WT;
     float s = 0.f;
     if (J.cols) {
         int c = idx % J.cols;
-        // padded feature of source column c
         int f = -1;
-        for (int q = 0; q < J.nseg; q++)
-            if (c >= J.seg[q].s0 && c < J.seg[q].s0 + J.seg[q].len) f = J.seg[q].p0 + (c - J.seg[q].s0);
+        for (int k = 0; k < J.nseg; k++)
+            if (c >= J.seg[k].s0 && c < J.seg[k].s0 + J.seg[k].len) f = J.seg[k].p0 + (c - J.seg[k].s0);
         int tk = f / WT, kl = f % WT;
         const float *sl = slabs + J.slab_base + (size_t)(tn * J.ktiles + tk) * nsplit * SLAB + nl * WT + kl;
         for (int sp = 0; sp < nsplit; sp++) s += sl[(size_t)sp * SLAB];
@@ -748,7 +806,7 @@ inline WPlan make_wplan(const Flags &F, int nsplit) {
     return W;
 }
 
-constexpr int NSPLIT = 32;
+constexpr int NSPLIT = 13;  // 38 blocks-tiles x 13 = 494 workgroups: one wave of 2 per CU
 
 }  // namespace mlp
 }  // namespace dgs
@@ -896,45 +954,53 @@ extern "C" int dgs_deform_backward(int flags, int N, const float *packed, const 
     WPlan W = make_wplan(F, NSPLIT);
     WJob *djobs = nullptr;
     if (int rc = job_table(flags, W, &djobs)) return rc;
-    const int pps = div_up((int)(Ns / 8), NSPLIT) * 8;
+    const int cps = div_up((int)(Ns / PC), NSPLIT);
     {
         ScopedTimer tm("mlp_dw", stream);
-        hipLaunchKernelGGL(k_dw, dim3((unsigned)W.jobs.size() * NSPLIT), dim3(256), 0, stream, djobs, NSPLIT, Ns, pps, dz,
+        hipLaunchKernelGGL(k_dw, dim3((unsigned)W.jobs.size() * NSPLIT), dim3(256), 0, stream, djobs, NSPLIT, Ns, cps, dz,
                            saved, slabs);
     }
     DGS_LAUNCH_CHECK("k_dw", false, stream);
-    // reductions into the parameter gradients
-    auto reduce = [&](int pw, int pb, const WPlan::Layer &L, int rowpad0, int ns, const Seg *s) -> int {
+    // one batched reduction launch into every parameter gradient
+    RJobs R{};
+    int total = 0;
+    auto add = [&](int pidx, int rowpad0, int ns, const Seg *sg, const WPlan::Layer &L, bool bias) {
         int r, c;
-        param_shape(P, pw, r, c);
-        RJob J{};
-        J.dst = grads[pw]; J.rows = r; J.cols = c; J.rowpad0 = rowpad0; J.nseg = ns;
-        for (int q = 0; q < ns; q++) J.seg[q] = s[q];
+        param_shape(P, pidx, r, c);
+        RJob &J = R.j[R.n];
+        J.dst = grads[pidx]; J.rows = r; J.cols = bias ? 0 : c; J.rowpad0 = rowpad0; J.nseg = ns;
+        for (int q = 0; q < ns; q++) J.seg[q] = sg[q];
         J.slab_base = L.slab_base; J.ktiles = L.ktiles;
-        hipLaunchKernelGGL(k_dw_reduce, dim3(div_up(r * c, 256)), dim3(256), 0, stream, J, NSPLIT, slabs);
-        RJob B = J;
-        B.dst = grads[pb]; B.cols = 0;
-        hipLaunchKernelGGL(k_dw_reduce, dim3(div_up(r, 256)), dim3(256), 0, stream, B, NSPLIT, slabs);
-        return 0;
+        R.begin[R.n] = total;
+        total += bias ? r : r * c;
+        R.n++;
     };
+    for (int i = 0; i < 8; i++) {
+        Seg sg[3];
+        int ns = layer_in_segs(F, i, sg);
+        add(P.pLw[i], 0, ns, sg, W.layers[i], false);
+        add(P.pLb[i], 0, ns, sg, W.layers[i], true);
+    }
     {
-        ScopedTimer tm("mlp_dw_reduce", stream);
-        for (int i = 0; i < 8; i++) {
-            Seg s[3];
-            int ns = layer_in_segs(F, i, s);
-            reduce(P.pLw[i], P.pLb[i], W.layers[i], 0, ns, s);
-        }
         Seg full = seg(0, 256, 0);
         int r0 = 0;
-        for (int h = 0; h < P.nheads; h++) {
-            reduce(P.pHw[h], P.pHb[h], W.layers[8], r0, 1, &full);
-            r0 += P.hrows[h];
+        for (int hh = 0; hh < P.nheads; hh++) {
+            add(P.pHw[hh], r0, 1, &full, W.layers[8], false);
+            add(P.pHb[hh], r0, 1, &full, W.layers[8], true);
+            r0 += P.hrows[hh];
         }
         if (F.blender) {
             Seg st = seg(0, F.tin, 0);
-            reduce(P.pT0w, P.pT0b, W.layers[9], 0, 1, &st);
-            reduce(P.pT2w, P.pT2b, W.layers[10], 0, 1, &full);
+            add(P.pT0w, 0, 1, &st, W.layers[9], false);
+            add(P.pT0b, 0, 1, &st, W.layers[9], true);
+            add(P.pT2w, 0, 1, &full, W.layers[10], false);
+            add(P.pT2b, 0, 1, &full, W.layers[10], true);
         }
+    }
+    R.begin[R.n] = total;
+    {
+        ScopedTimer tm("mlp_dw_reduce", stream);
+        hipLaunchKernelGGL(k_dw_reduce, dim3(div_up(total, 256)), dim3(256), 0, stream, R, NSPLIT, slabs);
     }
     DGS_LAUNCH_CHECK("k_dw_reduce", false, stream);
     return DGS_OK;

@@ -46,6 +46,9 @@ _SIGS = {
     "dgs_deform_backward": ([I, I, P, P, P, P, P, P], I),
     "dgs_deform_outputs": ([I], I),
     "dgs_knn_dist2": ([I, P, P, P], I),
+    "dgs_l1_ssim_scratch_floats": ([I, I, I], SZ),
+    "dgs_l1_ssim_forward": ([I, I, I, P, P, F, P, P, P], I),
+    "dgs_l1_ssim_backward": ([I, I, I, P, P, F, P, P, P, P], I),
 }
 
 EXPORTED = tuple(_SIGS)

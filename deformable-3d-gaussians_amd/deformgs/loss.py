@@ -57,3 +57,45 @@ def _ssim(img1, img2, window, window_size, channel, size_average=True):
 def psnr(img1, img2):
     mse = ((img1 - img2) ** 2).view(img1.shape[0], -1).mean(1, keepdim=True)
     return 20 * torch.log10(1.0 / torch.sqrt(mse))
+
+
+# ---- fused HIP path (libdgs_hip: dgs_l1_ssim_*) used by the training step ----
+class _FusedL1SSIM(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, img, gt, lambda_dssim):
+        from . import _lib
+        lib = _lib.load()
+        img = img.float().contiguous()
+        gt = gt.float().contiguous()
+        _lib.require_cuda(img, gt)
+        C, H, W = img.shape[-3:]
+        scratch = torch.empty(lib.dgs_l1_ssim_scratch_floats(C, H, W), dtype=torch.float32, device=img.device)
+        out = torch.empty(3, dtype=torch.float32, device=img.device)
+        _lib.check(lib.dgs_l1_ssim_forward(C, H, W, _lib.ptr(img), _lib.ptr(gt), float(lambda_dssim), _lib.ptr(out),
+                                           _lib.ptr(scratch), _lib.stream_ptr(img.device)), "l1_ssim_forward")
+        ctx.save_for_backward(img, gt, scratch)
+        ctx.lam = float(lambda_dssim)
+        loss, l1, s = out[0], out[1], out[2]
+        ctx.mark_non_differentiable(l1, s)
+        return loss, l1, s
+
+    @staticmethod
+    def backward(ctx, dloss, dl1, dssim):
+        from . import _lib
+        img, gt, scratch = ctx.saved_tensors
+        C, H, W = img.shape[-3:]
+        grad = torch.empty_like(img)
+        dl = dloss.float().contiguous()
+        _lib.check(_lib.load().dgs_l1_ssim_backward(C, H, W, _lib.ptr(img), _lib.ptr(gt), ctx.lam, _lib.ptr(scratch),
+                                                    _lib.ptr(dl), _lib.ptr(grad), _lib.stream_ptr(img.device)),
+                   "l1_ssim_backward")
+        return grad, None, None
+
+
+def l1_ssim_loss(image, gt, lambda_dssim=0.2):
+    """(1-l)*l1_loss + l*(1-ssim) of train_baseline.py:126-127 in one fused HIP kernel pair.
+    Returns (loss, Ll1, ssim_value); only `loss` carries a gradient (w.r.t. image)."""
+    if gt.requires_grad and torch.is_grad_enabled():
+        raise NotImplementedError("fused L1+SSIM differentiates w.r.t. the rendered image only")
+    loss, l1, s = _FusedL1SSIM.apply(image, gt.detach(), lambda_dssim)
+    return loss, l1, s

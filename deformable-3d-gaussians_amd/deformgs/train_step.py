@@ -3,7 +3,7 @@ harness): deform -> render -> 0.8*L1 + 0.2*(1-SSIM) -> backward [-> grad all-red
 """
 import torch
 
-from .loss import l1_loss, ssim
+from .loss import l1_ssim_loss
 from .renderer import render
 
 
@@ -18,8 +18,8 @@ def forward_backward(gaussians, deform, cam, gt_image, pipe, background, is_6dof
         d_xyz, d_rotation, d_scaling = deform.step(gaussians.get_xyz.detach(), time_input + ast_noise)
     pkg = render(cam, gaussians, pipe, background, d_xyz, d_rotation, d_scaling, is_6dof)
     image = pkg["render"]
-    Ll1 = l1_loss(image, gt_image)
-    loss = (1.0 - lambda_dssim) * Ll1 + lambda_dssim * (1.0 - ssim(image, gt_image))
+    # (1-l)*l1_loss(image, gt) + l*(1-ssim(image, gt)) (train_baseline.py:126-127), fused HIP kernels
+    loss, Ll1, _ = l1_ssim_loss(image, gt_image, lambda_dssim)
     loss.backward()
     return loss, pkg
 

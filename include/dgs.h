@@ -17,6 +17,7 @@
  *   dgs_deform_*         <- DeformNetworkBaseline.forward / autograd backward
  *                           (utils/time_utils.py:56-127, called via scene/deform_model.py:323-324)
  *   dgs_knn_dist2        <- simple_knn._C.distCUDA2 (scene/gaussian_model.py:20,105-106)
+ *   dgs_l1_ssim_*        <- l1_loss + ssim (utils/loss_utils.py:18-73) as used at train_baseline.py:126-127
  */
 #ifndef DGS_H
 #define DGS_H
@@ -115,6 +116,16 @@ int dgs_deform_forward(int flags, int N, const float *xyz, const float *t, const
 int dgs_deform_backward(int flags, int N, const float *packed, const float *saved, const float *dout,
                         float *scratch, float *const *grads, void *stream);
 int dgs_deform_outputs(int flags);
+
+/* ---- fused photometric loss (utils/loss_utils.py:18-73, train_baseline.py:126-127) ----
+ * img, gt: (C,H,W). out3 (device) = [loss, mean L1, mean SSIM] with
+ * loss = (1-lambda) * L1 + lambda * (1 - SSIM). scratch: dgs_l1_ssim_scratch_floats floats, kept
+ * from forward for backward. dloss (device scalar, may be NULL = 1) scales dL/dimg. */
+size_t dgs_l1_ssim_scratch_floats(int C, int H, int W);
+int dgs_l1_ssim_forward(int C, int H, int W, const float *img, const float *gt, float lambda, float *out3,
+                        float *scratch, void *stream);
+int dgs_l1_ssim_backward(int C, int H, int W, const float *img, const float *gt, float lambda,
+                         const float *scratch, const float *dloss, float *grad, void *stream);
 
 /* ---- simple-knn replacement: mean squared distance to the 3 nearest neighbours ---- */
 int dgs_knn_dist2(int P, const float *points, float *dist2, void *stream);

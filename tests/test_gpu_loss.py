@@ -1,0 +1,39 @@
+"""Fused HIP L1+SSIM (dgs_l1_ssim_*) vs the reference's own loss (golden) and the torch mirror.
+Tolerance: loss / L1 / SSIM values to 1e-6 abs; dL/dimg to 1e-6 relative to its max (fp32 sums in a
+different order than MIOpen's conv)."""
+import numpy as np
+import pytest
+import torch
+
+from deformgs.loss import l1_loss, l1_ssim_loss, ssim
+
+pytestmark = pytest.mark.gpu
+
+
+def test_fused_loss_golden(golden_dir):
+    f = np.load(f"{golden_dir}/loss.npz")
+    img = torch.from_numpy(f["img1"]).cuda().requires_grad_(True)
+    gt = torch.from_numpy(f["img2"]).cuda()
+    loss, l1, s = l1_ssim_loss(img, gt, 0.2)
+    assert abs(l1.item() - float(f["l1"])) < 1e-6
+    assert abs(s.item() - float(f["ssim"])) < 1e-6
+    assert abs(loss.item() - float(f["loss"])) < 1e-6
+    loss.backward()
+    g = img.grad.cpu().numpy()
+    assert np.abs(g - f["grad"]).max() <= 1e-5 * np.abs(f["grad"]).max()
+
+
+@pytest.mark.parametrize("shape", [(3, 800, 800), (3, 61, 83), (1, 16, 16), (3, 5, 200)])
+def test_fused_loss_vs_torch(shape):
+    torch.manual_seed(0)
+    a = torch.rand(shape, device="cuda")
+    b = torch.rand(shape, device="cuda")
+    x1 = a.clone().requires_grad_(True)
+    ref = 0.8 * l1_loss(x1, b) + 0.2 * (1.0 - ssim(x1, b))
+    (3.0 * ref).backward()
+    x2 = a.clone().requires_grad_(True)
+    loss, _, _ = l1_ssim_loss(x2, b, 0.2)
+    (3.0 * loss).backward()
+    assert abs(loss.item() - ref.item()) < 2e-6
+    gr, gg = x1.grad.cpu().numpy(), x2.grad.cpu().numpy()
+    assert np.abs(gr - gg).max() <= 1e-5 * np.abs(gr).max()
