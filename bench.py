@@ -71,11 +71,15 @@ def kernel_algorithmic(name, N, P, HW):
         return 20.0 * N + 12.0 * P, "byte", "hbm"
     if name == "ranges":
         return 8.0 * P, "byte", "hbm"
+    if name == "ssim_fwd":
+        return 3 * HW * (4 + 4 + 12), "byte", "hbm"
+    if name == "ssim_bwd":
+        return 3 * HW * (4 + 4 + 12 + 4), "byte", "hbm"
     return None
 
 
 KERNEL_CLASSES = ["mlp_fwd", "mlp_bwd", "mlp_dw", "mlp_dw_reduce", "preprocess_fwd", "duplicate", "sort", "ranges",
-                  "blend_fwd", "blend_bwd", "preprocess_bwd"]
+                  "blend_fwd", "blend_bwd", "preprocess_bwd", "ssim_fwd", "ssim_bwd"]
 
 
 def cpu_baseline(N, res, steps):

@@ -107,7 +107,12 @@ class _RasterizeGaussians(torch.autograd.Function):
             raise Exception("Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!")
         _lib.require_cuda(means3D, opacities, shs, colors_precomp, scales, rotations, cov3D_precomp)
         P = means3D.shape[0]
-        M = 0 if shs is None else shs.reshape(P, -1, 3).shape[1]
+        if shs is None:
+            M = 0
+        elif shs.dim() == 3:
+            M = shs.shape[1]
+        else:
+            M = shs.numel() // (3 * P) if P else 0
         H, W = int(raster_settings.image_height), int(raster_settings.image_width)
         dev = means3D.device
         color = torch.empty((3, H, W), dtype=torch.float32, device=dev)
