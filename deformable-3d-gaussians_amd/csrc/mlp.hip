@@ -286,17 +286,28 @@ __device__ inline f32x16 zero16() {
 
 #define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_32x32x2f32((a), (b), (c), 0, 0, 0)
 
-// acc0/acc1 (m-tiles 0/1) += A[ntile] . X over chunks [c0, c1) of the LDS image starting at group g0
+struct NoSide {
+    __device__ void operator()(int) const {}
+};
+
+// acc0/acc1 (m-tiles 0/1) += A[ntile] . X over chunks [c0, c1) of the LDS image starting at group g0.
+// The A fragments (1 KiB per wave-load) are prefetched two chunks ahead; side(i) runs once per chunk
+// (interleaved LDS->HBM stores of the previous layer's activations).
+template <class Side = NoSide>
 __device__ inline void gemm_2m(const float4 *__restrict__ Apk, int c0, int c1, const float4 *lds, int g0, int lane,
-                               f32x16 &acc0, f32x16 &acc1) {
+                               f32x16 &acc0, f32x16 &acc1, Side side = Side()) {
     const int h = lane >> 5, m = lane & 31;
-    float4 a_next = (c0 < c1) ? Apk[c0 * 64 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 p0 = (c0 < c1) ? Apk[c0 * 64 + lane] : z4;
+    float4 p1 = (c0 + 1 < c1) ? Apk[(c0 + 1) * 64 + lane] : z4;
     for (int c = c0; c < c1; c++) {
-        float4 a = a_next;
-        if (c + 1 < c1) a_next = Apk[(c + 1) * 64 + lane];
+        float4 a = p0;
+        p0 = p1;
+        if (c + 2 < c1) p1 = Apk[(c + 2) * 64 + lane];
         const float4 *grp = lds + (g0 + 2 * c + h) * BM;
         float4 b0 = grp[m];
         float4 b1 = grp[32 + m];
+        side(c - c0);
         acc0 = MFMA(a.x, b0.x, acc0);
         acc1 = MFMA(a.x, b1.x, acc1);
         acc0 = MFMA(a.y, b0.y, acc0);
@@ -309,20 +320,77 @@ __device__ inline void gemm_2m(const float4 *__restrict__ Apk, int c0, int c1, c
 }
 
 // single m-tile variant (narrow K-split layers)
+template <class Side = NoSide>
 __device__ inline void gemm_1m(const float4 *__restrict__ Apk, int c0, int c1, const float4 *lds, int g0, int mt,
-                               int lane, f32x16 &acc) {
+                               int lane, f32x16 &acc, Side side = Side()) {
     const int h = lane >> 5, m = lane & 31;
-    float4 a_next = (c0 < c1) ? Apk[c0 * 64 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 p0 = (c0 < c1) ? Apk[c0 * 64 + lane] : z4;
+    float4 p1 = (c0 + 1 < c1) ? Apk[(c0 + 1) * 64 + lane] : z4;
     for (int c = c0; c < c1; c++) {
-        float4 a = a_next;
-        if (c + 1 < c1) a_next = Apk[(c + 1) * 64 + lane];
+        float4 a = p0;
+        p0 = p1;
+        if (c + 2 < c1) p1 = Apk[(c + 2) * 64 + lane];
         float4 b = lds[(g0 + 2 * c + h) * BM + mt * 32 + m];
+        side(c - c0);
         acc = MFMA(a.x, b.x, acc);
         acc = MFMA(a.y, b.y, acc);
         acc = MFMA(a.z, b.z, acc);
         acc = MFMA(a.w, b.w, acc);
     }
 }
+
+// Deferred LDS -> HBM copy of up to two group ranges (activation rows [row0, row0 + 4ng) of a
+// feature-major [rows][Ns] array), issued a few float4 units per thread per GEMM chunk so the stores
+// drain under the next layer's MFMAs instead of in a store-only phase. Unit = 4 features x 1 point:
+// ds_read_b128 + 4 coalesced 256-B wave stores. Every range is a multiple of NTHR units.
+struct Pending {
+    int g0a, nga, r0a, g0b, r0b;  // range a (and optional range b, placed after a)
+    int n, units, pos, per;
+    __device__ void set1(int g, int ngr, int r0) {
+        n = 1; g0a = g; nga = ngr; r0a = r0;
+        units = ngr * BM / NTHR; pos = 0;
+    }
+    __device__ void add(int g, int ngr, int r0) {
+        if (n == 0) { set1(g, ngr, r0); return; }
+        g0b = g; r0b = r0; n = 2;
+        units += ngr * BM / NTHR;
+    }
+    __device__ void pace(int chunks) { per = chunks > 0 ? (units - pos + chunks - 1) / chunks : units - pos; }
+};
+
+struct PendingSide {
+    Pending *q;
+    const float4 *lds;
+    float *dst;
+    size_t Ns;
+    int p0, tid;
+    __device__ void unit() const {
+        Pending &Q = *q;
+        if (Q.pos >= Q.units) return;
+        int e = tid + NTHR * Q.pos;
+        Q.pos++;
+        const bool second = Q.n > 1 && e >= Q.nga * BM;
+        if (second) e -= Q.nga * BM;
+        const int g0 = second ? Q.g0b : Q.g0a;
+        const int r0 = second ? Q.r0b : Q.r0a;
+        const int gi = e / BM, m = e % BM;
+        float4 v = lds[(g0 + gi) * BM + m];
+        float *d = dst + (size_t)(r0 + 4 * gi) * Ns + p0 + m;
+        d[0] = v.x;
+        d[Ns] = v.y;
+        d[2 * Ns] = v.z;
+        d[3 * Ns] = v.w;
+    }
+    __device__ void operator()(int) const {
+        for (int k = 0; k < q->per; k++) unit();
+    }
+    __device__ void flush() const {
+        while (q->pos < q->units) unit();
+        q->n = 0;
+        q->units = q->pos = 0;
+    }
+};
 
 // accumulator (n-tile base n0, m-tile mt) -> LDS groups starting at gout, with bias/relu
 __device__ inline void acc_to_lds(const f32x16 &acc, float4 *lds, int gout, int n0, int mt, int lane,
@@ -371,12 +439,13 @@ struct FwdArgs {
 
 // narrow layer: 1 output n-tile, K split over 8 waves (4 quarters x 2 m-tiles), fixed-order sum,
 // result (+bias) written to LDS groups gout..gout+7 (32 features)
+template <class Side = NoSide>
 __device__ inline void narrow_layer(const float4 *Apk, int nchunks, float4 *lds, int g0, int gout, const float *bias,
-                                    int wave, int lane, int tid) {
+                                    int wave, int lane, int tid, Side side = Side()) {
     const int mt = wave & 1, q = wave >> 1;
     const int per = nchunks / 4;
     f32x16 acc = zero16();
-    gemm_1m(Apk, q * per, (q + 1) * per, lds, g0, mt, lane, acc);
+    gemm_1m(Apk, q * per, (q + 1) * per, lds, g0, mt, lane, acc, side);
     // partial -> PART region slot q (8 groups per slot)
     acc_to_lds(acc, lds, G_PART + 8 * q, 0, mt, lane, nullptr, false);
     __syncthreads();
@@ -446,37 +515,50 @@ __global__ __launch_bounds__(NTHR) void k_mlp_fwd(FwdArgs a) {
         }
     }
     __syncthreads();
+    // saved activations leave LDS under the following GEMMs (Pending); nothing is stored when
+    // a.saved == nullptr (inference)
+    Pending pend;
+    pend.n = 0; pend.units = 0; pend.pos = 0; pend.per = 0; pend.nga = 0;
+    PendingSide side{&pend, lds, a.saved, a.Ns, p0, tid};
     if (a.saved) {
-        lds_to_global(lds, G_XE, 16, a.saved, S_XE, a.Ns, p0, tid);
-        if (F.blender) lds_to_global(lds, G_TIN, 4, a.saved, S_TIN, a.Ns, p0, tid);
-        else lds_to_global(lds, G_TE, 8, a.saved, S_TE, a.Ns, p0, tid);
+        pend.set1(G_XE, 16, S_XE);
+        if (F.blender) pend.add(G_TIN, 4, S_TIN);
+        else pend.add(G_TE, 8, S_TE);
     }
     const float *bias = a.packed;
     // ---- timenet (blender): Linear(13,256) + ReLU -> H ; Linear(256,30) -> TE ----
     if (F.blender) {
         f32x16 c0 = zero16(), c1 = zero16();
-        gemm_2m(pk + a.fT1 / 4 + wave * 2 * 64, 0, 2, lds, G_TIN, lane, c0, c1);
+        pend.pace(2);
+        gemm_2m(pk + a.fT1 / 4 + wave * 2 * 64, 0, 2, lds, G_TIN, lane, c0, c1, side);
         acc_to_lds(c0, lds, G_H, wave * 32, 0, lane, bias + a.bT1, true);
         acc_to_lds(c1, lds, G_H, wave * 32, 1, lane, bias + a.bT1, true);
         __syncthreads();
-        if (a.saved) lds_to_global(lds, G_H, 64, a.saved, S_TH, a.Ns, p0, tid);
-        narrow_layer(pk + a.fT2 / 4, 32, lds, G_H, G_TE, bias + a.bT2, wave, lane, tid);
-        if (a.saved) lds_to_global(lds, G_TE, 8, a.saved, S_TE, a.Ns, p0, tid);
+        side.flush();
+        if (a.saved) pend.set1(G_H, 64, S_TH);
+        pend.pace(8);
+        narrow_layer(pk + a.fT2 / 4, 32, lds, G_H, G_TE, bias + a.bT2, wave, lane, tid, side);
+        side.flush();
+        if (a.saved) pend.set1(G_TE, 8, S_TE);
     }
     // ---- trunk: 8 x (Linear + ReLU), skip cat after layer 4 (time_utils.py:107-112) ----
     for (int L = 0; L < 8; L++) {
         const int g0 = (L == 0 || L == 5) ? G_XE : G_H;
         const int nch = layer_kpad(L) / 8;
         f32x16 c0 = zero16(), c1 = zero16();
-        gemm_2m(pk + a.fL[L] / 4 + wave * nch * 64, 0, nch, lds, g0, lane, c0, c1);
+        pend.pace(nch);
+        gemm_2m(pk + a.fL[L] / 4 + wave * nch * 64, 0, nch, lds, g0, lane, c0, c1, side);
+        side.flush();
         __syncthreads();  // all waves finished reading H before it is overwritten
         acc_to_lds(c0, lds, G_H, wave * 32, 0, lane, bias + a.bL[L], true);
         acc_to_lds(c1, lds, G_H, wave * 32, 1, lane, bias + a.bL[L], true);
         __syncthreads();
-        if (a.saved) lds_to_global(lds, G_H, 64, a.saved, s_h(L), a.Ns, p0, tid);
+        if (a.saved) pend.set1(G_H, 64, s_h(L));
     }
+    pend.pace(8);
     // ---- heads (no activation): [warp | branch_w, branch_v], rotation, scaling -> TE region ----
-    narrow_layer(pk + a.fHd / 4, 32, lds, G_H, G_TE, bias + a.bHd, wave, lane, tid);
+    narrow_layer(pk + a.fHd / 4, 32, lds, G_H, G_TE, bias + a.bHd, wave, lane, tid, side);
+    side.flush();
     for (int e = tid; e < F.nout * BM; e += NTHR) {
         int c = e % F.nout, m = e / F.nout;
         int p = p0 + m;
@@ -500,20 +582,38 @@ struct BwdArgs {
 
 // wide transposed layer: out n-tile = wave (rows [32w, 32w+32) of the 256-feature output),
 // reading K from LDS groups g0.., masked by saved activations (relu'), written to LDS H + global dZ
-__device__ inline void mask_store(f32x16 &acc, const float *__restrict__ saved_rows, float *__restrict__ dz_rows,
-                                  size_t Ns, int p0, int mt, int lane, int n0) {
+struct Mask16 {
+    float v[16];
+};
+
+// relu' mask rows of one 32x32 accumulator tile, loaded ahead of the GEMM that needs them
+__device__ inline void mask_load(Mask16 &mk, const float *__restrict__ saved_rows, size_t Ns, int p0, int mt, int lane,
+                                 int n0) {
     const int h = lane >> 5, m = lane & 31;
-    const size_t base = (size_t)(n0 + 4 * h) * Ns + p0 + mt * 32 + m;
-    const float *sv = saved_rows + base;
-    float *dz = dz_rows + base;
+    const float *sv = saved_rows + (size_t)(n0 + 4 * h) * Ns + p0 + mt * 32 + m;
     const int ns = (int)Ns;  // a 32-row tile spans < 2^31 floats
 #pragma unroll
+    for (int r = 0; r < 16; r++) mk.v[r] = sv[(8 * (r >> 2) + (r & 3)) * ns];
+}
+
+__device__ inline void mask_apply_store(f32x16 &acc, const Mask16 &mk, float *__restrict__ dz_rows, size_t Ns, int p0,
+                                        int mt, int lane, int n0) {
+    const int h = lane >> 5, m = lane & 31;
+    float *dz = dz_rows + (size_t)(n0 + 4 * h) * Ns + p0 + mt * 32 + m;
+    const int ns = (int)Ns;
+#pragma unroll
     for (int r = 0; r < 16; r++) {
-        const int o = (8 * (r >> 2) + (r & 3)) * ns;
-        float v = sv[o] > 0.f ? acc[r] : 0.f;
+        float v = mk.v[r] > 0.f ? acc[r] : 0.f;
         acc[r] = v;
-        dz[o] = v;
+        dz[(8 * (r >> 2) + (r & 3)) * ns] = v;
     }
+}
+
+__device__ inline void mask_store(f32x16 &acc, const float *__restrict__ saved_rows, float *__restrict__ dz_rows,
+                                  size_t Ns, int p0, int mt, int lane, int n0) {
+    Mask16 mk;
+    mask_load(mk, saved_rows, Ns, p0, mt, lane, n0);
+    mask_apply_store(acc, mk, dz_rows, Ns, p0, mt, lane, n0);
 }
 
 __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
@@ -555,10 +655,13 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
             gemm_1m(pk + a.tL[5] / 4 + (F_TE / 32) * 32 * 64, q * 8, q * 8 + 8, lds, G_H, mt, lane, ct);
             acc_to_lds(ct, lds, G_PART + 8 * q, 0, mt, lane, nullptr, false);
         }
+        Mask16 mk0, mk1;  // relu' of H_{L-1}, in flight during the GEMM
+        mask_load(mk0, a.saved + (size_t)s_h(L - 1) * a.Ns, a.Ns, p0, 0, lane, wave * 32);
+        mask_load(mk1, a.saved + (size_t)s_h(L - 1) * a.Ns, a.Ns, p0, 1, lane, wave * 32);
         f32x16 c0 = zero16(), c1 = zero16();
         gemm_2m(pk + a.tL[L] / 4 + (tile0 + wave) * 32 * 64, 0, 32, lds, G_H, lane, c0, c1);
-        mask_store(c0, a.saved + (size_t)s_h(L - 1) * a.Ns, a.dz + (size_t)(Z_L0 + (L - 1) * 256) * a.Ns, a.Ns, p0, 0, lane, wave * 32);
-        mask_store(c1, a.saved + (size_t)s_h(L - 1) * a.Ns, a.dz + (size_t)(Z_L0 + (L - 1) * 256) * a.Ns, a.Ns, p0, 1, lane, wave * 32);
+        mask_apply_store(c0, mk0, a.dz + (size_t)(Z_L0 + (L - 1) * 256) * a.Ns, a.Ns, p0, 0, lane, wave * 32);
+        mask_apply_store(c1, mk1, a.dz + (size_t)(Z_L0 + (L - 1) * 256) * a.Ns, a.Ns, p0, 1, lane, wave * 32);
         __syncthreads();
         if (L == 5 && F.blender) {
             for (int e = tid; e < 8 * BM; e += NTHR) {
