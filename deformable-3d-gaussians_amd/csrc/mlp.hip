@@ -298,12 +298,16 @@ __device__ inline void gemm_2m(const float4 *__restrict__ Apk, int c0, int c1, c
                                f32x16 &acc0, f32x16 &acc1, Side side = Side()) {
     const int h = lane >> 5, m = lane & 31;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 p0 = (c0 < c1) ? Apk[c0 * 64 + lane] : z4;
-    float4 p1 = (c0 + 1 < c1) ? Apk[(c0 + 1) * 64 + lane] : z4;
-    for (int c = c0; c < c1; c++) {
-        float4 a = p0;
-        p0 = p1;
-        if (c + 2 < c1) p1 = Apk[(c + 2) * 64 + lane];
+    // 4-deep register ring of A fragments: a fragment is waited for 4 chunks (~2k cycles) after
+    // its load was issued, so the interleaved activation stores (which share vmcnt with the loads
+    // on CDNA4) issued before it have long drained.
+    float4 r0 = (c0 < c1) ? Apk[c0 * 64 + lane] : z4;
+    float4 r1 = (c0 + 1 < c1) ? Apk[(c0 + 1) * 64 + lane] : z4;
+    float4 r2 = (c0 + 2 < c1) ? Apk[(c0 + 2) * 64 + lane] : z4;
+    float4 r3 = (c0 + 3 < c1) ? Apk[(c0 + 3) * 64 + lane] : z4;
+    auto step = [&](int c, float4 &slot) {
+        float4 a = slot;
+        if (c + 4 < c1) slot = Apk[(c + 4) * 64 + lane];
         const float4 *grp = lds + (g0 + 2 * c + h) * BM;
         float4 b0 = grp[m];
         float4 b1 = grp[32 + m];
@@ -316,7 +320,17 @@ __device__ inline void gemm_2m(const float4 *__restrict__ Apk, int c0, int c1, c
         acc1 = MFMA(a.z, b1.z, acc1);
         acc0 = MFMA(a.w, b0.w, acc0);
         acc1 = MFMA(a.w, b1.w, acc1);
+    };
+    int c = c0;
+    for (; c + 4 <= c1; c += 4) {
+        step(c, r0);
+        step(c + 1, r1);
+        step(c + 2, r2);
+        step(c + 3, r3);
     }
+    if (c < c1) step(c, r0);
+    if (c + 1 < c1) step(c + 1, r1);
+    if (c + 2 < c1) step(c + 2, r2);
 }
 
 // single m-tile variant (narrow K-split layers)
@@ -347,14 +361,17 @@ __device__ inline void gemm_1m(const float4 *__restrict__ Apk, int c0, int c1, c
 struct Pending {
     int g0a, nga, r0a, g0b, r0b;  // range a (and optional range b, placed after a)
     int n, units, pos, per;
+    int total;  // float4 units over all ranges (per-thread rounds = ceil(total / NTHR))
     __device__ void set1(int g, int ngr, int r0) {
         n = 1; g0a = g; nga = ngr; r0a = r0;
-        units = ngr * BM / NTHR; pos = 0;
+        total = ngr * BM;
+        units = div_up(total, NTHR); pos = 0;
     }
     __device__ void add(int g, int ngr, int r0) {
         if (n == 0) { set1(g, ngr, r0); return; }
         g0b = g; r0b = r0; n = 2;
-        units += ngr * BM / NTHR;
+        total += ngr * BM;
+        units = div_up(total, NTHR);
     }
     __device__ void pace(int chunks) { per = chunks > 0 ? (units - pos + chunks - 1) / chunks : units - pos; }
 };
@@ -370,6 +387,7 @@ struct PendingSide {
         if (Q.pos >= Q.units) return;
         int e = tid + NTHR * Q.pos;
         Q.pos++;
+        if (e >= Q.total) return;
         const bool second = Q.n > 1 && e >= Q.nga * BM;
         if (second) e -= Q.nga * BM;
         const int g0 = second ? Q.g0b : Q.g0a;
@@ -388,7 +406,7 @@ struct PendingSide {
     __device__ void flush() const {
         while (q->pos < q->units) unit();
         q->n = 0;
-        q->units = q->pos = 0;
+        q->units = q->pos = q->total = 0;
     }
 };
 
@@ -518,7 +536,7 @@ __global__ __launch_bounds__(NTHR) void k_mlp_fwd(FwdArgs a) {
     // saved activations leave LDS under the following GEMMs (Pending); nothing is stored when
     // a.saved == nullptr (inference)
     Pending pend;
-    pend.n = 0; pend.units = 0; pend.pos = 0; pend.per = 0; pend.nga = 0;
+    pend.n = 0; pend.units = 0; pend.pos = 0; pend.per = 0; pend.nga = 0; pend.total = 0;
     PendingSide side{&pend, lds, a.saved, a.Ns, p0, tid};
     if (a.saved) {
         pend.set1(G_XE, 16, S_XE);

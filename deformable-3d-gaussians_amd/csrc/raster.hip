@@ -693,19 +693,20 @@ extern "C" int dgs_raster_forward(const dgs_raster_settings *s, int P, int M, co
                                   float *out_color, float *out_depth, int *out_radii, dgs_raster_ctx **ctx_out,
                                   int *num_rendered, void *stream_) {
     hipStream_t stream = (hipStream_t)stream_;
-    if (!s || !ctx_out || P < 0 || !out_color || !out_depth || !out_radii || (P > 0 && (!means3D || !opacities))) {
+    if (!s || !ctx_out || P < 0 || !out_color || !out_depth || (P > 0 && (!means3D || !opacities || !out_radii))) {
         set_error("dgs_raster_forward: null argument");
         return DGS_ERR_ARGS;
     }
-    if ((shs == nullptr) == (colors_precomp == nullptr)) {
+    // (an empty point set has null data pointers everywhere: nothing to validate)
+    if (P > 0 && (shs == nullptr) == (colors_precomp == nullptr)) {
         set_error("Please provide exactly one of either SHs or precomputed colors!");
         return DGS_ERR_ARGS;
     }
-    if (cov3D_precomp == nullptr && (scales == nullptr || rotations == nullptr)) {
+    if (P > 0 && cov3D_precomp == nullptr && (scales == nullptr || rotations == nullptr)) {
         set_error("Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
         return DGS_ERR_ARGS;
     }
-    if (shs && (M < 1 || M < (s->sh_degree + 1) * (s->sh_degree + 1) || s->sh_degree > 3)) {
+    if (P > 0 && shs && (M < 1 || M < (s->sh_degree + 1) * (s->sh_degree + 1) || s->sh_degree > 3)) {
         set_error("dgs_raster_forward: SH degree/coefficient count unsupported (degree <= 3, M >= (D+1)^2)");
         return DGS_ERR_ARGS;
     }
@@ -822,7 +823,12 @@ extern "C" int dgs_raster_backward(dgs_raster_ctx *c, const float *dL_dcolor, co
                                    float *dL_dcolors, float *dL_dopacity, float *dL_dcov3D, float *dL_dshs,
                                    float *dL_dscales, float *dL_drotations, void *stream_) {
     hipStream_t stream = (hipStream_t)stream_;
-    if (!c || !dL_dcolor || !dL_dmeans3D || !dL_dmeans2D || !dL_dmeans2D_densify || !dL_dopacity) {
+    if (!c || !dL_dcolor) {
+        set_error("dgs_raster_backward: null argument");
+        return DGS_ERR_ARGS;
+    }
+    if (c->P == 0) return DGS_OK;
+    if (!dL_dmeans3D || !dL_dmeans2D || !dL_dmeans2D_densify || !dL_dopacity) {
         set_error("dgs_raster_backward: null argument");
         return DGS_ERR_ARGS;
     }
