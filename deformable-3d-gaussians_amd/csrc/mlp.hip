@@ -729,121 +729,169 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// dW = dZ X^T over all points (split-N MFMA GEMM into slabs) + fixed-order reduction
+// dW = dZ X^T over all points: one 256x256 tile per layer (L5: 256 + 96 input columns), split over
+// the point axis in proportion to each tile's work so ~one workgroup per CU finishes together;
+// fixed-order slab reduction (deterministic).
 // ------------------------------------------------------------------------------------------------
+constexpr int WT = 256;            // tile edge (rows of dZ, rows of X)
+constexpr int SLAB = WT * WT + WT; // tile + bias row sums
+constexpr int PC = 32;             // points per LDS chunk
+constexpr int LDA = PC + 4;        // padded LDS row (floats)
+constexpr int MAXJ = 12;
+constexpr int DW_THREADS = 512;    // 8 waves: 2 (n) x 4 (k), 128 x 64 per wave
+
+// component-wise select (a select of the float4 struct itself can be lowered through scratch)
+__device__ inline float4 zsel4(float4 v, bool ok) {
+    return make_float4(ok ? v.x : 0.f, ok ? v.y : 0.f, ok ? v.z : 0.f, ok ? v.w : 0.f);
+}
+
 struct WJob {
-    int zrow, nrows;   // dZ rows [zrow, zrow + nrows) (padded layer outputs)
-    int xrow, krows;   // X rows in saved
-    int tn, tk;        // tile index (128 x 128)
-    int slab;          // float offset of this tile's slab block (splits x (128*128 + 128))
+    int zrow, nrows;   // dZ rows [zrow, zrow + nrows) (padded layer outputs, <= 256)
+    int xrow, krows;   // X rows [xrow, xrow + krows) in saved (<= 256)
+    int nsplit;        // workgroups over the point axis
+    int block0;        // first workgroup (= first slab) of this job
+};
+struct WJobs {
+    WJob j[MAXJ];
+    int n;
 };
 
-constexpr int WT = 128;
-constexpr int SLAB = WT * WT + WT;
-constexpr int PC = 32;           // points per LDS chunk
-constexpr int LDA = PC + 4;      // padded LDS row (floats)
-
-// One 128x128 tile of dW (+ bias row sums) over a contiguous point range. 4 waves (2x2 of 64x64),
-// chunk of 32 points staged through double-buffered LDS: coalesced 128-B row loads for the next
-// chunk are issued before the MFMAs of the current one (register-staged, written after compute).
-__global__ __launch_bounds__(256) void k_dw(const WJob *__restrict__ jobs, int nsplit, size_t Ns, int chunks_per_split,
-                                            const float *__restrict__ dz, const float *__restrict__ saved,
-                                            float *__restrict__ slabs) {
-    __shared__ float4 lds4[2 * 2 * WT * LDA / 4];
-    float *ldsf = reinterpret_cast<float *>(lds4);
-    const WJob J = jobs[blockIdx.x / nsplit];
-    const int split = blockIdx.x % nsplit;
+__global__ __launch_bounds__(DW_THREADS) void k_dw(WJobs JT, size_t Ns, const float *__restrict__ dz,
+                                                   const float *__restrict__ saved, float *__restrict__ slabs) {
+    extern __shared__ float4 dw_lds[];
+    float *ldsf = reinterpret_cast<float *>(dw_lds);
+    // job of this workgroup: static-index selects over the kernel-argument table (no scratch copy)
+    WJob J = JT.j[0];
+#pragma unroll
+    for (int q = 1; q < MAXJ; q++)
+        if (q < JT.n && (int)blockIdx.x >= JT.j[q].block0) J = JT.j[q];
+    const int split = blockIdx.x - J.block0;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int wn = wave >> 1, wk = wave & 1;
+    const int wn = wave >> 2, wk = wave & 3;  // wave tile: rows [128 wn, +128), cols [64 wk, +64)
     const int h = lane >> 5, i = lane & 31;
-    const int nchunks_total = (int)(Ns / PC);
-    const int c0 = split * chunks_per_split;
-    const int c1 = min(nchunks_total, c0 + chunks_per_split);
-    // global staging map: element e = tid + 256*j (j < 4): row = e / 8, float4 column = e % 8
-    const float *srcA[4];
-    const float *srcB[4];
-    bool okA[4], okB[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        int e = tid + 256 * j;
-        int row = e >> 3, col = (e & 7) * 4;
-        int nr = J.tn * WT + row, kr = J.tk * WT + row;
-        okA[j] = nr < J.nrows;
-        okB[j] = kr < J.krows;
-        srcA[j] = dz + (size_t)(J.zrow + (okA[j] ? nr : 0)) * Ns + col;
-        srcB[j] = saved + (size_t)(J.xrow + (okB[j] ? kr : 0)) * Ns + col;
-    }
+    const int nch = (int)(Ns / PC);
+    const int per = div_up(nch, J.nsplit);
+    const int c0 = split * per;
+    const int c1 = min(nch, c0 + per);
+    // staging map: element e = tid + 512 j (j < 4): row = e / 8 (0..255), float4 column = e % 8
+    const float *baseA = dz + (size_t)J.zrow * Ns;
+    const float *baseB = saved + (size_t)J.xrow * Ns;
+    const int ns = (int)Ns;  // 256 rows x Ns < 2^31
+    const int srow = tid >> 3, scol = (tid & 7) * 4;
+#define DW_OFF(lim, j) ((srow + 64 * (j)) < (lim) ? (srow + 64 * (j)) * ns + scol : -1)
+    const int oA0 = DW_OFF(J.nrows, 0), oA1 = DW_OFF(J.nrows, 1), oA2 = DW_OFF(J.nrows, 2), oA3 = DW_OFF(J.nrows, 3);
+    const int oB0 = DW_OFF(J.krows, 0), oB1 = DW_OFF(J.krows, 1), oB2 = DW_OFF(J.krows, 2), oB3 = DW_OFF(J.krows, 3);
+#undef DW_OFF
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 ra[4], rb[4];
-    auto gload = [&](int c) {
-        const size_t po = (size_t)c * PC;
+    float4 ra0, ra1, ra2, ra3, rb0, rb1, rb2, rb3;
+    // rows past the job's extent load row 0 (always valid) and are zeroed after the load: an
+    // unconditional global_load keeps hipcc from turning `ok ? *p : 0` into a flat load of a
+    // pointer select between global memory and a scratch-held zero
+#define DW_LD(base, o, po) (*reinterpret_cast<const float4 *>((base) + ((o) >= 0 ? (o) : scol) + (po)))
+#define DW_Z(v, o) zsel4((v), (o) >= 0)
+#define DW_GLOAD(c)                                                                                        \
+    do {                                                                                                   \
+        const int po_ = (c) * PC;                                                                          \
+        ra0 = DW_LD(baseA, oA0, po_); ra1 = DW_LD(baseA, oA1, po_);                                        \
+        ra2 = DW_LD(baseA, oA2, po_); ra3 = DW_LD(baseA, oA3, po_);                                        \
+        rb0 = DW_LD(baseB, oB0, po_); rb1 = DW_LD(baseB, oB1, po_);                                        \
+        rb2 = DW_LD(baseB, oB2, po_); rb3 = DW_LD(baseB, oB3, po_);                                        \
+        ra0 = DW_Z(ra0, oA0); ra1 = DW_Z(ra1, oA1); ra2 = DW_Z(ra2, oA2); ra3 = DW_Z(ra3, oA3);            \
+        rb0 = DW_Z(rb0, oB0); rb1 = DW_Z(rb1, oB1); rb2 = DW_Z(rb2, oB2); rb3 = DW_Z(rb3, oB3);            \
+    } while (0)
+#define DW_LSTORE(buf)                                                                                     \
+    do {                                                                                                   \
+        float *A_ = ldsf + (buf) * (2 * WT * LDA);                                                         \
+        float *B_ = A_ + WT * LDA;                                                                         \
+        const int row_ = tid >> 3, col_ = (tid & 7) * 4;                                                   \
+        *reinterpret_cast<float4 *>(A_ + (row_ + 0) * LDA + col_) = ra0;                                   \
+        *reinterpret_cast<float4 *>(A_ + (row_ + 64) * LDA + col_) = ra1;                                  \
+        *reinterpret_cast<float4 *>(A_ + (row_ + 128) * LDA + col_) = ra2;                                 \
+        *reinterpret_cast<float4 *>(A_ + (row_ + 192) * LDA + col_) = ra3;                                 \
+        *reinterpret_cast<float4 *>(B_ + (row_ + 0) * LDA + col_) = rb0;                                   \
+        *reinterpret_cast<float4 *>(B_ + (row_ + 64) * LDA + col_) = rb1;                                  \
+        *reinterpret_cast<float4 *>(B_ + (row_ + 128) * LDA + col_) = rb2;                                 \
+        *reinterpret_cast<float4 *>(B_ + (row_ + 192) * LDA + col_) = rb3;                                 \
+    } while (0)
+    // this wave's active sub-tiles (wave-uniform): rows 128 wn + 32 t, cols 64 wk + 32 u
+    const int nact_r = min(4, max(0, div_up(J.nrows - 128 * wn, 32)));  // active 32-row sub-tiles
+    const int nact_c = min(2, max(0, div_up(J.krows - 64 * wk, 32)));   // active 32-col sub-tiles
+    const bool any = nact_r > 0 && nact_c > 0;
+    f32x16 acc[4][2];
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            ra[j] = okA[j] ? *reinterpret_cast<const float4 *>(srcA[j] + po) : z4;
-            rb[j] = okB[j] ? *reinterpret_cast<const float4 *>(srcB[j] + po) : z4;
-        }
-    };
-    auto lstore = [&](int buf) {
-        float *A = ldsf + buf * (2 * WT * LDA);
-        float *B = A + WT * LDA;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            int e = tid + 256 * j;
-            int row = e >> 3, col = (e & 7) * 4;
-            *reinterpret_cast<float4 *>(A + row * LDA + col) = ra[j];
-            *reinterpret_cast<float4 *>(B + row * LDA + col) = rb[j];
-        }
-    };
-    f32x16 c00 = zero16(), c01 = zero16(), c10 = zero16(), c11 = zero16();
-    float bs0 = 0.f, bs1 = 0.f;
+    for (int t = 0; t < 4; t++) {
+        acc[t][0] = zero16();
+        acc[t][1] = zero16();
+    }
+    float bs0 = 0.f, bs1 = 0.f, bs2 = 0.f, bs3 = 0.f;
     if (c0 < c1) {
-        gload(c0);
-        lstore(0);
+        DW_GLOAD(c0);
+        DW_LSTORE(0);
     }
     __syncthreads();
-    const int ra0 = wn * 64 + i, ra1 = ra0 + 32, rb0 = wk * 64 + i, rb1 = rb0 + 32;
     for (int c = c0; c < c1; c++) {
         const int buf = (c - c0) & 1;
         const bool more = c + 1 < c1;
-        if (more) gload(c + 1);
+        if (more) DW_GLOAD(c + 1);
         const float *A = ldsf + buf * (2 * WT * LDA);
         const float *B = A + WT * LDA;
+        if (any) {
 #pragma unroll
-        for (int g = 0; g < PC / 8; g++) {
-            const int o = 8 * g + 4 * h;
-            float4 a0 = *reinterpret_cast<const float4 *>(A + ra0 * LDA + o);
-            float4 a1 = *reinterpret_cast<const float4 *>(A + ra1 * LDA + o);
-            float4 b0 = *reinterpret_cast<const float4 *>(B + rb0 * LDA + o);
-            float4 b1 = *reinterpret_cast<const float4 *>(B + rb1 * LDA + o);
-            bs0 += (a0.x + a0.y) + (a0.z + a0.w);
-            bs1 += (a1.x + a1.y) + (a1.z + a1.w);
-            c00 = MFMA(a0.x, b0.x, c00); c01 = MFMA(a0.x, b1.x, c01); c10 = MFMA(a1.x, b0.x, c10); c11 = MFMA(a1.x, b1.x, c11);
-            c00 = MFMA(a0.y, b0.y, c00); c01 = MFMA(a0.y, b1.y, c01); c10 = MFMA(a1.y, b0.y, c10); c11 = MFMA(a1.y, b1.y, c11);
-            c00 = MFMA(a0.z, b0.z, c00); c01 = MFMA(a0.z, b1.z, c01); c10 = MFMA(a1.z, b0.z, c10); c11 = MFMA(a1.z, b1.z, c11);
-            c00 = MFMA(a0.w, b0.w, c00); c01 = MFMA(a0.w, b1.w, c01); c10 = MFMA(a1.w, b0.w, c10); c11 = MFMA(a1.w, b1.w, c11);
+            for (int g = 0; g < PC / 8; g++) {
+                const int o = 8 * g + 4 * h;
+                float4 a[4], bb[2];
+#pragma unroll
+                for (int t = 0; t < 4; t++) a[t] = *reinterpret_cast<const float4 *>(A + (128 * wn + 32 * t + i) * LDA + o);
+#pragma unroll
+                for (int u = 0; u < 2; u++) bb[u] = *reinterpret_cast<const float4 *>(B + (64 * wk + 32 * u + i) * LDA + o);
+                if (wk == 0) {
+                    bs0 += (a[0].x + a[0].y) + (a[0].z + a[0].w);
+                    bs1 += (a[1].x + a[1].y) + (a[1].z + a[1].w);
+                    bs2 += (a[2].x + a[2].y) + (a[2].z + a[2].w);
+                    bs3 += (a[3].x + a[3].y) + (a[3].z + a[3].w);
+                }
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    if (t >= nact_r) continue;
+#pragma unroll
+                    for (int u = 0; u < 2; u++) {
+                        if (u >= nact_c) continue;
+                        acc[t][u] = MFMA(a[t].x, bb[u].x, acc[t][u]);
+                        acc[t][u] = MFMA(a[t].y, bb[u].y, acc[t][u]);
+                        acc[t][u] = MFMA(a[t].z, bb[u].z, acc[t][u]);
+                        acc[t][u] = MFMA(a[t].w, bb[u].w, acc[t][u]);
+                    }
+                }
+            }
         }
-        if (more) lstore(buf ^ 1);
+        if (more) DW_LSTORE(buf ^ 1);
         __syncthreads();
     }
-    float *slab = slabs + J.slab + (size_t)split * SLAB;
-    auto store = [&](const f32x16 &c, int nb, int kb) {
+#undef DW_GLOAD
+#undef DW_LSTORE
+#undef DW_LD
+#undef DW_Z
+    float *slab = slabs + (size_t)blockIdx.x * SLAB;
 #pragma unroll
-        for (int r = 0; r < 16; r++) {
-            int n = nb + 8 * (r >> 2) + 4 * h + (r & 3);
-            slab[n * WT + kb + i] = c[r];
+    for (int t = 0; t < 4; t++)
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int nb = 128 * wn + 32 * t, kb = 64 * wk + 32 * u;
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                int n = nb + 8 * (r >> 2) + 4 * h + (r & 3);
+                slab[n * WT + kb + i] = acc[t][u][r];
+            }
         }
-    };
-    store(c00, wn * 64, wk * 64);
-    store(c01, wn * 64, wk * 64 + 32);
-    store(c10, wn * 64 + 32, wk * 64);
-    store(c11, wn * 64 + 32, wk * 64 + 32);
     if (wk == 0) {
-        // lanes l and l+32 hold the same row: combine halves, lane < 32 writes
-        bs0 += __shfl_xor(bs0, 32);
-        bs1 += __shfl_xor(bs1, 32);
+        // lanes l and l+32 hold the same row
+        float v0 = bs0 + __shfl_xor(bs0, 32), v1 = bs1 + __shfl_xor(bs1, 32);
+        float v2 = bs2 + __shfl_xor(bs2, 32), v3 = bs3 + __shfl_xor(bs3, 32);
         if (h == 0) {
-            slab[WT * WT + wn * 64 + i] = bs0;
-            slab[WT * WT + wn * 64 + 32 + i] = bs1;
+            slab[WT * WT + 128 * wn + i] = v0;
+            slab[WT * WT + 128 * wn + 32 + i] = v1;
+            slab[WT * WT + 128 * wn + 64 + i] = v2;
+            slab[WT * WT + 128 * wn + 96 + i] = v3;
         }
     }
 }
@@ -854,8 +902,8 @@ struct RJob {
     int rowpad0;       // padded output row of source row 0 (head stacking)
     int nseg;
     Seg seg[3];        // source col <-> padded feature
-    int slab_base;     // slab offset of tile (0,0) of the layer
-    int ktiles;        // number of k tiles of the layer
+    int block0[2];     // first slab of the layer's k-tile 0 / 1 (features [0,256) / [256,512))
+    int nsplit[2];
 };
 
 constexpr int MAXR = 28;
@@ -866,7 +914,7 @@ struct RJobs {
 };
 
 // one thread per gradient element of every parameter; sums the splits in a fixed order
-__global__ __launch_bounds__(256) void k_dw_reduce(RJobs R, int nsplit, const float *__restrict__ slabs) {
+__global__ __launch_bounds__(256) void k_dw_reduce(RJobs R, const float *__restrict__ slabs) {
     int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= R.begin[R.n]) return;
     int q = 0;
@@ -875,59 +923,65 @@ __global__ __launch_bounds__(256) void k_dw_reduce(RJobs R, int nsplit, const fl
     idx -= R.begin[q];
     int r = J.cols ? idx / J.cols : idx;
     int n = J.rowpad0 + r;
-    int tn = n / WT, nl = n % WT;
     float s = 0.f;
     if (J.cols) {
         int c = idx % J.cols;
         int f = -1;
         for (int k = 0; k < J.nseg; k++)
             if (c >= J.seg[k].s0 && c < J.seg[k].s0 + J.seg[k].len) f = J.seg[k].p0 + (c - J.seg[k].s0);
-        int tk = f / WT, kl = f % WT;
-        const float *sl = slabs + J.slab_base + (size_t)(tn * J.ktiles + tk) * nsplit * SLAB + nl * WT + kl;
-        for (int sp = 0; sp < nsplit; sp++) s += sl[(size_t)sp * SLAB];
+        int kt = f / WT, kl = f % WT;
+        const float *sl = slabs + (size_t)J.block0[kt] * SLAB + n * WT + kl;
+        for (int sp = 0; sp < J.nsplit[kt]; sp++) s += sl[(size_t)sp * SLAB];
     } else {
-        const float *sl = slabs + J.slab_base + (size_t)(tn * J.ktiles) * nsplit * SLAB + WT * WT + nl;
-        for (int sp = 0; sp < nsplit; sp++) s += sl[(size_t)sp * SLAB];
+        const float *sl = slabs + (size_t)J.block0[0] * SLAB + WT * WT + n;
+        for (int sp = 0; sp < J.nsplit[0]; sp++) s += sl[(size_t)sp * SLAB];
     }
     J.dst[idx] = s;
 }
 
-// dW job list for the flags (host)
+// dW job list for the flags (host): layers L0..L7 (L5 as two k-tiles), heads, T1, T2
 struct WPlan {
-    std::vector<WJob> jobs;
-    struct Layer {
-        int zrow, nrows, xrow, krows, ntiles, ktiles, slab_base;
-    };
-    std::vector<Layer> layers;  // order: L0..L7, heads, T1, T2
-    int slab_floats;
+    WJobs jobs;
+    int layer_job[11][2];  // job index of k-tile 0/1 per layer (-1 if none)
+    int nblocks;
 };
 
-inline WPlan make_wplan(const Flags &F, int nsplit) {
-    WPlan W;
-    int off = 0;
-    auto add = [&](int zrow, int nrows, int xrow, int krows) {
-        WPlan::Layer L{zrow, nrows, xrow, krows, div_up(nrows, WT), div_up(krows, WT), off};
-        for (int tn = 0; tn < L.ntiles; tn++)
-            for (int tk = 0; tk < L.ktiles; tk++) {
-                W.jobs.push_back(WJob{zrow, nrows, xrow, krows, tn, tk, off});
-                off += nsplit * SLAB;
-            }
-        W.layers.push_back(L);
+constexpr int DW_TARGET_BLOCKS = 256;  // one 8-wave workgroup per CU (LDS 147 KiB)
+
+inline WPlan make_wplan(const Flags &F) {
+    WPlan W{};
+    struct Raw {
+        int zrow, nrows, xrow, krows, layer, kt;
     };
+    Raw raw[MAXJ];
+    int nr = 0;
     for (int i = 0; i < 8; i++) {
         int xrow = (i == 0 || i == 5) ? S_XE : s_h(i - 1);
-        add(Z_L0 + 256 * i, 256, xrow, layer_kpad(i));
+        int kp = layer_kpad(i);
+        for (int kt = 0; kt * WT < kp; kt++)
+            raw[nr++] = Raw{Z_L0 + 256 * i, 256, xrow + kt * WT, min(WT, kp - kt * WT), i, kt};
     }
-    add(Z_G, 32, s_h(7), 256);
+    raw[nr++] = Raw{Z_G, 32, s_h(7), 256, 8, 0};
     if (F.blender) {
-        add(Z_T1, 256, S_TIN, 16);
-        add(Z_TE, 32, S_TH, 256);
+        raw[nr++] = Raw{Z_T1, 256, S_TIN, 16, 9, 0};
+        raw[nr++] = Raw{Z_TE, 32, S_TH, 256, 10, 0};
     }
-    W.slab_floats = off;
+    for (int l = 0; l < 11; l++) W.layer_job[l][0] = W.layer_job[l][1] = -1;
+    double total = 0;
+    for (int q = 0; q < nr; q++) total += (double)div_up(raw[q].nrows, 32) * div_up(raw[q].krows, 32);
+    int b = 0;
+    for (int q = 0; q < nr; q++) {
+        double w = (double)div_up(raw[q].nrows, 32) * div_up(raw[q].krows, 32);
+        int ns = (int)(DW_TARGET_BLOCKS * w / total + 0.5);
+        if (ns < 1) ns = 1;
+        W.jobs.j[q] = WJob{raw[q].zrow, raw[q].nrows, raw[q].xrow, raw[q].krows, ns, b};
+        W.layer_job[raw[q].layer][raw[q].kt] = q;
+        b += ns;
+    }
+    W.jobs.n = nr;
+    W.nblocks = b;
     return W;
 }
-
-constexpr int NSPLIT = 13;  // 38 blocks-tiles x 13 = 494 workgroups: one wave of 2 per CU
 
 }  // namespace mlp
 }  // namespace dgs
@@ -941,31 +995,10 @@ extern "C" size_t dgs_deform_packed_floats(int flags) { return (size_t)make_plan
 static size_t padded_points(int N) { return (size_t)div_up(N, BM) * BM; }
 extern "C" size_t dgs_deform_saved_floats(int flags, int N) { return (size_t)make_flags(flags).nsaved * padded_points(N); }
 
-// constant dW job table per (device, flags), uploaded once
-static int job_table(int flags, const WPlan &W, WJob **out) {
-    static std::mutex mu;
-    static std::map<std::pair<int, int>, WJob *> tables;
-    int dev = 0;
-    DGS_HIP_CHECK(hipGetDevice(&dev));
-    std::lock_guard<std::mutex> lk(mu);
-    auto key = std::make_pair(dev, flags);
-    auto it = tables.find(key);
-    if (it != tables.end()) {
-        *out = it->second;
-        return DGS_OK;
-    }
-    WJob *d = nullptr;
-    DGS_HIP_CHECK(hipMalloc(&d, sizeof(WJob) * W.jobs.size()));
-    DGS_HIP_CHECK(hipMemcpy(d, W.jobs.data(), sizeof(WJob) * W.jobs.size(), hipMemcpyHostToDevice));
-    tables[key] = d;
-    *out = d;
-    return DGS_OK;
-}
-
 extern "C" size_t dgs_deform_scratch_floats(int flags, int N) {
     Flags F = make_flags(flags);
-    WPlan W = make_wplan(F, NSPLIT);
-    return (size_t)F.nz * padded_points(N) + (size_t)W.slab_floats;
+    WPlan W = make_wplan(F);
+    return (size_t)F.nz * padded_points(N) + (size_t)W.nblocks * SLAB;
 }
 
 static int param_shape(const Plan &P, int idx, int &rows, int &cols) {
@@ -1072,26 +1105,32 @@ extern "C" int dgs_deform_backward(int flags, int N, const float *packed, const 
         hipLaunchKernelGGL(k_mlp_bwd, dim3(div_up(N, BM)), dim3(NTHR), 0, stream, b);
     }
     DGS_LAUNCH_CHECK("k_mlp_bwd", false, stream);
-    WPlan W = make_wplan(F, NSPLIT);
-    WJob *djobs = nullptr;
-    if (int rc = job_table(flags, W, &djobs)) return rc;
-    const int cps = div_up((int)(Ns / PC), NSPLIT);
+    WPlan W = make_wplan(F);
     {
+        static bool attr_set = false;  // 147 KiB dynamic LDS
+        const size_t lds_bytes = sizeof(float) * 2 * 2 * WT * LDA;
+        if (!attr_set) {
+            DGS_HIP_CHECK(hipFuncSetAttribute((const void *)k_dw, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes));
+            attr_set = true;
+        }
         ScopedTimer tm("mlp_dw", stream);
-        hipLaunchKernelGGL(k_dw, dim3((unsigned)W.jobs.size() * NSPLIT), dim3(256), 0, stream, djobs, NSPLIT, Ns, cps, dz,
-                           saved, slabs);
+        hipLaunchKernelGGL(k_dw, dim3(W.nblocks), dim3(DW_THREADS), lds_bytes, stream, W.jobs, Ns, dz, saved, slabs);
     }
     DGS_LAUNCH_CHECK("k_dw", false, stream);
     // one batched reduction launch into every parameter gradient
     RJobs R{};
     int total = 0;
-    auto add = [&](int pidx, int rowpad0, int ns, const Seg *sg, const WPlan::Layer &L, bool bias) {
+    auto add = [&](int pidx, int rowpad0, int ns, const Seg *sg, int layer, bool bias) {
         int r, c;
         param_shape(P, pidx, r, c);
         RJob &J = R.j[R.n];
         J.dst = grads[pidx]; J.rows = r; J.cols = bias ? 0 : c; J.rowpad0 = rowpad0; J.nseg = ns;
         for (int q = 0; q < ns; q++) J.seg[q] = sg[q];
-        J.slab_base = L.slab_base; J.ktiles = L.ktiles;
+        for (int kt = 0; kt < 2; kt++) {
+            int jq = W.layer_job[layer][kt];
+            J.block0[kt] = jq >= 0 ? W.jobs.j[jq].block0 : 0;
+            J.nsplit[kt] = jq >= 0 ? W.jobs.j[jq].nsplit : 0;
+        }
         R.begin[R.n] = total;
         total += bias ? r : r * c;
         R.n++;
@@ -1099,29 +1138,29 @@ extern "C" int dgs_deform_backward(int flags, int N, const float *packed, const 
     for (int i = 0; i < 8; i++) {
         Seg sg[3];
         int ns = layer_in_segs(F, i, sg);
-        add(P.pLw[i], 0, ns, sg, W.layers[i], false);
-        add(P.pLb[i], 0, ns, sg, W.layers[i], true);
+        add(P.pLw[i], 0, ns, sg, i, false);
+        add(P.pLb[i], 0, ns, sg, i, true);
     }
     {
         Seg full = seg(0, 256, 0);
         int r0 = 0;
         for (int hh = 0; hh < P.nheads; hh++) {
-            add(P.pHw[hh], r0, 1, &full, W.layers[8], false);
-            add(P.pHb[hh], r0, 1, &full, W.layers[8], true);
+            add(P.pHw[hh], r0, 1, &full, 8, false);
+            add(P.pHb[hh], r0, 1, &full, 8, true);
             r0 += P.hrows[hh];
         }
         if (F.blender) {
             Seg st = seg(0, F.tin, 0);
-            add(P.pT0w, 0, 1, &st, W.layers[9], false);
-            add(P.pT0b, 0, 1, &st, W.layers[9], true);
-            add(P.pT2w, 0, 1, &full, W.layers[10], false);
-            add(P.pT2b, 0, 1, &full, W.layers[10], true);
+            add(P.pT0w, 0, 1, &st, 9, false);
+            add(P.pT0b, 0, 1, &st, 9, true);
+            add(P.pT2w, 0, 1, &full, 10, false);
+            add(P.pT2b, 0, 1, &full, 10, true);
         }
     }
     R.begin[R.n] = total;
     {
         ScopedTimer tm("mlp_dw_reduce", stream);
-        hipLaunchKernelGGL(k_dw_reduce, dim3(div_up(total, 256)), dim3(256), 0, stream, R, NSPLIT, slabs);
+        hipLaunchKernelGGL(k_dw_reduce, dim3(div_up(total, 256)), dim3(256), 0, stream, R, slabs);
     }
     DGS_LAUNCH_CHECK("k_dw_reduce", false, stream);
     return DGS_OK;
