@@ -489,7 +489,8 @@ __device__ inline void narrow_layer(const float4 *Apk, int nchunks, float4 *lds,
 
 __global__ __launch_bounds__(NTHR) void k_mlp_fwd(FwdArgs a) {
     __shared__ float4 lds[G_TOTAL * BM];
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform (scalar branches)
     const int p0 = blockIdx.x * BM;
     const Flags F = make_flags(a.flags);
     const float4 *pk = reinterpret_cast<const float4 *>(a.packed);
@@ -636,7 +637,8 @@ __device__ inline void mask_store(f32x16 &acc, const float *__restrict__ saved_r
 
 __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
     __shared__ float4 lds[G_TOTAL * BM];
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform (scalar branches)
     const int p0 = blockIdx.x * BM;
     const Flags F = make_flags(a.flags);
     const float4 *pk = reinterpret_cast<const float4 *>(a.packed);
@@ -766,7 +768,8 @@ __global__ __launch_bounds__(DW_THREADS) void k_dw(WJobs JT, size_t Ns, const fl
     for (int q = 1; q < MAXJ; q++)
         if (q < JT.n && (int)blockIdx.x >= JT.j[q].block0) J = JT.j[q];
     const int split = blockIdx.x - J.block0;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform (scalar branches)
     const int wn = wave >> 2, wk = wave & 3;  // wave tile: rows [128 wn, +128), cols [64 wk, +64)
     const int h = lane >> 5, i = lane & 31;
     const int nch = (int)(Ns / PC);
