@@ -787,7 +787,8 @@ __global__ __launch_bounds__(DW_THREADS) void k_dw(WJobs JT, size_t Ns, const fl
 #undef DW_OFF
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
     float4 ra0, ra1, ra2, ra3, rb0, rb1, rb2, rb3;
-    // rows past the job's extent load row 0 (always valid) and are zeroed after the load: an
+    // rows past the job's extent load row 0 (always valid) and are zeroed at the LDS store (after
+    // the chunk's MFMAs, so the loads stay in flight across them): an
     // unconditional global_load keeps hipcc from turning `ok ? *p : 0` into a flat load of a
     // pointer select between global memory and a scratch-held zero
 #define DW_LD(base, o, po) (*reinterpret_cast<const float4 *>((base) + ((o) >= 0 ? (o) : scol) + (po)))
@@ -799,22 +800,20 @@ __global__ __launch_bounds__(DW_THREADS) void k_dw(WJobs JT, size_t Ns, const fl
         ra2 = DW_LD(baseA, oA2, po_); ra3 = DW_LD(baseA, oA3, po_);                                        \
         rb0 = DW_LD(baseB, oB0, po_); rb1 = DW_LD(baseB, oB1, po_);                                        \
         rb2 = DW_LD(baseB, oB2, po_); rb3 = DW_LD(baseB, oB3, po_);                                        \
-        ra0 = DW_Z(ra0, oA0); ra1 = DW_Z(ra1, oA1); ra2 = DW_Z(ra2, oA2); ra3 = DW_Z(ra3, oA3);            \
-        rb0 = DW_Z(rb0, oB0); rb1 = DW_Z(rb1, oB1); rb2 = DW_Z(rb2, oB2); rb3 = DW_Z(rb3, oB3);            \
     } while (0)
 #define DW_LSTORE(buf)                                                                                     \
     do {                                                                                                   \
         float *A_ = ldsf + (buf) * (2 * WT * LDA);                                                         \
         float *B_ = A_ + WT * LDA;                                                                         \
         const int row_ = tid >> 3, col_ = (tid & 7) * 4;                                                   \
-        *reinterpret_cast<float4 *>(A_ + (row_ + 0) * LDA + col_) = ra0;                                   \
-        *reinterpret_cast<float4 *>(A_ + (row_ + 64) * LDA + col_) = ra1;                                  \
-        *reinterpret_cast<float4 *>(A_ + (row_ + 128) * LDA + col_) = ra2;                                 \
-        *reinterpret_cast<float4 *>(A_ + (row_ + 192) * LDA + col_) = ra3;                                 \
-        *reinterpret_cast<float4 *>(B_ + (row_ + 0) * LDA + col_) = rb0;                                   \
-        *reinterpret_cast<float4 *>(B_ + (row_ + 64) * LDA + col_) = rb1;                                  \
-        *reinterpret_cast<float4 *>(B_ + (row_ + 128) * LDA + col_) = rb2;                                 \
-        *reinterpret_cast<float4 *>(B_ + (row_ + 192) * LDA + col_) = rb3;                                 \
+        *reinterpret_cast<float4 *>(A_ + (row_ + 0) * LDA + col_) = DW_Z(ra0, oA0);                        \
+        *reinterpret_cast<float4 *>(A_ + (row_ + 64) * LDA + col_) = DW_Z(ra1, oA1);                       \
+        *reinterpret_cast<float4 *>(A_ + (row_ + 128) * LDA + col_) = DW_Z(ra2, oA2);                      \
+        *reinterpret_cast<float4 *>(A_ + (row_ + 192) * LDA + col_) = DW_Z(ra3, oA3);                      \
+        *reinterpret_cast<float4 *>(B_ + (row_ + 0) * LDA + col_) = DW_Z(rb0, oB0);                        \
+        *reinterpret_cast<float4 *>(B_ + (row_ + 64) * LDA + col_) = DW_Z(rb1, oB1);                       \
+        *reinterpret_cast<float4 *>(B_ + (row_ + 128) * LDA + col_) = DW_Z(rb2, oB2);                      \
+        *reinterpret_cast<float4 *>(B_ + (row_ + 192) * LDA + col_) = DW_Z(rb3, oB3);                      \
     } while (0)
     // this wave's active sub-tiles (wave-uniform): rows 128 wn + 32 t, cols 64 wk + 32 u
     const int nact_r = min(4, max(0, div_up(J.nrows - 128 * wn, 32)));  // active 32-row sub-tiles

@@ -1,0 +1,135 @@
+"""Frame-parallel data parallelism on CPU (gloo, world_size 2): the same code the bench runs over
+RCCL, exercised without a GPU."""
+import os
+import socket
+import types
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from deformgs.dist import GradAllReduce, init_from_env, rank_identical_generator, sync_densification_stats
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, fn, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    try:
+        r, w, _ = init_from_env("gloo")
+        assert (r, w) == (rank, world)
+        q.put((rank, fn(rank, world)))
+    except Exception as e:  # surfaced in the parent
+        q.put((rank, e))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def _run(fn, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fn, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        r, v = q.get(timeout=120)
+        out[r] = v
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r, v in out.items():
+        if isinstance(v, Exception):
+            raise v
+    return out
+
+
+def _grad_case(rank, world):
+    torch.manual_seed(0)
+    params = [torch.nn.Parameter(torch.randn(s)) for s in [(7, 3), (100,), (5, 5, 2), (3,)]]
+    frozen = torch.nn.Parameter(torch.randn(4), requires_grad=False)
+    for i, p in enumerate(params[:3]):  # last param: no grad on this step
+        p.grad = torch.full_like(p, float(rank + 1) * (i + 1))
+    # tiny buckets force several collectives; identical on both ranks
+    GradAllReduce(lambda: params + [frozen], bucket_bytes=256)()
+    return [None if p.grad is None else p.grad.clone() for p in params], frozen.grad
+
+
+def _grad_uneven_case(rank, world):
+    p = torch.nn.Parameter(torch.zeros(10))
+    q = torch.nn.Parameter(torch.zeros(6))
+    # rank 0 has q.grad, rank 1 does not: the missing grad contributes zeros
+    p.grad = torch.arange(10.0) * (rank + 1)
+    if rank == 0:
+        q.grad = torch.ones(6) * 4.0
+    GradAllReduce(lambda: [p, q])()
+    return p.grad.clone(), q.grad.clone()
+
+
+def _stats_case(rank, world):
+    g = types.SimpleNamespace(
+        xyz_gradient_accum=torch.full((5, 1), float(rank + 1)),
+        denom=torch.full((5, 1), 2.0),
+        max_radii2D=torch.tensor([1.0, 5.0, 3.0, 0.0, 2.0]) * (1 if rank == 0 else -1) + rank * 4,
+    )
+    sync_densification_stats(g)
+    return g.xyz_gradient_accum.clone(), g.denom.clone(), g.max_radii2D.clone()
+
+
+def _gen_case(rank, world):
+    gen = rank_identical_generator("cpu", seed=77)
+    return torch.randn(16, generator=gen), torch.rand(8, generator=gen)
+
+
+def test_grad_allreduce_average():
+    out = _run(_grad_case)
+    grads0, fz0 = out[0]
+    grads1, _ = out[1]
+    for i in range(3):
+        want = torch.full_like(grads0[i], 1.5 * (i + 1))  # mean of (1, 2) * (i + 1)
+        torch.testing.assert_close(grads0[i], want)
+        torch.testing.assert_close(grads1[i], want)
+    # no grad anywhere -> zeros (never None after the step, so the optimizer sees the same on all ranks)
+    assert torch.count_nonzero(grads0[3]) == 0 and torch.count_nonzero(grads1[3]) == 0
+    assert fz0 is None  # frozen params are skipped
+
+
+def test_grad_allreduce_missing_grad_counts_as_zero():
+    out = _run(_grad_uneven_case)
+    for r in (0, 1):
+        pg, qg = out[r]
+        torch.testing.assert_close(pg, torch.arange(10.0) * 1.5)
+        torch.testing.assert_close(qg, torch.full((6,), 2.0))
+
+
+def test_sync_densification_stats():
+    out = _run(_stats_case)
+    for r in (0, 1):
+        acc, den, rad = out[r]
+        torch.testing.assert_close(acc, torch.full((5, 1), 3.0))
+        torch.testing.assert_close(den, torch.full((5, 1), 4.0))
+        torch.testing.assert_close(rad, torch.tensor([3.0, 5.0, 3.0, 4.0, 2.0]))
+
+
+def test_rank_identical_generator():
+    out = _run(_gen_case)
+    torch.testing.assert_close(out[0][0], out[1][0], rtol=0, atol=0)
+    torch.testing.assert_close(out[0][1], out[1][1], rtol=0, atol=0)
+
+
+def test_single_process_is_noop():
+    p = torch.nn.Parameter(torch.ones(3))
+    p.grad = torch.full((3,), 2.0)
+    GradAllReduce(lambda: [p])()
+    torch.testing.assert_close(p.grad, torch.full((3,), 2.0))
+    sync_densification_stats(types.SimpleNamespace())  # not initialised -> untouched
