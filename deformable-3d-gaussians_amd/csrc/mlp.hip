@@ -239,39 +239,20 @@ __host__ __device__ inline int seg_lookup(const Seg *s, int ns, int p) {
     return -1;
 }
 
-struct ParamDesc {
-    const float *ptr;
-    int rows, cols;
+// Packing is one gather launch: map[i] = (parameter << 22) | element for packed float i, or -1 for
+// zero padding. The map depends only on the flags (built once on the host, cached on the device).
+constexpr int PACK_MAXP = 32;
+constexpr int PACK_SHIFT = 22;
+struct PackPtrs {
+    const float *p[PACK_MAXP];
 };
 
-// One thread per packed float. Heads jobs share an image: only write where the n-segment matches.
-__global__ void k_pack(PackJob job, ParamDesc src, float *__restrict__ packed, bool zero_fill) {
-    int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    int total = job.ntiles * job.nchunks * 256;
-    if (idx >= total) return;
-    int t = idx & 3;
-    int lane = (idx >> 2) & 63;
-    int rest = idx >> 8;
-    int chunk = rest % job.nchunks;
-    int ntile = rest / job.nchunks;
-    int n = ntile * 32 + (lane & 31);
-    int f = chunk * 8 + 4 * (lane >> 5) + t;
-    int sn = seg_lookup(job.segn, job.nseg_n, n);
-    int sf = seg_lookup(job.segf, job.nseg_f, f);
-    float v = 0.f;
-    bool mine = job.transpose ? (sf >= 0) : (sn >= 0);
-    if (sn >= 0 && sf >= 0) v = job.transpose ? src.ptr[sf * src.cols + sn] : src.ptr[sn * src.cols + sf];
-    if (mine || zero_fill) packed[job.off + idx] = v;
-}
-
-__global__ void k_pack_bias(BiasJob job, ParamDesc src, float *__restrict__ packed, bool zero_fill) {
-    int n = blockIdx.x * blockDim.x + threadIdx.x;
-    if (n >= job.npad) return;
-    int s = seg_lookup(job.seg, job.nseg, n);
-    if (s >= 0)
-        packed[job.off + n] = src.ptr[s];
-    else if (zero_fill)
-        packed[job.off + n] = 0.f;
+__global__ __launch_bounds__(256) void k_pack_map(const int *__restrict__ map, PackPtrs src, float *__restrict__ packed,
+                                                  int total) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int c = map[i];
+    packed[i] = c < 0 ? 0.f : src.p[c >> PACK_SHIFT][c & ((1 << PACK_SHIFT) - 1)];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -337,8 +318,8 @@ __device__ inline void gemm_2m(const float4 *__restrict__ Apk, int c0, int c1, c
 template <class Side = NoSide>
 __device__ inline void gemm_1m(const float4 *__restrict__ Apk, int c0, int c1, const float4 *lds, int g0, int mt,
                                int lane, f32x16 &acc, Side side = Side()) {
-    const int h = lane >> 5, m = lane & 31;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int h = lane >> 5, m = lane & 31;
     float4 p0 = (c0 < c1) ? Apk[c0 * 64 + lane] : z4;
     float4 p1 = (c0 + 1 < c1) ? Apk[(c0 + 1) * 64 + lane] : z4;
     for (int c = c0; c < c1; c++) {
@@ -752,25 +733,22 @@ struct WJob {
     int xrow, krows;   // X rows [xrow, xrow + krows) in saved (<= 256)
     int nsplit;        // workgroups over the point axis
     int block0;        // first workgroup (= first slab) of this job
+    int narrow;        // wave layout: 0 = 2 (rows) x 4 (cols) waves of 128 x 64; 1 = 8 x 1 waves of
+                       // 32 x 128 (jobs with krows <= 128: every wave has work)
 };
 struct WJobs {
     WJob j[MAXJ];
     int n;
 };
 
-__global__ __launch_bounds__(DW_THREADS) void k_dw(WJobs JT, size_t Ns, const float *__restrict__ dz,
-                                                   const float *__restrict__ saved, float *__restrict__ slabs) {
-    extern __shared__ float4 dw_lds[];
-    float *ldsf = reinterpret_cast<float *>(dw_lds);
-    // job of this workgroup: static-index selects over the kernel-argument table (no scratch copy)
-    WJob J = JT.j[0];
-#pragma unroll
-    for (int q = 1; q < MAXJ; q++)
-        if (q < JT.n && (int)blockIdx.x >= JT.j[q].block0) J = JT.j[q];
+template <bool NARROW>
+__device__ __forceinline__ void dw_tile(const WJob &J, size_t Ns, const float *__restrict__ dz,
+                                        const float *__restrict__ saved, float *__restrict__ slabs,
+                                        float *ldsf) {
     const int split = blockIdx.x - J.block0;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform (scalar branches)
-    const int wn = wave >> 2, wk = wave & 3;  // wave tile: rows [128 wn, +128), cols [64 wk, +64)
+    const int wn = wave >> 2, wk = wave & 3;  // wide wave tile: rows [128 wn, +128), cols [64 wk, +64)
     const int h = lane >> 5, i = lane & 31;
     const int nch = (int)(Ns / PC);
     const int per = div_up(nch, J.nsplit);
@@ -785,21 +763,26 @@ __global__ __launch_bounds__(DW_THREADS) void k_dw(WJobs JT, size_t Ns, const fl
     const int oA0 = DW_OFF(J.nrows, 0), oA1 = DW_OFF(J.nrows, 1), oA2 = DW_OFF(J.nrows, 2), oA3 = DW_OFF(J.nrows, 3);
     const int oB0 = DW_OFF(J.krows, 0), oB1 = DW_OFF(J.krows, 1), oB2 = DW_OFF(J.krows, 2), oB3 = DW_OFF(J.krows, 3);
 #undef DW_OFF
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
     float4 ra0, ra1, ra2, ra3, rb0, rb1, rb2, rb3;
     // rows past the job's extent load row 0 (always valid) and are zeroed at the LDS store (after
     // the chunk's MFMAs, so the loads stay in flight across them): an
     // unconditional global_load keeps hipcc from turning `ok ? *p : 0` into a flat load of a
     // pointer select between global memory and a scratch-held zero
-#define DW_LD(base, o, po) (*reinterpret_cast<const float4 *>((base) + ((o) >= 0 ? (o) : scol) + (po)))
+    // 32-bit byte offsets from a uniform base -> global_load with an SGPR base (saddr) and one
+    // offset VGPR per load instead of a 64-bit address pair
+#define DW_U(o) ((uint32_t)(((o) >= 0 ? (o) : scol) * 4))
+    const uint32_t uA0 = DW_U(oA0), uA1 = DW_U(oA1), uA2 = DW_U(oA2), uA3 = DW_U(oA3);
+    const uint32_t uB0 = DW_U(oB0), uB1 = DW_U(oB1), uB2 = DW_U(oB2), uB3 = DW_U(oB3);
+#undef DW_U
+#define DW_LD(base, u, po) (*reinterpret_cast<const float4 *>(reinterpret_cast<const char *>(base) + (uint32_t)((u) + (uint32_t)(po) * 4u)))
 #define DW_Z(v, o) zsel4((v), (o) >= 0)
 #define DW_GLOAD(c)                                                                                        \
     do {                                                                                                   \
         const int po_ = (c) * PC;                                                                          \
-        ra0 = DW_LD(baseA, oA0, po_); ra1 = DW_LD(baseA, oA1, po_);                                        \
-        ra2 = DW_LD(baseA, oA2, po_); ra3 = DW_LD(baseA, oA3, po_);                                        \
-        rb0 = DW_LD(baseB, oB0, po_); rb1 = DW_LD(baseB, oB1, po_);                                        \
-        rb2 = DW_LD(baseB, oB2, po_); rb3 = DW_LD(baseB, oB3, po_);                                        \
+        ra0 = DW_LD(baseA, uA0, po_); ra1 = DW_LD(baseA, uA1, po_);                                        \
+        ra2 = DW_LD(baseA, uA2, po_); ra3 = DW_LD(baseA, uA3, po_);                                        \
+        rb0 = DW_LD(baseB, uB0, po_); rb1 = DW_LD(baseB, uB1, po_);                                        \
+        rb2 = DW_LD(baseB, uB2, po_); rb3 = DW_LD(baseB, uB3, po_);                                        \
     } while (0)
 #define DW_LSTORE(buf)                                                                                     \
     do {                                                                                                   \
@@ -815,9 +798,11 @@ __global__ __launch_bounds__(DW_THREADS) void k_dw(WJobs JT, size_t Ns, const fl
         *reinterpret_cast<float4 *>(B_ + (row_ + 128) * LDA + col_) = DW_Z(rb2, oB2);                      \
         *reinterpret_cast<float4 *>(B_ + (row_ + 192) * LDA + col_) = DW_Z(rb3, oB3);                      \
     } while (0)
-    // this wave's active sub-tiles (wave-uniform): rows 128 wn + 32 t, cols 64 wk + 32 u
-    const int nact_r = min(4, max(0, div_up(J.nrows - 128 * wn, 32)));  // active 32-row sub-tiles
-    const int nact_c = min(2, max(0, div_up(J.krows - 64 * wk, 32)));   // active 32-col sub-tiles
+    // this wave's active sub-tiles (wave-uniform). wide: rows 128 wn + 32 t, cols 64 wk + 32 u
+    // (acc[t][u]); narrow: rows 32 wave, cols 32 v (acc[v >> 1][v & 1], v < 4)
+    constexpr bool narrow = NARROW;
+    const int nact_r = narrow ? (32 * wave < J.nrows ? 1 : 0) : min(4, max(0, div_up(J.nrows - 128 * wn, 32)));
+    const int nact_c = narrow ? min(4, div_up(J.krows, 32)) : min(2, max(0, div_up(J.krows - 64 * wk, 32)));
     const bool any = nact_r > 0 && nact_c > 0;
     f32x16 acc[4][2];
 #pragma unroll
@@ -837,7 +822,25 @@ __global__ __launch_bounds__(DW_THREADS) void k_dw(WJobs JT, size_t Ns, const fl
         if (more) DW_GLOAD(c + 1);
         const float *A = ldsf + buf * (2 * WT * LDA);
         const float *B = A + WT * LDA;
-        if (any) {
+        if (any && narrow) {
+#pragma unroll
+            for (int g = 0; g < PC / 8; g++) {
+                const int o = 8 * g + 4 * h;
+                const float4 a0 = *reinterpret_cast<const float4 *>(A + (32 * wave + i) * LDA + o);
+                float4 bb[4];
+#pragma unroll
+                for (int v = 0; v < 4; v++) bb[v] = *reinterpret_cast<const float4 *>(B + (32 * v + i) * LDA + o);
+                bs0 += (a0.x + a0.y) + (a0.z + a0.w);
+#pragma unroll
+                for (int v = 0; v < 4; v++) {
+                    if (v >= nact_c) continue;
+                    acc[v >> 1][v & 1] = MFMA(a0.x, bb[v].x, acc[v >> 1][v & 1]);
+                    acc[v >> 1][v & 1] = MFMA(a0.y, bb[v].y, acc[v >> 1][v & 1]);
+                    acc[v >> 1][v & 1] = MFMA(a0.z, bb[v].z, acc[v >> 1][v & 1]);
+                    acc[v >> 1][v & 1] = MFMA(a0.w, bb[v].w, acc[v >> 1][v & 1]);
+                }
+            }
+        } else if (any) {
 #pragma unroll
             for (int g = 0; g < PC / 8; g++) {
                 const int o = 8 * g + 4 * h;
@@ -874,6 +877,21 @@ __global__ __launch_bounds__(DW_THREADS) void k_dw(WJobs JT, size_t Ns, const fl
 #undef DW_LD
 #undef DW_Z
     float *slab = slabs + (size_t)blockIdx.x * SLAB;
+    if (narrow) {
+        // rows past nrows / cols past krows hold zeros or partial garbage that k_dw_reduce never reads
+#pragma unroll
+        for (int v = 0; v < 4; v++) {
+            const int nb = 32 * wave, kb = 32 * v;
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                int n = nb + 8 * (r >> 2) + 4 * h + (r & 3);
+                slab[n * WT + kb + i] = acc[v >> 1][v & 1][r];
+            }
+        }
+        float v0 = bs0 + __shfl_xor(bs0, 32);
+        if (h == 0) slab[WT * WT + 32 * wave + i] = v0;
+        return;
+    }
 #pragma unroll
     for (int t = 0; t < 4; t++)
 #pragma unroll
@@ -896,6 +914,22 @@ __global__ __launch_bounds__(DW_THREADS) void k_dw(WJobs JT, size_t Ns, const fl
             slab[WT * WT + 128 * wn + 96 + i] = v3;
         }
     }
+}
+
+__global__ __launch_bounds__(DW_THREADS) void k_dw(WJobs JT, size_t Ns, const float *__restrict__ dz,
+                                                   const float *__restrict__ saved, float *__restrict__ slabs) {
+    extern __shared__ float4 dw_lds[];
+    // job of this workgroup: static-index selects over the kernel-argument table (no scratch copy)
+    WJob J = JT.j[0];
+#pragma unroll
+    for (int q = 1; q < MAXJ; q++)
+        if (q < JT.n && (int)blockIdx.x >= JT.j[q].block0) J = JT.j[q];
+    // the two wave layouts are separate code regions (a runtime switch inside one loop makes the
+    // register allocator spill the accumulators)
+    if (J.narrow)
+        dw_tile<true>(J, Ns, dz, saved, slabs, reinterpret_cast<float *>(dw_lds));
+    else
+        dw_tile<false>(J, Ns, dz, saved, slabs, reinterpret_cast<float *>(dw_lds));
 }
 
 struct RJob {
@@ -969,14 +1003,32 @@ inline WPlan make_wplan(const Flags &F) {
         raw[nr++] = Raw{Z_TE, 32, S_TH, 256, 10, 0};
     }
     for (int l = 0; l < 11; l++) W.layer_job[l][0] = W.layer_job[l][1] = -1;
-    double total = 0;
-    for (int q = 0; q < nr; q++) total += (double)div_up(raw[q].nrows, 32) * div_up(raw[q].krows, 32);
+    // per-chunk cost = the busiest SIMD's MFMA tiles (waves w and w + 4 share SIMD w % 4), floored
+    // at the load latency a chunk cannot hide (~5 tiles of MFMA time)
+    double cost[MAXJ], total = 0;
+    for (int q = 0; q < nr; q++) {
+        const bool nar = raw[q].krows <= 128;
+        int simd[4] = {0, 0, 0, 0};
+        for (int w = 0; w < 8; w++) {
+            int tr, tc;
+            if (nar) {
+                tr = 32 * w < raw[q].nrows ? 1 : 0;
+                tc = min(4, div_up(raw[q].krows, 32));
+            } else {
+                tr = min(4, max(0, div_up(raw[q].nrows - 128 * (w >> 2), 32)));
+                tc = min(2, max(0, div_up(raw[q].krows - 64 * (w & 3), 32)));
+            }
+            simd[w & 3] += tr * tc;
+        }
+        int crit = max(max(simd[0], simd[1]), max(simd[2], simd[3]));
+        cost[q] = (double)max(crit, 5);
+        total += cost[q];
+    }
     int b = 0;
     for (int q = 0; q < nr; q++) {
-        double w = (double)div_up(raw[q].nrows, 32) * div_up(raw[q].krows, 32);
-        int ns = (int)(DW_TARGET_BLOCKS * w / total + 0.5);
+        int ns = (int)(DW_TARGET_BLOCKS * cost[q] / total + 0.5);
         if (ns < 1) ns = 1;
-        W.jobs.j[q] = WJob{raw[q].zrow, raw[q].nrows, raw[q].xrow, raw[q].krows, ns, b};
+        W.jobs.j[q] = WJob{raw[q].zrow, raw[q].nrows, raw[q].xrow, raw[q].krows, ns, b, raw[q].krows <= 128 ? 1 : 0};
         W.layer_job[raw[q].layer][raw[q].kt] = q;
         b += ns;
     }
@@ -1024,32 +1076,78 @@ static int param_shape(const Plan &P, int idx, int &rows, int &cols) {
     return -1;
 }
 
+// host emulation of the packed-image layout (forward A images, transposed backward images, biases)
+static std::vector<int> build_pack_map(const Plan &P) {
+    std::vector<int> map((size_t)P.total, -1);
+    for (const PackJob &j : P.jobs) {
+        int r, c;
+        param_shape(P, j.src, r, c);
+        const bool head = (j.off == P.fHd || j.off == P.tHd);  // head images are shared by several jobs
+        const int total = j.ntiles * j.nchunks * 256;
+        for (int idx = 0; idx < total; idx++) {
+            int t = idx & 3, lane = (idx >> 2) & 63, rest = idx >> 8;
+            int chunk = rest % j.nchunks, ntile = rest / j.nchunks;
+            int n = ntile * 32 + (lane & 31);
+            int f = chunk * 8 + 4 * (lane >> 5) + t;
+            int sn = seg_lookup(j.segn, j.nseg_n, n);
+            int sf = seg_lookup(j.segf, j.nseg_f, f);
+            bool mine = j.transpose ? (sf >= 0) : (sn >= 0);
+            int code = -1;
+            if (sn >= 0 && sf >= 0) code = (j.src << PACK_SHIFT) | (j.transpose ? sf * c + sn : sn * c + sf);
+            if (mine || !head) map[(size_t)j.off + idx] = code;
+        }
+    }
+    for (const BiasJob &b : P.biases)
+        for (int n = 0; n < b.npad; n++) {
+            int sidx = seg_lookup(b.seg, b.nseg, n);
+            if (sidx >= 0) map[(size_t)b.off + n] = (b.src << PACK_SHIFT) | sidx;
+            else if (b.off != P.bHd) map[(size_t)b.off + n] = -1;
+        }
+    return map;
+}
+
+static std::mutex g_map_mu;
+static std::map<std::pair<int, int>, int *> g_pack_maps;  // (device, flags) -> device map
+
+static int *pack_map_for(const Plan &P, int flags) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(g_map_mu);
+    auto it = g_pack_maps.find({dev, flags});
+    if (it != g_pack_maps.end()) return it->second;
+    std::vector<int> h = build_pack_map(P);
+    int *d = nullptr;
+    if (hipMalloc(&d, h.size() * sizeof(int)) != hipSuccess) return nullptr;
+    if (hipMemcpy(d, h.data(), h.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(d);
+        return nullptr;
+    }
+    g_pack_maps[{dev, flags}] = d;
+    return d;
+}
+
 extern "C" int dgs_deform_pack(int flags, const float *const *params, float *packed, void *stream_) {
     hipStream_t stream = (hipStream_t)stream_;
     Plan P = make_plan(flags);
-    for (int k = 0; k < P.nparams; k++)
+    if (P.nparams > PACK_MAXP) {
+        set_error("dgs_deform_pack: too many parameters");
+        return DGS_ERR_ARGS;
+    }
+    PackPtrs src{};
+    for (int k = 0; k < P.nparams; k++) {
         if (!params[k]) {
             set_error("dgs_deform_pack: null parameter pointer");
             return DGS_ERR_ARGS;
         }
-    // head images are shared by several jobs: zero them once, then each job writes its rows
-    DGS_HIP_CHECK(hipMemsetAsync(packed + P.fHd, 0, sizeof(float) * (32 * 256 + 8 * 4 * 256 + 32), stream));
-    for (const PackJob &j : P.jobs) {
-        int r, c;
-        param_shape(P, j.src, r, c);
-        ParamDesc d{params[j.src], r, c};
-        bool head = (j.off == P.fHd || j.off == P.tHd);
-        int total = j.ntiles * j.nchunks * 256;
-        hipLaunchKernelGGL(k_pack, dim3(div_up(total, 256)), dim3(256), 0, stream, j, d, packed, !head);
+        src.p[k] = params[k];
     }
-    for (const BiasJob &b : P.biases) {
-        int r, c;
-        param_shape(P, b.src, r, c);
-        ParamDesc d{params[b.src], r, 0};
-        bool head = (b.off == P.bHd);
-        hipLaunchKernelGGL(k_pack_bias, dim3(div_up(b.npad, 64)), dim3(64), 0, stream, b, d, packed, !head);
+    const int *map = pack_map_for(P, flags);
+    if (!map) {
+        set_error("dgs_deform_pack: could not allocate the pack map");
+        return DGS_ERR_HIP;
     }
-    DGS_LAUNCH_CHECK("k_pack", false, stream);
+    hipLaunchKernelGGL(k_pack_map, dim3(div_up(P.total, 256)), dim3(256), 0, stream, map, src, packed, P.total);
+    DGS_LAUNCH_CHECK("k_pack_map", false, stream);
     return DGS_OK;
 }
 

@@ -226,8 +226,21 @@ __global__ __launch_bounds__(256) void k_blend_fwd(const uint2 *__restrict__ ran
 // ------------------------------------------------------------------------------------------------
 // backward kernels
 // ------------------------------------------------------------------------------------------------
-// Sum over the 64 lanes, result valid in lane 63 (gfx9 DPP: row_shr 1/2/4/8, row_bcast 15/31).
-__device__ inline float wave_sum63(float v) {
+// Reduce-scatter of the 12 per-Gaussian partial gradients over the 64 lanes (gfx950 lane swaps):
+//   fold32(a, b): v_permlane32_swap pairs lane l with l+32 -> lanes 0-31 carry a, 32-63 carry b;
+//   fold16(a, b): v_permlane16_swap pairs 16-lane rows 0<->1, 2<->3 -> each row carries one value;
+//   row_sum15: DPP row_shr 1/2/4/8 -> the row total in the row's lane 15.
+// 6 + 3 swaps and 3 x 4 DPP adds replace 12 independent 64-lane reductions (72 DPP adds + 12
+// readlanes); the sums end in lanes 15/31/47/63 of three registers.
+__device__ inline float fold32(float a, float b) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ inline float fold16(float a, float b) {
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ inline float row_sum15(float v) {
     int x = __float_as_int(v);
     v += __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true));
     x = __float_as_int(v);
@@ -236,14 +249,8 @@ __device__ inline float wave_sum63(float v) {
     v += __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true));
     x = __float_as_int(v);
     v += __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true));
-    x = __float_as_int(v);
-    v += __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false));
-    x = __float_as_int(v);
-    v += __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false));
     return v;
 }
-
-__device__ inline float lane63(float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63)); }
 
 __global__ __launch_bounds__(256) void k_blend_bwd(const uint2 *__restrict__ ranges, const uint32_t *__restrict__ vals,
                                                    int W, int H, int gx, const float *bg,
@@ -343,23 +350,18 @@ __global__ __launch_bounds__(256) void k_blend_bwd(const uint2 *__restrict__ ran
                 v_cz = -0.5f * gdy * dy * dLdG;
                 v_op = G * dLda;
             }
-            float s_mx = lane63(wave_sum63(v_mx));
-            float s_my = lane63(wave_sum63(v_my));
-            float s_cx = lane63(wave_sum63(v_cx));
-            float s_cy = lane63(wave_sum63(v_cy));
-            float s_cz = lane63(wave_sum63(v_cz));
-            float s_op = lane63(wave_sum63(v_op));
-            float s_r = lane63(wave_sum63(v_r));
-            float s_g = lane63(wave_sum63(v_g));
-            float s_b = lane63(wave_sum63(v_b));
-            float s_d = lane63(wave_sum63(v_d));
-            float s_ax = lane63(wave_sum63(fabsf(v_mx)));
-            float s_ay = lane63(wave_sum63(fabsf(v_my)));
-            // spread the 12 sums over lanes 0..11 -> one 48-byte atomic wave-instruction
-            float val = lane == 0 ? s_mx : lane == 1 ? s_my : lane == 2 ? s_cx : lane == 3 ? s_cy
-                      : lane == 4 ? s_cz : lane == 5 ? s_op : lane == 6 ? s_r : lane == 7 ? s_g
-                      : lane == 8 ? s_b : lane == 9 ? s_d : lane == 10 ? s_ax : s_ay;
-            if (lane < ACC_STRIDE) atomicAdd(acc + (size_t)s_id[j] * ACC_STRIDE + lane, val);
+            // pairs (a, b) fold to rows [a_lo, b_lo, a_hi, b_hi] of w: row r of w_k holds field
+            // 4k + {0, 2, 1, 3}[r] (ACC_MX..ACC_DY order)
+            const float w0 = row_sum15(fold16(fold32(v_mx, v_my), fold32(v_cx, v_cy)));
+            const float w1 = row_sum15(fold16(fold32(v_cz, v_op), fold32(v_r, v_g)));
+            const float w2 = row_sum15(fold16(fold32(v_b, v_d), fold32(fabsf(v_mx), fabsf(v_my))));
+            if ((lane & 15) == 15) {
+                const int row = lane >> 4;
+                float *dst = acc + (size_t)s_id[j] * ACC_STRIDE + ((row & 1) << 1) + (row >> 1);
+                atomicAdd(dst, w0);
+                atomicAdd(dst + 4, w1);
+                atomicAdd(dst + 8, w2);
+            }
         }
     }
 }
