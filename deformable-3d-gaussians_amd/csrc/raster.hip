@@ -19,7 +19,9 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <map>
 #include <mutex>
+#include <tuple>
 #include <vector>
 
 #include "raster_kernels.h"
@@ -121,7 +123,7 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const float2 *__restri
                                                    const float4 *__restrict__ rgbd,
                                                    const uint32_t *__restrict__ offsets, int gx, int gy,
                                                    uint64_t *__restrict__ keys,
-                                                   uint32_t *__restrict__ vals) {
+                                                   uint32_t *__restrict__ vals, uint32_t cap) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P) return;
     int r = radii[i];
@@ -133,14 +135,19 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const float2 *__restri
     uint64_t db = (uint64_t)__float_as_uint(rgbd[i].w);
     for (int y = y0; y < y1; y++)
         for (int x = x0; x < x1; x++) {
-            keys[off] = ((uint64_t)(y * gx + x) << 32) | db;
-            vals[off] = (uint32_t)i;
+            if (off < cap) {  // speculative capacity: an overflowing launch is redone by the host
+                keys[off] = ((uint64_t)(y * gx + x) << 32) | db;
+                vals[off] = (uint32_t)i;
+            }
             off++;
         }
 }
 
-__global__ __launch_bounds__(256) void k_ranges(int L, const uint64_t *__restrict__ keys, uint2 *__restrict__ ranges) {
+// L (the pair count) is read on the device: the grid covers the speculative capacity
+__global__ __launch_bounds__(256) void k_ranges(const uint32_t *__restrict__ count, const uint64_t *__restrict__ keys,
+                                                uint2 *__restrict__ ranges) {
     int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int L = (int)*count;
     if (idx >= L) return;
     uint32_t t = (uint32_t)(keys[idx] >> 32);
     if (idx == 0) {
@@ -648,6 +655,8 @@ struct dgs_raster_ctx {
     hipEvent_t released = nullptr;
     hipStream_t last_stream = nullptr;
     bool pending_release = false;
+    uint32_t *h_total = nullptr;  // pinned host word: the num_rendered read-back (no staging copy)
+    hipEvent_t count_ev = nullptr;  // recorded after the read-back copy
 };
 
 namespace {
@@ -655,6 +664,75 @@ std::mutex g_pool_mu;
 std::vector<dgs_raster_ctx *> g_pool;
 
 size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
+
+// hipcub temp-storage sizes, cached per (device, size class): the size queries cost tens of us of
+// host time each inside the num_rendered sync window. Sizes are queried for the class's upper end
+// (temp storage grows monotonically with the item count).
+std::mutex g_tmp_mu;
+std::map<std::tuple<int, int, int, int>, size_t> g_tmp_sizes;  // (kind, device, class, end_bit)
+
+int size_class(int n) {  // 1/16-octave classes
+    if (n <= 4096) return 0;
+    int hb = 31 - __builtin_clz((unsigned)n);
+    int frac = (int)(((unsigned long long)n << 4 >> hb) & 15);
+    return hb * 16 + frac + 1;
+}
+int class_upper(int cls) {
+    if (cls == 0) return 4096;
+    int hb = (cls - 1) / 16, frac = (cls - 1) % 16;
+    unsigned long long v = ((16ull + frac + 1) << hb) >> 4;
+    return v > 0x7fffffffull ? 0x7fffffff : (int)v;
+}
+
+// Speculative pair capacity per device: binning is launched for this many pairs before the host
+// knows num_rendered, so the CPU does not drain the GPU queue at the read-back (it waits on an
+// event recorded right after the scan while duplicate/sort/blend run). A count above the capacity
+// re-runs binning with a grown capacity (results are always exact).
+std::mutex g_cap_mu;
+std::map<int, int> g_pair_cap;
+
+int grown_cap(long long nr) {
+    long long c = nr + nr / 8 + 65536;
+    return (int)std::min<long long>(c, 0x7fffffffLL);
+}
+
+int pair_cap_get(int device) {
+    std::lock_guard<std::mutex> lk(g_cap_mu);
+    auto it = g_pair_cap.find(device);
+    return it == g_pair_cap.end() ? 0 : it->second;
+}
+
+void pair_cap_observe(int device, int nr) {
+    std::lock_guard<std::mutex> lk(g_cap_mu);
+    int &c = g_pair_cap[device];
+    const int want = grown_cap(nr);
+    if (want > c || (long long)nr * 2 < c) c = want;  // grow at once; shrink when far above
+}
+
+hipError_t scan_tmp_bytes(int device, int P, hipStream_t stream, size_t &bytes) {
+    const int cls = size_class(P);
+    std::lock_guard<std::mutex> lk(g_tmp_mu);
+    auto key = std::make_tuple(0, device, cls, 0);
+    auto it = g_tmp_sizes.find(key);
+    if (it != g_tmp_sizes.end()) { bytes = it->second; return hipSuccess; }
+    hipError_t e = hipcub::DeviceScan::InclusiveSum(nullptr, bytes, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                                    class_upper(cls), stream);
+    if (e == hipSuccess) g_tmp_sizes[key] = bytes;
+    return e;
+}
+
+hipError_t sort_tmp_bytes(int device, int n, int end_bit, hipStream_t stream, size_t &bytes) {
+    const int cls = size_class(n);
+    std::lock_guard<std::mutex> lk(g_tmp_mu);
+    auto key = std::make_tuple(1, device, cls, end_bit);
+    auto it = g_tmp_sizes.find(key);
+    if (it != g_tmp_sizes.end()) { bytes = it->second; return hipSuccess; }
+    hipcub::DoubleBuffer<uint64_t> kb(nullptr, nullptr);
+    hipcub::DoubleBuffer<uint32_t> vb(nullptr, nullptr);
+    hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, kb, vb, class_upper(cls), 0, end_bit, stream);
+    if (e == hipSuccess) g_tmp_sizes[key] = bytes;
+    return e;
+}
 
 int bits_for(uint32_t n) {
     int b = 0;
@@ -688,6 +766,58 @@ dgs_raster_ctx *ctx_acquire(int device, hipStream_t stream) {
     return c;
 }
 }  // namespace
+
+// Binning for `cap` pairs (>= num_rendered, or the speculative capacity) + the blend: key buffer
+// pre-filled with all-ones (past every tile id in the sorted bits, so the unused tail sorts last and
+// leaves the stable order of the real pairs untouched), bounded duplicate, radix sort of cap items,
+// ranges from the device-side count, forward blend.
+static int bin_and_blend(dgs_raster_ctx *c, int cap, int P, int device, hipStream_t stream, bool dbg, float *out_color,
+                         float *out_depth) {
+    const int T = c->gx * c->gy;
+    DGS_HIP_CHECK(hipMemsetAsync(c->ranges, 0, 8ull * T, stream));
+    if (cap > 0) {
+        const int end_bit = 32 + bits_for((uint32_t)T);
+        size_t sort_tmp = 0;
+        DGS_HIP_CHECK(sort_tmp_bytes(device, cap, end_bit, stream, sort_tmp));
+        size_t o_k0 = 0, o_k1 = align_up(8ull * cap), o_v0 = align_up(o_k1 + 8ull * cap),
+               o_v1 = align_up(o_v0 + 4ull * cap), o_t = align_up(o_v1 + 4ull * cap);
+        if (int rc = c->bin.ensure(o_t + sort_tmp + 256)) return rc;
+        char *b = (char *)c->bin.p;
+        uint64_t *k0 = (uint64_t *)(b + o_k0), *k1 = (uint64_t *)(b + o_k1);
+        uint32_t *v0 = (uint32_t *)(b + o_v0), *v1 = (uint32_t *)(b + o_v1);
+        {
+            ScopedTimer tm("duplicate", stream);
+            DGS_HIP_CHECK(hipMemsetAsync(k0, 0xff, 8ull * cap, stream));
+            hipLaunchKernelGGL(k_duplicate, dim3(div_up(P, 256)), dim3(256), 0, stream, P, c->xy, c->radii, c->rgbd,
+                               c->offsets, c->gx, c->gy, k0, v0, (uint32_t)cap);
+        }
+        DGS_LAUNCH_CHECK("k_duplicate", dbg, stream);
+        hipcub::DoubleBuffer<uint64_t> kbuf(k0, k1);
+        hipcub::DoubleBuffer<uint32_t> vbuf(v0, v1);
+        {
+            ScopedTimer tm("sort", stream);
+            DGS_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(b + o_t, sort_tmp, kbuf, vbuf, cap, 0, end_bit, stream));
+        }
+        c->keys = kbuf.Current();
+        c->vals = vbuf.Current();
+        {
+            ScopedTimer tm("ranges", stream);
+            hipLaunchKernelGGL(k_ranges, dim3(div_up(cap, 256)), dim3(256), 0, stream, c->offsets + (P - 1), c->keys,
+                               c->ranges);
+        }
+        DGS_LAUNCH_CHECK("k_ranges", dbg, stream);
+    } else {
+        c->keys = nullptr;
+        c->vals = nullptr;
+    }
+    {
+        ScopedTimer tm("blend_fwd", stream);
+        hipLaunchKernelGGL(k_blend_fwd, dim3(T), dim3(TILE_PIX), 0, stream, c->ranges, c->vals, c->W, c->H, c->gx, c->xy,
+                           c->conic_o, c->rgbd, c->s.bg, c->final_T, c->n_contrib, out_color, out_depth);
+    }
+    DGS_LAUNCH_CHECK("k_blend_fwd", dbg, stream);
+    return DGS_OK;
+}
 
 extern "C" int dgs_raster_forward(const dgs_raster_settings *s, int P, int M, const float *means3D,
                                   const float *shs, const float *colors_precomp, const float *opacities,
@@ -737,7 +867,7 @@ extern "C" int dgs_raster_forward(const dgs_raster_settings *s, int P, int M, co
     size_t off_xy = 0, off_co = align_up(off_xy + 8ull * P), off_cd = align_up(off_co + 16ull * P),
            off_t = align_up(off_cd + 16ull * P), off_o = align_up(off_t + 4ull * P), off_cl = align_up(off_o + 4ull * P);
     size_t scan_tmp = 0;
-    if (P > 0) DGS_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, scan_tmp, (uint32_t *)nullptr, (uint32_t *)nullptr, P, stream));
+    if (P > 0) DGS_HIP_CHECK(scan_tmp_bytes(device, P, stream, scan_tmp));
     size_t off_st = align_up(off_cl + P);
     if (int rc = c->geom.ensure(off_st + scan_tmp + 256)) { ctx_out[0] = nullptr; delete c; return rc; }
     char *g = (char *)c->geom.p;
@@ -767,54 +897,30 @@ extern "C" int dgs_raster_forward(const dgs_raster_settings *s, int P, int M, co
         }
         DGS_LAUNCH_CHECK("k_preprocess", dbg, stream);
         DGS_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(g + off_st, scan_tmp, c->tiles, c->offsets, P, stream));
-        uint32_t total = 0;
-        DGS_HIP_CHECK(hipMemcpyAsync(&total, c->offsets + (P - 1), 4, hipMemcpyDeviceToHost, stream));
-        DGS_HIP_CHECK(hipStreamSynchronize(stream));
-        nr = (int)total;
+        if (!c->h_total) DGS_HIP_CHECK(hipHostMalloc((void **)&c->h_total, sizeof(uint32_t), hipHostMallocDefault));
+        if (!c->count_ev) DGS_HIP_CHECK(hipEventCreateWithFlags(&c->count_ev, hipEventDisableTiming));
+        DGS_HIP_CHECK(hipMemcpyAsync(c->h_total, c->offsets + (P - 1), 4, hipMemcpyDeviceToHost, stream));
+        DGS_HIP_CHECK(hipEventRecord(c->count_ev, stream));
+        int cap = pair_cap_get(device);
+        const bool speculative = cap > 0 && !dbg;
+        if (!speculative) {
+            DGS_HIP_CHECK(hipEventSynchronize(c->count_ev));
+            nr = (int)*c->h_total;
+            cap = nr;
+        }
+        if (int rc = bin_and_blend(c, cap, P, device, stream, dbg, out_color, out_depth)) return rc;
+        if (speculative) {
+            DGS_HIP_CHECK(hipEventSynchronize(c->count_ev));
+            nr = (int)*c->h_total;
+            if (nr > cap) {  // overflow: redo binning + blend at the exact size
+                if (int rc = bin_and_blend(c, nr, P, device, stream, dbg, out_color, out_depth)) return rc;
+            }
+        }
+        pair_cap_observe(device, nr);
+    } else {
+        if (int rc = bin_and_blend(c, 0, P, device, stream, dbg, out_color, out_depth)) return rc;
     }
     c->num_rendered = nr;
-    DGS_HIP_CHECK(hipMemsetAsync(c->ranges, 0, 8ull * T, stream));
-    if (nr > 0) {
-        const int end_bit = 32 + bits_for((uint32_t)T);
-        size_t sort_tmp = 0;
-        hipcub::DoubleBuffer<uint64_t> kb(nullptr, nullptr);
-        hipcub::DoubleBuffer<uint32_t> vb(nullptr, nullptr);
-        DGS_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, kb, vb, nr, 0, end_bit, stream));
-        size_t o_k0 = 0, o_k1 = align_up(8ull * nr), o_v0 = align_up(o_k1 + 8ull * nr), o_v1 = align_up(o_v0 + 4ull * nr),
-               o_t = align_up(o_v1 + 4ull * nr);
-        if (int rc = c->bin.ensure(o_t + sort_tmp + 256)) { delete c; return rc; }
-        char *b = (char *)c->bin.p;
-        uint64_t *k0 = (uint64_t *)(b + o_k0), *k1 = (uint64_t *)(b + o_k1);
-        uint32_t *v0 = (uint32_t *)(b + o_v0), *v1 = (uint32_t *)(b + o_v1);
-        {
-            ScopedTimer tm("duplicate", stream);
-            hipLaunchKernelGGL(k_duplicate, dim3(div_up(P, 256)), dim3(256), 0, stream, P, c->xy, out_radii, c->rgbd,
-                               c->offsets, c->gx, c->gy, k0, v0);
-        }
-        DGS_LAUNCH_CHECK("k_duplicate", dbg, stream);
-        hipcub::DoubleBuffer<uint64_t> kbuf(k0, k1);
-        hipcub::DoubleBuffer<uint32_t> vbuf(v0, v1);
-        {
-            ScopedTimer tm("sort", stream);
-            DGS_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(b + o_t, sort_tmp, kbuf, vbuf, nr, 0, end_bit, stream));
-        }
-        c->keys = kbuf.Current();
-        c->vals = vbuf.Current();
-        {
-            ScopedTimer tm("ranges", stream);
-            hipLaunchKernelGGL(k_ranges, dim3(div_up(nr, 256)), dim3(256), 0, stream, nr, c->keys, c->ranges);
-        }
-        DGS_LAUNCH_CHECK("k_ranges", dbg, stream);
-    } else {
-        c->keys = nullptr;
-        c->vals = nullptr;
-    }
-    {
-        ScopedTimer tm("blend_fwd", stream);
-        hipLaunchKernelGGL(k_blend_fwd, dim3(T), dim3(TILE_PIX), 0, stream, c->ranges, c->vals, c->W, c->H, c->gx, c->xy,
-                           c->conic_o, c->rgbd, s->bg, c->final_T, c->n_contrib, out_color, out_depth);
-    }
-    DGS_LAUNCH_CHECK("k_blend_fwd", dbg, stream);
     *ctx_out = c;
     if (num_rendered) *num_rendered = nr;
     return DGS_OK;
@@ -878,6 +984,7 @@ extern "C" void dgs_raster_ctx_free(dgs_raster_ctx *c) {
         g_pool.push_back(c);
     } else {
         c->geom.release(); c->bin.release(); c->img.release(); c->acc.release(); c->tmp.release();
+        if (c->h_total) (void)hipHostFree(c->h_total);
         delete c;
     }
 }

@@ -27,6 +27,14 @@ class RasterSettings(ctypes.Structure):
     ]
 
 
+class AdamTensor(ctypes.Structure):
+    """dgs_adam_tensor (include/dgs.h)."""
+    _fields_ = [
+        ("param", P), ("grad", P), ("exp_avg", P), ("exp_avg_sq", P), ("numel", ctypes.c_int64),
+        ("step_size", F), ("bc2_sqrt", F),
+    ]
+
+
 _SIGS = {
     "dgs_last_error": ([], ctypes.c_char_p),
     "dgs_version": ([], ctypes.c_char_p),
@@ -49,6 +57,9 @@ _SIGS = {
     "dgs_l1_ssim_scratch_floats": ([I, I, I], SZ),
     "dgs_l1_ssim_forward": ([I, I, I, P, P, F, P, P, P], I),
     "dgs_l1_ssim_backward": ([I, I, I, P, P, F, P, P, P, P], I),
+    "dgs_adam_step": ([I, ctypes.POINTER(AdamTensor), ctypes.c_double, ctypes.c_double, ctypes.c_double, P], I),
+    "dgs_gaussian_inputs_forward": ([I, I] + [P] * 7 + [I] + [P] * 5 + [P], I),
+    "dgs_gaussian_inputs_backward": ([I, I] + [P] * 15 + [I, P], I),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -9,7 +9,8 @@ import os
 import torch
 
 from .deform_network import DeformNetwork, DeformNetworkBaseline
-from .general import adam_kwargs as _adam_kw, get_expon_lr_func
+from .adam import Adam
+from .general import get_expon_lr_func
 
 
 def searchForMaxIteration(folder):
@@ -34,7 +35,7 @@ class DeformModelBaseline:
     def train_setting(self, training_args):
         l = [{'params': list(self.deform.parameters()),
               'lr': training_args.position_lr_init * self.spatial_lr_scale, "name": "deform"}]
-        self.optimizer = torch.optim.Adam(l, lr=0.0, eps=1e-15, **_adam_kw(l))
+        self.optimizer = Adam(l, lr=0.0, eps=1e-15)
         self.deform_scheduler_args = get_expon_lr_func(lr_init=training_args.position_lr_init * self.spatial_lr_scale,
                                                        lr_final=training_args.position_lr_final,
                                                        lr_delay_mult=training_args.position_lr_delay_mult,

@@ -15,7 +15,7 @@ from torch import nn
 
 from . import _lib
 from .general import build_rotation, get_expon_lr_func, inverse_sigmoid, strip_symmetric, build_scaling_rotation
-from .general import adam_kwargs as _adam_kw
+from .adam import Adam
 from .sh import RGB2SH
 
 
@@ -130,7 +130,7 @@ class GaussianModel:
             {'params': [self._scaling], 'lr': training_args.scaling_lr * self.spatial_lr_scale, "name": "scaling"},
             {'params': [self._rotation], 'lr': training_args.rotation_lr, "name": "rotation"},
         ]
-        self.optimizer = torch.optim.Adam(l, lr=0.0, eps=1e-15, **_adam_kw(l))
+        self.optimizer = Adam(l, lr=0.0, eps=1e-15)
         self.xyz_scheduler_args = get_expon_lr_func(lr_init=training_args.position_lr_init * self.spatial_lr_scale,
                                                     lr_final=training_args.position_lr_final * self.spatial_lr_scale,
                                                     lr_delay_mult=training_args.position_lr_delay_mult,

@@ -53,12 +53,3 @@ def build_rotation(r):
 
 def build_scaling_rotation(s, r):
     return build_rotation(r) * s[:, None, :]
-
-
-def adam_kwargs(param_groups):
-    """torch.optim.Adam options for the reference's Adam(lr=0, eps=1e-15) groups: the single-launch
-    fused implementation when every parameter is a GPU tensor (same update rule)."""
-    ps = [p for g in param_groups for p in g["params"]]
-    if ps and all(p.is_cuda for p in ps):
-        return {"fused": True}
-    return {}

@@ -2,7 +2,10 @@
 
 The rasterizer underneath is this repo's diff_gaussian_rasterization (libdgs_hip.so). Glue math
 (means3D = xyz + d_xyz or the 6-DoF transform, scales = exp(_scaling) + d_scale, rotations =
-normalize(_rotation) + d_rot without re-normalisation, opacity = sigmoid) is unchanged.
+normalize(_rotation) + d_rot without re-normalisation, opacity = sigmoid) is unchanged; on the
+training path (no 6-DoF, SHs and covariance in the rasterizer, deltas straight from the fused
+deformation network or absent) it runs as one HIP launch each way (dgs_gaussian_inputs_*), whose
+backward writes the deformation network's (N, 10) output gradient directly.
 """
 import math
 
@@ -10,8 +13,82 @@ import torch
 
 from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
 
+from . import _lib
 from .rigid import from_homogenous, to_homogenous
 from .sh import eval_sh
+
+
+class _GaussianInputs(torch.autograd.Function):
+    """(xyz, f_dc, f_rest, scaling, rotation, opacity, deform (N, 10) | None) ->
+    (means3D, shs, opacities, scales, rotations) of gaussian_renderer/__init__.py:70-112."""
+
+    @staticmethod
+    def forward(ctx, xyz, f_dc, f_rest, scaling, rotation, opacity, deform):
+        lib = _lib.load()
+        P = xyz.shape[0]
+        M_rest = f_rest.shape[1]
+        dev = xyz.device
+        e = lambda *shape: torch.empty(shape, dtype=torch.float32, device=dev)  # noqa: E731
+        means3D, shs, scales, rots, opac = e(P, 3), e(P, 1 + M_rest, 3), e(P, 3), e(P, 4), e(P, 1)
+        ds = deform.stride(0) if deform is not None else 0
+        _lib.check(lib.dgs_gaussian_inputs_forward(
+            P, M_rest, _lib.ptr(xyz), _lib.ptr(f_dc), _lib.ptr(f_rest), _lib.ptr(scaling), _lib.ptr(rotation),
+            _lib.ptr(opacity), _lib.ptr(deform), ds, _lib.ptr(means3D), _lib.ptr(shs), _lib.ptr(scales),
+            _lib.ptr(rots), _lib.ptr(opac), _lib.stream_ptr(dev)), "gaussian_inputs_forward")
+        ctx.save_for_backward(scaling, rotation, opacity)
+        ctx.M_rest = M_rest
+        ctx.has_deform = deform is not None
+        return means3D, shs, opac, scales, rots
+
+    @staticmethod
+    def backward(ctx, g_means, g_shs, g_opac, g_scales, g_rots):
+        lib = _lib.load()
+        scaling, rotation, opacity = ctx.saved_tensors
+        P, M_rest = scaling.shape[0], ctx.M_rest
+        dev = scaling.device
+        z = lambda t, *shape: (torch.zeros(shape, dtype=torch.float32, device=dev) if t is None  # noqa: E731
+                               else t.contiguous())
+        g_means, g_shs, g_opac = z(g_means, P, 3), z(g_shs, P, 1 + M_rest, 3), z(g_opac, P, 1)
+        g_scales, g_rots = z(g_scales, P, 3), z(g_rots, P, 4)
+        need = ctx.needs_input_grad
+        e = lambda ok, *shape: torch.empty(shape, dtype=torch.float32, device=dev) if ok else None  # noqa: E731
+        o_xyz, o_dc, o_rest = e(need[0], P, 3), e(need[1], P, 1, 3), e(need[2], P, M_rest, 3)
+        o_sc, o_rot, o_op = e(need[3], P, 3), e(need[4], P, 4), e(need[5], P, 1)
+        o_def = e(ctx.has_deform and need[6], P, 10)
+        _lib.check(lib.dgs_gaussian_inputs_backward(
+            P, M_rest, _lib.ptr(scaling), _lib.ptr(rotation), _lib.ptr(opacity), _lib.ptr(g_means), _lib.ptr(g_shs),
+            _lib.ptr(g_scales), _lib.ptr(g_rots), _lib.ptr(g_opac), _lib.ptr(o_xyz), _lib.ptr(o_dc), _lib.ptr(o_rest),
+            _lib.ptr(o_sc), _lib.ptr(o_rot), _lib.ptr(o_op), _lib.ptr(o_def), 10, _lib.stream_ptr(dev)),
+            "gaussian_inputs_backward")
+        return o_xyz, o_dc, o_rest, o_sc, o_rot, o_op, o_def
+
+
+def _fused_deform_rows(pc, d_xyz, d_rotation, d_scaling):
+    """The (N, 10) deformation output the three deltas are column views of, 0 for no deformation,
+    or None when the deltas have any other form (then the generic torch glue runs)."""
+    if not torch.is_tensor(d_xyz) and not torch.is_tensor(d_rotation) and not torch.is_tensor(d_scaling):
+        return 0 if (d_xyz == 0 and d_rotation == 0 and d_scaling == 0) else None
+    if not (torch.is_tensor(d_xyz) and torch.is_tensor(d_rotation) and torch.is_tensor(d_scaling)):
+        return None
+    b = d_xyz._base
+    if b is None or d_rotation._base is not b or d_scaling._base is not b:
+        return None
+    N = pc._xyz.shape[0]
+    if b.dim() != 2 or tuple(b.shape) != (N, 10) or not b.is_contiguous() or b.dtype != torch.float32:
+        return None
+    off = b.storage_offset()
+    for t, col, w in ((d_xyz, 0, 3), (d_rotation, 3, 4), (d_scaling, 7, 3)):
+        if tuple(t.shape) != (N, w) or t.stride() != (10, 1) or t.storage_offset() - off != col:
+            return None
+    return b
+
+
+def _fused_ok(pc):
+    ts = (pc._xyz, pc._features_dc, pc._features_rest, pc._scaling, pc._rotation, pc._opacity)
+    return (all(t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() for t in ts)
+            and pc._features_dc.dim() == 3 and pc._features_dc.shape[1] == 1
+            and pc.scaling_activation is torch.exp and pc.opacity_activation is torch.sigmoid
+            and pc.rotation_activation is torch.nn.functional.normalize)
 
 
 def render(viewpoint_camera, pc, pipe, bg_color, d_xyz, d_rotation, d_scaling, is_6dof=False,
@@ -34,6 +111,20 @@ def render(viewpoint_camera, pc, pipe, bg_color, d_xyz, d_rotation, d_scaling, i
         sh_degree=pc.active_sh_degree, campos=viewpoint_camera.camera_center, prefiltered=False,
         debug=getattr(pipe, "debug", False))
     rasterizer = GaussianRasterizer(raster_settings=raster_settings)
+    rows = None
+    if (not direct_compute and not is_6dof and override_color is None and not getattr(pipe, "compute_cov3D_python", False)
+            and not getattr(pipe, "convert_SHs_python", False) and _fused_ok(pc)):
+        rows = _fused_deform_rows(pc, d_xyz, d_rotation, d_scaling)
+    if rows is not None:
+        means3D, shs, opacity, scales, rotations = _GaussianInputs.apply(
+            pc._xyz, pc._features_dc, pc._features_rest, pc._scaling, pc._rotation, pc._opacity,
+            rows if torch.is_tensor(rows) else None)
+        rendered_image, radii, depth = rasterizer(
+            means3D=means3D, means2D=screenspace_points, means2D_densify=screenspace_points_densify, shs=shs,
+            colors_precomp=None, opacities=opacity, scales=scales, rotations=rotations, cov3D_precomp=None)
+        return {"render": rendered_image, "viewspace_points": screenspace_points,
+                "viewspace_points_densify": screenspace_points_densify, "visibility_filter": radii > 0,
+                "radii": radii, "depth": depth}
     if direct_compute:
         means3D = d_xyz
     elif is_6dof:

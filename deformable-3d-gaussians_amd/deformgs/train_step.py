@@ -3,6 +3,7 @@ harness): deform -> render -> 0.8*L1 + 0.2*(1-SSIM) -> backward [-> grad all-red
 """
 import torch
 
+from .adam import step_all
 from .loss import l1_ssim_loss
 from .renderer import render
 
@@ -25,10 +26,9 @@ def forward_backward(gaussians, deform, cam, gt_image, pipe, background, is_6dof
 
 
 def optimizer_step(gaussians, deform, iteration):
-    """train_baseline.py:176-182."""
-    gaussians.optimizer.step()
+    """train_baseline.py:176-182 (both optimizers' Adam updates in one HIP launch)."""
+    step_all(gaussians.optimizer, deform.optimizer)
     gaussians.update_learning_rate(iteration)
-    deform.optimizer.step()
     gaussians.optimizer.zero_grad(set_to_none=True)
     deform.optimizer.zero_grad()
     deform.update_learning_rate(iteration)

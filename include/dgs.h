@@ -18,6 +18,11 @@
  *                           (utils/time_utils.py:56-127, called via scene/deform_model.py:323-324)
  *   dgs_knn_dist2        <- simple_knn._C.distCUDA2 (scene/gaussian_model.py:20,105-106)
  *   dgs_l1_ssim_*        <- l1_loss + ssim (utils/loss_utils.py:18-73) as used at train_baseline.py:126-127
+ *   dgs_gaussian_inputs_* <- the glue of render() (gaussian_renderer/__init__.py:70-112: xyz + d_xyz,
+ *                           exp(scaling) + d_scaling, normalize(rotation) + d_rotation, sigmoid(opacity),
+ *                           cat(features_dc, features_rest)) and its autograd
+ *   dgs_adam_step        <- torch.optim.Adam(..., eps=1e-15).step() of scene/gaussian_model.py:132 and
+ *                           scene/deform_model.py:266 (train_baseline.py:176-182)
  */
 #ifndef DGS_H
 #define DGS_H
@@ -129,6 +134,39 @@ int dgs_l1_ssim_backward(int C, int H, int W, const float *img, const float *gt,
 
 /* ---- simple-knn replacement: mean squared distance to the 3 nearest neighbours ---- */
 int dgs_knn_dist2(int P, const float *points, float *dist2, void *stream);
+
+/* ---- rasterizer inputs of render() (gaussian_renderer/__init__.py:70-112, gaussian_model.py:39-50) ----
+ * means3D = xyz + d_xyz; scales = exp(scaling) + d_scaling; rotations = normalize(rotation) + d_rotation;
+ * opacities = sigmoid(opacity); shs (P, 1 + M_rest, 3) = cat(features_dc (P,1,3), features_rest (P,M_rest,3)).
+ * deform: rows of deform_stride floats holding [d_xyz(3) d_rotation(4) d_scaling(3)] (the deformation
+ * network output), or NULL for no deformation. Backward: g_* outputs may be NULL (not needed);
+ * g_deform receives the same row layout. */
+int dgs_gaussian_inputs_forward(int P, int M_rest, const float *xyz, const float *f_dc, const float *f_rest,
+                                const float *scaling, const float *rotation, const float *opacity,
+                                const float *deform, int deform_stride, float *means3D, float *shs,
+                                float *scales, float *rotations, float *opacities, void *stream);
+int dgs_gaussian_inputs_backward(int P, int M_rest, const float *scaling, const float *rotation,
+                                 const float *opacity, const float *d_means3D, const float *d_shs,
+                                 const float *d_scales, const float *d_rotations, const float *d_opacities,
+                                 float *g_xyz, float *g_dc, float *g_rest, float *g_scaling, float *g_rotation,
+                                 float *g_opacity, float *g_deform, int deform_stride, void *stream);
+
+/* ---- Adam over many tensors in one launch (torch.optim.Adam, amsgrad/weight_decay off) ----
+ * Per tensor (host array of n descriptors, device data pointers):
+ *   m = lerp(m, g, 1 - beta1); v = beta2 v + (1 - beta2) g^2;
+ *   p -= step_size * m / (sqrt(v) / bc2_sqrt + eps)
+ * with step_size = lr / (1 - beta1^t) and bc2_sqrt = sqrt(1 - beta2^t) computed by the caller;
+ * 1 - beta1 and 1 - beta2 are formed in double and rounded to float (torch's scalar handling). */
+typedef struct dgs_adam_tensor {
+    float *param;
+    const float *grad;
+    float *exp_avg;
+    float *exp_avg_sq;
+    int64_t numel;
+    float step_size;
+    float bc2_sqrt;
+} dgs_adam_tensor;
+int dgs_adam_step(int n, const dgs_adam_tensor *tensors, double beta1, double beta2, double eps, void *stream);
 
 #ifdef __cplusplus
 }
