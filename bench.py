@@ -25,6 +25,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense FP32 matrix peak (spec)
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")  # tools/pmc_traffic.py output
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak (spec)
 
 # algorithmic multiply-accumulates per point of the blender network
@@ -238,6 +239,16 @@ def main():
             roofline = {"bound": "hbm", "kernel": name, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "avg_launch_ms": avg_s * 1e3,
                         "launches": n}
+    if roofline is not None and os.path.exists(PMC_TRAFFIC):
+        # HBM bytes per launch of the same kernel from the committed rocprofv3 --pmc passes
+        # (FETCH_SIZE doubled for gfx950 + WRITE_SIZE; tools/gpu_prof.sh, tools/pmc_traffic.py)
+        try:
+            t = json.load(open(PMC_TRAFFIC)).get(roofline["kernel"])
+            if t:
+                roofline["traffic"] = t["traffic_bytes"]
+                roofline["traffic_source"] = "profiles/pmc_traffic.json (" + t.get("source", "?") + ")"
+        except (OSError, ValueError, KeyError):
+            pass
     value = world * args.steps / elapsed
     result = {
         "metric": "train iters/s (deform+raster fwd+bwd), 100k Gaussians @ 800x800",
