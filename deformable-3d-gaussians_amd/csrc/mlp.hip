@@ -255,9 +255,47 @@ __global__ __launch_bounds__(256) void k_pack_map(const int *__restrict__ map, P
     packed[i] = c < 0 ? 0.f : src.p[c >> PACK_SHIFT][c & ((1 << PACK_SHIFT) - 1)];
 }
 
+#ifdef DGS_MLP_PROFILE  // diagnostic build only (tools/mlp_phase.cpp): per-phase s_memtime stamps
+__device__ unsigned long long *dgs_mlp_prof;
+#define DGS_STAMP(k)                                                                               \
+    do {                                                                                           \
+        if (threadIdx.x == 0) dgs_mlp_prof[blockIdx.x * 256 + (k)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+// per-wave: lane 0 of every wave records (k is per wave), plus the wave's SIMD (HW_ID bits 5:4)
+#define DGS_WSTAMP(k)                                                                              \
+    do {                                                                                           \
+        if ((threadIdx.x & 63) == 0)                                                               \
+            dgs_mlp_prof[blockIdx.x * 256 + (k) + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#define DGS_WSIMD(k)                                                                               \
+    do {                                                                                           \
+        if ((threadIdx.x & 63) == 0)                                                               \
+            dgs_mlp_prof[blockIdx.x * 256 + (k) + (threadIdx.x >> 6)] =                              \
+                (__builtin_amdgcn_s_getreg(0xF804) >> 4) & 3;                                      \
+    } while (0)
+#else
+#define DGS_WSTAMP(k) \
+    do {              \
+    } while (0)
+#define DGS_WSIMD(k) \
+    do {             \
+    } while (0)
+#define DGS_STAMP(k) \
+    do {             \
+    } while (0)
+#endif
+
 // ------------------------------------------------------------------------------------------------
 // device GEMM pieces
 // ------------------------------------------------------------------------------------------------
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS traffic (lgkmcnt 0) but not
+// for its global stores. __syncthreads() also waits vmcnt(0) (release fence), which parked every
+// wave ~5 us per layer on the saved-activation stores. No wave of k_mlp_* reads global memory
+// another wave of the block wrote.
+__device__ inline void lds_barrier() {
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // gfx9 encoding: vmcnt 63, expcnt 7, lgkmcnt 0
+    __builtin_amdgcn_s_barrier();
+}
 __device__ inline f32x16 zero16() {
     f32x16 z;
 #pragma unroll
@@ -267,94 +305,28 @@ __device__ inline f32x16 zero16() {
 
 #define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_32x32x2f32((a), (b), (c), 0, 0, 0)
 
-struct NoSide {
-    __device__ void operator()(int) const {}
-};
-
-// acc0/acc1 (m-tiles 0/1) += A[ntile] . X over chunks [c0, c1) of the LDS image starting at group g0.
-// The A fragments (1 KiB per wave-load) are prefetched two chunks ahead; side(i) runs once per chunk
-// (interleaved LDS->HBM stores of the previous layer's activations).
-template <class Side = NoSide>
-__device__ inline void gemm_2m(const float4 *__restrict__ Apk, int c0, int c1, const float4 *lds, int g0, int lane,
-                               f32x16 &acc0, f32x16 &acc1, Side side = Side()) {
-    const int h = lane >> 5, m = lane & 31;
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    // 4-deep register ring of A fragments: a fragment is waited for 4 chunks (~2k cycles) after
-    // its load was issued, so the interleaved activation stores (which share vmcnt with the loads
-    // on CDNA4) issued before it have long drained.
-    float4 r0 = (c0 < c1) ? Apk[c0 * 64 + lane] : z4;
-    float4 r1 = (c0 + 1 < c1) ? Apk[(c0 + 1) * 64 + lane] : z4;
-    float4 r2 = (c0 + 2 < c1) ? Apk[(c0 + 2) * 64 + lane] : z4;
-    float4 r3 = (c0 + 3 < c1) ? Apk[(c0 + 3) * 64 + lane] : z4;
-    auto step = [&](int c, float4 &slot) {
-        float4 a = slot;
-        if (c + 4 < c1) slot = Apk[(c + 4) * 64 + lane];
-        const float4 *grp = lds + (g0 + 2 * c + h) * BM;
-        float4 b0 = grp[m];
-        float4 b1 = grp[32 + m];
-        side(c - c0);
-        acc0 = MFMA(a.x, b0.x, acc0);
-        acc1 = MFMA(a.x, b1.x, acc1);
-        acc0 = MFMA(a.y, b0.y, acc0);
-        acc1 = MFMA(a.y, b1.y, acc1);
-        acc0 = MFMA(a.z, b0.z, acc0);
-        acc1 = MFMA(a.z, b1.z, acc1);
-        acc0 = MFMA(a.w, b0.w, acc0);
-        acc1 = MFMA(a.w, b1.w, acc1);
-    };
-    int c = c0;
-    for (; c + 4 <= c1; c += 4) {
-        step(c, r0);
-        step(c + 1, r1);
-        step(c + 2, r2);
-        step(c + 3, r3);
-    }
-    if (c < c1) step(c, r0);
-    if (c + 1 < c1) step(c + 1, r1);
-    if (c + 2 < c1) step(c + 2, r2);
-}
-
-// single m-tile variant (narrow K-split layers)
-template <class Side = NoSide>
-__device__ inline void gemm_1m(const float4 *__restrict__ Apk, int c0, int c1, const float4 *lds, int g0, int mt,
-                               int lane, f32x16 &acc, Side side = Side()) {
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int h = lane >> 5, m = lane & 31;
-    float4 p0 = (c0 < c1) ? Apk[c0 * 64 + lane] : z4;
-    float4 p1 = (c0 + 1 < c1) ? Apk[(c0 + 1) * 64 + lane] : z4;
-    for (int c = c0; c < c1; c++) {
-        float4 a = p0;
-        p0 = p1;
-        if (c + 2 < c1) p1 = Apk[(c + 2) * 64 + lane];
-        float4 b = lds[(g0 + 2 * c + h) * BM + mt * 32 + m];
-        side(c - c0);
-        acc = MFMA(a.x, b.x, acc);
-        acc = MFMA(a.y, b.y, acc);
-        acc = MFMA(a.z, b.z, acc);
-        acc = MFMA(a.w, b.w, acc);
-    }
-}
-
-// Deferred LDS -> HBM copy of up to two group ranges (activation rows [row0, row0 + 4ng) of a
-// feature-major [rows][Ns] array), issued a few float4 units per thread per GEMM chunk so the stores
-// drain under the next layer's MFMAs instead of in a store-only phase. Unit = 4 features x 1 point:
-// ds_read_b128 + 4 coalesced 256-B wave stores. Every range is a multiple of NTHR units.
+// Deferred LDS -> HBM copy of up to three group ranges of feature-major [rows][Ns] arrays (saved
+// activations in the forward, dZ in the backward). A unit = 4 features x 1 point: one
+// ds_read_b128 + 4 coalesced 256-B wave stores. The GEMMs issue a FIXED number of units per 4-chunk
+// group, straight-line, so the compiler's vmcnt bookkeeping (stores count on gfx9) is exact and the
+// A-fragment waits never wait for these stores; a unit past the end rewrites the last unit (same
+// data to the same address).
 struct Pending {
-    int g0a, nga, r0a, g0b, r0b;  // range a (and optional range b, placed after a)
-    int n, units, pos, per;
-    int total;  // float4 units over all ranges (per-thread rounds = ceil(total / NTHR))
-    __device__ void set1(int g, int ngr, int r0) {
-        n = 1; g0a = g; nga = ngr; r0a = r0;
-        total = ngr * BM;
-        units = div_up(total, NTHR); pos = 0;
+    int g0[3], r0[3], end[3];  // LDS group, output row, cumulative end (float4 units) per range
+    int n, pos, total;
+    __device__ void clear() {
+        n = 0; pos = 0; total = 0;
+        end[0] = end[1] = end[2] = 0x7fffffff;
+        g0[0] = g0[1] = g0[2] = 0;
+        r0[0] = r0[1] = r0[2] = 0;
     }
-    __device__ void add(int g, int ngr, int r0) {
-        if (n == 0) { set1(g, ngr, r0); return; }
-        g0b = g; r0b = r0; n = 2;
+    __device__ void add(int g, int ngr, int r) {
+        g0[n] = g; r0[n] = r;
         total += ngr * BM;
-        units = div_up(total, NTHR);
+        end[n] = total;
+        n++;
     }
-    __device__ void pace(int chunks) { per = chunks > 0 ? (units - pos + chunks - 1) / chunks : units - pos; }
+    __device__ void set1(int g, int ngr, int r) { clear(); add(g, ngr, r); }
 };
 
 struct PendingSide {
@@ -365,31 +337,140 @@ struct PendingSide {
     int p0, tid;
     __device__ void unit() const {
         Pending &Q = *q;
-        if (Q.pos >= Q.units) return;
-        int e = tid + NTHR * Q.pos;
+        int e = min(tid + NTHR * Q.pos, Q.total - 1);
         Q.pos++;
-        if (e >= Q.total) return;
-        const bool second = Q.n > 1 && e >= Q.nga * BM;
-        if (second) e -= Q.nga * BM;
-        const int g0 = second ? Q.g0b : Q.g0a;
-        const int r0 = second ? Q.r0b : Q.r0a;
+        const bool k1 = e >= Q.end[0], k2 = e >= Q.end[1];
+        const int base = k2 ? Q.end[1] : (k1 ? Q.end[0] : 0);
+        const int g0 = k2 ? Q.g0[2] : (k1 ? Q.g0[1] : Q.g0[0]);
+        const int r0 = k2 ? Q.r0[2] : (k1 ? Q.r0[1] : Q.r0[0]);
+        e -= base;
         const int gi = e / BM, m = e % BM;
-        float4 v = lds[(g0 + gi) * BM + m];
+        const float4 v = lds[(g0 + gi) * BM + m];
         float *d = dst + (size_t)(r0 + 4 * gi) * Ns + p0 + m;
         d[0] = v.x;
         d[Ns] = v.y;
         d[2 * Ns] = v.z;
         d[3 * Ns] = v.w;
     }
-    __device__ void operator()(int) const {
-        for (int k = 0; k < q->per; k++) unit();
-    }
     __device__ void flush() const {
-        while (q->pos < q->units) unit();
-        q->n = 0;
-        q->units = q->pos = q->total = 0;
+        while (q->pos * NTHR < q->total) unit();
+        q->clear();
     }
 };
+
+struct NoSide {
+    __device__ void unit() const {}
+    __device__ void flush() const {}
+};
+
+struct NoPre {
+    __device__ void operator()() const {}
+};
+
+// acc0/acc1 (m-tiles 0/1) += A . X over NCH chunks starting at chunk c0 of the A image and of the
+// LDS image at group g0 (chunk c = groups g0 + 2c + h). Fully unrolled straight-line schedule (no
+// loop back-edge, so no register rotation and exact compiler vmcnt/lgkmcnt bookkeeping): per chunk
+// the A fragment 4 chunks ahead (4-deep ring, issued before this chunk's MFMAs), the next chunk's B
+// (double-buffered ds_read_b128), 8 MFMAs, and on every 4th chunk SPG side units. pre() runs after
+// the A prologue (its global loads are younger than the first fragments).
+template <int NCH, int SPG, class Side, class Pre = NoPre>
+__device__ inline void gemm_2m(const float4 *__restrict__ Apk, int c0, const float4 *lds, int g0, int lane,
+                               f32x16 &acc0, f32x16 &acc1, const Side &side, Pre pre = Pre(), int g_chunk_stamp = -1) {
+    static_assert(NCH >= 1, "empty GEMM");
+    const int h = lane >> 5, m = lane & 31;
+    const float4 *Ap = Apk + c0 * 64 + lane;
+    const float4 *Bp = lds + (g0 + 2 * c0 + h) * BM + m;
+    float4 ring[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        if (k < NCH) ring[k] = Ap[k * 64];
+    pre();
+    float4 bx[2], by[2];
+    bx[0] = Bp[0];
+    by[0] = Bp[32];
+#pragma unroll
+    for (int k = 0; k < NCH; k++) {
+        const float4 a = ring[k & 3];
+        if (k + 4 < NCH) ring[k & 3] = Ap[(k + 4) * 64];
+        if (k + 1 < NCH) {
+            bx[(k + 1) & 1] = Bp[2 * (k + 1) * BM];
+            by[(k + 1) & 1] = Bp[2 * (k + 1) * BM + 32];
+        }
+        const float4 b0 = bx[k & 1], b1 = by[k & 1];
+        acc0 = MFMA(a.x, b0.x, acc0);
+        acc1 = MFMA(a.x, b1.x, acc1);
+        acc0 = MFMA(a.y, b0.y, acc0);
+        acc1 = MFMA(a.y, b1.y, acc1);
+        acc0 = MFMA(a.z, b0.z, acc0);
+        acc1 = MFMA(a.z, b1.z, acc1);
+        acc0 = MFMA(a.w, b0.w, acc0);
+        acc1 = MFMA(a.w, b1.w, acc1);
+        if ((k & 3) == 0) {
+#pragma unroll
+            for (int s_ = 0; s_ < SPG; s_++) side.unit();
+        }
+#ifdef DGS_MLP_PROFILE
+        if (g_chunk_stamp >= 0 && (threadIdx.x & 63) == 0 && ((threadIdx.x >> 6) & 3) == 0)
+            dgs_mlp_prof[blockIdx.x * 256 + g_chunk_stamp + (threadIdx.x >> 8) * 64 + k] = __builtin_amdgcn_s_memtime();
+#endif
+        // keep the schedule: without this fence the scheduler sinks each A load next to its use
+        // (minimising registers) and every chunk waits a full L2 round trip
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// single m-tile variant (narrow K-split layers), same schedule
+template <int NCH, int SPG, class Side, class Pre = NoPre>
+__device__ inline void gemm_1m(const float4 *__restrict__ Apk, int c0, const float4 *lds, int g0, int mt, int lane,
+                               f32x16 &acc, const Side &side, Pre pre = Pre()) {
+    const int h = lane >> 5, m = lane & 31;
+    const float4 *Ap = Apk + c0 * 64 + lane;
+    const float4 *Bp = lds + (g0 + 2 * c0 + h) * BM + mt * 32 + m;
+    float4 ring[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        if (k < NCH) ring[k] = Ap[k * 64];
+    pre();
+    float4 bx[2];
+    bx[0] = Bp[0];
+#pragma unroll
+    for (int k = 0; k < NCH; k++) {
+        const float4 a = ring[k & 3];
+        if (k + 4 < NCH) ring[k & 3] = Ap[(k + 4) * 64];
+        if (k + 1 < NCH) bx[(k + 1) & 1] = Bp[2 * (k + 1) * BM];
+        const float4 b = bx[k & 1];
+        acc = MFMA(a.x, b.x, acc);
+        acc = MFMA(a.y, b.y, acc);
+        acc = MFMA(a.z, b.z, acc);
+        acc = MFMA(a.w, b.w, acc);
+        if ((k & 3) == 0) {
+#pragma unroll
+            for (int s_ = 0; s_ < SPG; s_++) side.unit();
+        }
+        // keep the schedule: without this fence the scheduler sinks each A load next to its use
+        // (minimising registers) and every chunk waits a full L2 round trip
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// short GEMM (timenet layer 0: 2 chunks), plain loads
+__device__ inline void gemm_small(const float4 *__restrict__ Apk, int nch, const float4 *lds, int g0, int lane,
+                                  f32x16 &acc0, f32x16 &acc1) {
+    const int h = lane >> 5, m = lane & 31;
+    for (int c = 0; c < nch; c++) {
+        const float4 a = Apk[c * 64 + lane];
+        const float4 *grp = lds + (g0 + 2 * c + h) * BM;
+        const float4 b0 = grp[m], b1 = grp[32 + m];
+        acc0 = MFMA(a.x, b0.x, acc0);
+        acc1 = MFMA(a.x, b1.x, acc1);
+        acc0 = MFMA(a.y, b0.y, acc0);
+        acc1 = MFMA(a.y, b1.y, acc1);
+        acc0 = MFMA(a.z, b0.z, acc0);
+        acc1 = MFMA(a.z, b1.z, acc1);
+        acc0 = MFMA(a.w, b0.w, acc0);
+        acc1 = MFMA(a.w, b1.w, acc1);
+    }
+}
 
 // accumulator (n-tile base n0, m-tile mt) -> LDS groups starting at gout, with bias/relu
 __device__ inline void acc_to_lds(const f32x16 &acc, float4 *lds, int gout, int n0, int mt, int lane,
@@ -410,6 +491,38 @@ __device__ inline void acc_to_lds(const f32x16 &acc, float4 *lds, int gout, int 
     }
 }
 
+// bias of this lane's accumulator rows (n0 + 8j + 4h .. +3, j < 4), loaded ahead of the GEMM
+struct Bias4 {
+    float4 v[4];
+};
+
+struct BiasPre {
+    Bias4 *b;
+    const float *bias;
+    int n0, lane;
+    __device__ void operator()() const {
+        const int h = lane >> 5;
+#pragma unroll
+        for (int j = 0; j < 4; j++) b->v[j] = *reinterpret_cast<const float4 *>(bias + n0 + 8 * j + 4 * h);
+    }
+};
+
+// accumulator + preloaded bias, relu -> LDS groups starting at gout
+__device__ inline void acc_bias_relu_to_lds(const f32x16 &acc, const Bias4 &b, float4 *lds, int gout, int n0, int mt,
+                                            int lane) {
+    const int h = lane >> 5, m = lane & 31;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int f = n0 + 8 * j + 4 * h;
+        float4 v;
+        v.x = fmaxf(acc[4 * j] + b.v[j].x, 0.f);
+        v.y = fmaxf(acc[4 * j + 1] + b.v[j].y, 0.f);
+        v.z = fmaxf(acc[4 * j + 2] + b.v[j].z, 0.f);
+        v.w = fmaxf(acc[4 * j + 3] + b.v[j].w, 0.f);
+        lds[(gout + f / 4) * BM + mt * 32 + m] = v;
+    }
+}
+
 // LDS groups [g0, g0+ng) (features 4*ng) -> global rows [row0, row0 + 4ng) of a [rows][Ns] array
 __device__ inline void lds_to_global(const float4 *lds, int g0, int ng, float *__restrict__ dst, int row0, size_t Ns,
                                      int p0, int tid) {
@@ -425,6 +538,7 @@ __device__ inline void lds_to_global(const float4 *lds, int g0, int ng, float *_
 // ------------------------------------------------------------------------------------------------
 // forward
 // ------------------------------------------------------------------------------------------------
+
 struct FwdArgs {
     int N;
     size_t Ns;
@@ -436,18 +550,8 @@ struct FwdArgs {
     int flags;
 };
 
-// narrow layer: 1 output n-tile, K split over 8 waves (4 quarters x 2 m-tiles), fixed-order sum,
-// result (+bias) written to LDS groups gout..gout+7 (32 features)
-template <class Side = NoSide>
-__device__ inline void narrow_layer(const float4 *Apk, int nchunks, float4 *lds, int g0, int gout, const float *bias,
-                                    int wave, int lane, int tid, Side side = Side()) {
-    const int mt = wave & 1, q = wave >> 1;
-    const int per = nchunks / 4;
-    f32x16 acc = zero16();
-    gemm_1m(Apk, q * per, (q + 1) * per, lds, g0, mt, lane, acc, side);
-    // partial -> PART region slot q (8 groups per slot)
-    acc_to_lds(acc, lds, G_PART + 8 * q, 0, mt, lane, nullptr, false);
-    __syncthreads();
+// 4 K-quarter partials (PART slots) -> sum in a fixed order (+bias) -> LDS groups gout..gout+7
+__device__ inline void sum_parts(float4 *lds, int gout, const float *bias, int tid, bool accumulate) {
     for (int e = tid; e < 8 * BM; e += NTHR) {
         int gi = e / BM, m = e % BM;
         float4 s0 = lds[(G_PART + gi) * BM + m];
@@ -463,18 +567,38 @@ __device__ inline void narrow_layer(const float4 *Apk, int nchunks, float4 *lds,
             float4 b = *reinterpret_cast<const float4 *>(bias + 4 * gi);
             r.x += b.x; r.y += b.y; r.z += b.z; r.w += b.w;
         }
-        lds[(gout + gi) * BM + m] = r;
+        float4 &d = lds[(gout + gi) * BM + m];
+        if (accumulate) {
+            d.x += r.x; d.y += r.y; d.z += r.z; d.w += r.w;
+        } else {
+            d = r;
+        }
     }
-    __syncthreads();
 }
 
-__global__ __launch_bounds__(NTHR) void k_mlp_fwd(FwdArgs a) {
+// narrow layer: 1 output n-tile, K split over 8 waves (4 quarters x 2 m-tiles), fixed-order sum,
+// result (+bias) written to LDS groups gout..gout+7 (32 features)
+template <int SPG, class Side>
+__device__ inline void narrow_layer(const float4 *Apk, float4 *lds, int g0, int gout, const float *bias, int wave,
+                                    int lane, int tid, const Side &side) {
+    const int mt = wave & 1, q = wave >> 1;
+    f32x16 acc = zero16();
+    gemm_1m<8, SPG>(Apk, q * 8, lds, g0, mt, lane, acc, side);  // 32 chunks = 4 quarters x 8
+    acc_to_lds(acc, lds, G_PART + 8 * q, 0, mt, lane, nullptr, false);
+    lds_barrier();
+    sum_parts(lds, gout, bias, tid, false);
+    lds_barrier();
+}
+
+template <bool SAVE>
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_mlp_fwd(FwdArgs a) {
     __shared__ float4 lds[G_TOTAL * BM];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform (scalar branches)
     const int p0 = blockIdx.x * BM;
     const Flags F = make_flags(a.flags);
     const float4 *pk = reinterpret_cast<const float4 *>(a.packed);
+    DGS_STAMP(0);
     float *lf = reinterpret_cast<float *>(lds);
     // ---- positional encodings (utils/time_utils.py:42-54) ----
     for (int e = tid; e < 64 * BM; e += NTHR) {
@@ -514,14 +638,16 @@ __global__ __launch_bounds__(NTHR) void k_mlp_fwd(FwdArgs a) {
             lf[((tg + f / 4) * BM + m) * 4 + (f & 3)] = v;
         }
     }
-    __syncthreads();
-    // saved activations leave LDS under the following GEMMs (Pending); nothing is stored when
-    // a.saved == nullptr (inference)
+    lds_barrier();
+    DGS_STAMP(1);
+    // saved activations leave LDS under the following GEMMs (every GEMM below has a non-empty
+    // pending set when SAVE: XE/TIN/TE, then each layer's output)
     Pending pend;
-    pend.n = 0; pend.units = 0; pend.pos = 0; pend.per = 0; pend.nga = 0; pend.total = 0;
-    PendingSide side{&pend, lds, a.saved, a.Ns, p0, tid};
-    if (a.saved) {
-        pend.set1(G_XE, 16, S_XE);
+    pend.clear();
+    const PendingSide ps{&pend, lds, a.saved, a.Ns, p0, tid};
+    const NoSide ns{};
+    if (SAVE) {
+        pend.add(G_XE, 16, S_XE);
         if (F.blender) pend.add(G_TIN, 4, S_TIN);
         else pend.add(G_TE, 8, S_TE);
     }
@@ -529,41 +655,71 @@ __global__ __launch_bounds__(NTHR) void k_mlp_fwd(FwdArgs a) {
     // ---- timenet (blender): Linear(13,256) + ReLU -> H ; Linear(256,30) -> TE ----
     if (F.blender) {
         f32x16 c0 = zero16(), c1 = zero16();
-        pend.pace(2);
-        gemm_2m(pk + a.fT1 / 4 + wave * 2 * 64, 0, 2, lds, G_TIN, lane, c0, c1, side);
+        gemm_small(pk + a.fT1 / 4 + wave * 2 * 64, 2, lds, G_TIN, lane, c0, c1);
         acc_to_lds(c0, lds, G_H, wave * 32, 0, lane, bias + a.bT1, true);
         acc_to_lds(c1, lds, G_H, wave * 32, 1, lane, bias + a.bT1, true);
-        __syncthreads();
-        side.flush();
-        if (a.saved) pend.set1(G_H, 64, S_TH);
-        pend.pace(8);
-        narrow_layer(pk + a.fT2 / 4, 32, lds, G_H, G_TE, bias + a.bT2, wave, lane, tid, side);
-        side.flush();
-        if (a.saved) pend.set1(G_TE, 8, S_TE);
+        lds_barrier();
+        DGS_STAMP(2);
+        // XE + TIN (2.5 units) and TH (8 units) leave under T2 (2 groups x 6 units)
+        if (SAVE) {
+            pend.add(G_H, 64, S_TH);
+            narrow_layer<6>(pk + a.fT2 / 4, lds, G_H, G_TE, bias + a.bT2, wave, lane, tid, ps);
+            ps.flush();
+            pend.set1(G_TE, 8, S_TE);
+        } else {
+            narrow_layer<0>(pk + a.fT2 / 4, lds, G_H, G_TE, bias + a.bT2, wave, lane, tid, ns);
+        }
     }
+    DGS_STAMP(3);
     // ---- trunk: 8 x (Linear + ReLU), skip cat after layer 4 (time_utils.py:107-112) ----
     for (int L = 0; L < 8; L++) {
         const int g0 = (L == 0 || L == 5) ? G_XE : G_H;
         const int nch = layer_kpad(L) / 8;
         f32x16 c0 = zero16(), c1 = zero16();
-        pend.pace(nch);
-        gemm_2m(pk + a.fL[L] / 4 + wave * nch * 64, 0, nch, lds, g0, lane, c0, c1, side);
-        side.flush();
-        __syncthreads();  // all waves finished reading H before it is overwritten
-        acc_to_lds(c0, lds, G_H, wave * 32, 0, lane, bias + a.bL[L], true);
-        acc_to_lds(c1, lds, G_H, wave * 32, 1, lane, bias + a.bL[L], true);
-        __syncthreads();
-        if (a.saved) pend.set1(G_H, 64, s_h(L));
+        const float4 *Aw = pk + a.fL[L] / 4 + wave * nch * 64;
+        Bias4 bv;
+        const BiasPre bp{&bv, bias + a.bL[L], wave * 32, lane};
+        if (nch == 32) {
+#ifdef DGS_MLP_PROFILE
+            if (SAVE) gemm_2m<32, 1>(Aw, 0, lds, g0, lane, c0, c1, ps, bp, L == 1 ? 64 : -1);
+#else
+            if (SAVE) gemm_2m<32, 1>(Aw, 0, lds, g0, lane, c0, c1, ps, bp);
+#endif
+            else gemm_2m<32, 0>(Aw, 0, lds, g0, lane, c0, c1, ns, bp);
+        } else if (nch == 12) {
+            if (SAVE) gemm_2m<12, 1>(Aw, 0, lds, g0, lane, c0, c1, ps, bp);
+            else gemm_2m<12, 0>(Aw, 0, lds, g0, lane, c0, c1, ns, bp);
+        } else {
+            if (SAVE) gemm_2m<44, 1>(Aw, 0, lds, g0, lane, c0, c1, ps, bp);
+            else gemm_2m<44, 0>(Aw, 0, lds, g0, lane, c0, c1, ns, bp);
+        }
+        DGS_STAMP(4 + 3 * L);
+        if (L == 1) DGS_WSTAMP(40);
+        if (L == 0) DGS_WSIMD(48);
+        if (SAVE) ps.flush();
+        lds_barrier();  // all waves finished reading H before it is overwritten
+        DGS_STAMP(5 + 3 * L);
+        acc_bias_relu_to_lds(c0, bv, lds, G_H, wave * 32, 0, lane);
+        acc_bias_relu_to_lds(c1, bv, lds, G_H, wave * 32, 1, lane);
+        lds_barrier();
+        DGS_STAMP(6 + 3 * L);
+        if (L == 0) DGS_WSTAMP(32);
+        if (SAVE) pend.set1(G_H, 64, s_h(L));
     }
-    pend.pace(8);
     // ---- heads (no activation): [warp | branch_w, branch_v], rotation, scaling -> TE region ----
-    narrow_layer(pk + a.fHd / 4, 32, lds, G_H, G_TE, bias + a.bHd, wave, lane, tid, side);
-    side.flush();
+    if (SAVE) {
+        narrow_layer<4>(pk + a.fHd / 4, lds, G_H, G_TE, bias + a.bHd, wave, lane, tid, ps);
+        ps.flush();
+    } else {
+        narrow_layer<0>(pk + a.fHd / 4, lds, G_H, G_TE, bias + a.bHd, wave, lane, tid, ns);
+    }
+    DGS_STAMP(28);
     for (int e = tid; e < F.nout * BM; e += NTHR) {
         int c = e % F.nout, m = e / F.nout;
         int p = p0 + m;
         if (p < a.N) a.out[(size_t)p * F.nout + c] = lf[((G_TE + c / 4) * BM + m) * 4 + (c & 3)];
     }
+    DGS_STAMP(29);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -580,13 +736,11 @@ struct BwdArgs {
     int flags;
 };
 
-// wide transposed layer: out n-tile = wave (rows [32w, 32w+32) of the 256-feature output),
-// reading K from LDS groups g0.., masked by saved activations (relu'), written to LDS H + global dZ
+// relu' mask rows of one 32x32 accumulator tile (the saved activations of the layer input)
 struct Mask16 {
     float v[16];
 };
 
-// relu' mask rows of one 32x32 accumulator tile, loaded ahead of the GEMM that needs them
 __device__ inline void mask_load(Mask16 &mk, const float *__restrict__ saved_rows, size_t Ns, int p0, int mt, int lane,
                                  int n0) {
     const int h = lane >> 5, m = lane & 31;
@@ -596,27 +750,35 @@ __device__ inline void mask_load(Mask16 &mk, const float *__restrict__ saved_row
     for (int r = 0; r < 16; r++) mk.v[r] = sv[(8 * (r >> 2) + (r & 3)) * ns];
 }
 
-__device__ inline void mask_apply_store(f32x16 &acc, const Mask16 &mk, float *__restrict__ dz_rows, size_t Ns, int p0,
-                                        int mt, int lane, int n0) {
-    const int h = lane >> 5, m = lane & 31;
-    float *dz = dz_rows + (size_t)(n0 + 4 * h) * Ns + p0 + mt * 32 + m;
-    const int ns = (int)Ns;
+__device__ inline void mask_apply(f32x16 &acc, const Mask16 &mk) {
 #pragma unroll
-    for (int r = 0; r < 16; r++) {
-        float v = mk.v[r] > 0.f ? acc[r] : 0.f;
-        acc[r] = v;
-        dz[(8 * (r >> 2) + (r & 3)) * ns] = v;
-    }
+    for (int r = 0; r < 16; r++) acc[r] = mk.v[r] > 0.f ? acc[r] : 0.f;
 }
 
 __device__ inline void mask_store(f32x16 &acc, const float *__restrict__ saved_rows, float *__restrict__ dz_rows,
                                   size_t Ns, int p0, int mt, int lane, int n0) {
     Mask16 mk;
     mask_load(mk, saved_rows, Ns, p0, mt, lane, n0);
-    mask_apply_store(acc, mk, dz_rows, Ns, p0, mt, lane, n0);
+    mask_apply(acc, mk);
+    const int h = lane >> 5, m = lane & 31;
+    float *dz = dz_rows + (size_t)(n0 + 4 * h) * Ns + p0 + mt * 32 + m;
+    const int ns = (int)Ns;
+#pragma unroll
+    for (int r = 0; r < 16; r++) dz[(8 * (r >> 2) + (r & 3)) * ns] = acc[r];
 }
 
-__global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
+struct MaskPre {  // both m-tiles' relu' masks, issued after the GEMM prologue
+    Mask16 *mk0, *mk1;
+    const float *rows;
+    size_t Ns;
+    int p0, lane, n0;
+    __device__ void operator()() const {
+        mask_load(*mk0, rows, Ns, p0, 0, lane, n0);
+        mask_load(*mk1, rows, Ns, p0, 1, lane, n0);
+    }
+};
+
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_mlp_bwd(BwdArgs a) {
     __shared__ float4 lds[G_TOTAL * BM];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform (scalar branches)
@@ -624,7 +786,7 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
     const Flags F = make_flags(a.flags);
     const float4 *pk = reinterpret_cast<const float4 *>(a.packed);
     float *lf = reinterpret_cast<float *>(lds);
-    // dOut -> LDS TIN..(use PART slot 0 region? no: TE region is the head-gradient image G)
+    // dOut -> LDS TE region (the head-gradient image G) and dz rows Z_G
     for (int e = tid; e < 32 * BM; e += NTHR) {
         int m = e % BM, c = e / BM;
         int p = p0 + m;
@@ -632,20 +794,28 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
         lf[((G_TE + c / 4) * BM + m) * 4 + (c & 3)] = v;
         a.dz[(size_t)(Z_G + c) * a.Ns + p] = v;
     }
-    __syncthreads();
+    lds_barrier();
+    // dZ_i leaves LDS (G_H) under the next GEMM
+    Pending pend;
+    pend.clear();
+    const PendingSide ps{&pend, lds, a.dz, a.Ns, p0, tid};
+    const NoSide ns{};
     // heads^T: dH7 = W_h^T dOut (K = 32 from TE region) -> mask H7 -> dZ7
     {
+        Mask16 mk0, mk1;
         f32x16 c0 = zero16(), c1 = zero16();
-        gemm_2m(pk + a.tHd / 4 + wave * 4 * 64, 0, 4, lds, G_TE, lane, c0, c1);
-        mask_store(c0, a.saved + (size_t)s_h(7) * a.Ns, a.dz + (size_t)(Z_L0 + 7 * 256) * a.Ns, a.Ns, p0, 0, lane, wave * 32);
-        mask_store(c1, a.saved + (size_t)s_h(7) * a.Ns, a.dz + (size_t)(Z_L0 + 7 * 256) * a.Ns, a.Ns, p0, 1, lane, wave * 32);
-        __syncthreads();  // TE (dOut image) reads done before TE is reused for dTE
+        gemm_2m<4, 0>(pk + a.tHd / 4 + wave * 4 * 64, 0, lds, G_TE, lane, c0, c1, ns,
+                      MaskPre{&mk0, &mk1, a.saved + (size_t)s_h(7) * a.Ns, a.Ns, p0, lane, wave * 32});
+        mask_apply(c0, mk0);
+        mask_apply(c1, mk1);
+        lds_barrier();  // TE (dOut image) reads done before TE is reused for dTE
         acc_to_lds(c0, lds, G_H, wave * 32, 0, lane, nullptr, false);
         acc_to_lds(c1, lds, G_H, wave * 32, 1, lane, nullptr, false);
     }
     // zero the dTE accumulator (TE region holds dL/dt_emb from layers 5 and 0)
     for (int e = tid; e < 8 * BM; e += NTHR) lds[G_TE * BM + e] = make_float4(0.f, 0.f, 0.f, 0.f);
-    __syncthreads();
+    lds_barrier();
+    pend.set1(G_H, 64, Z_L0 + 7 * 256);
     for (int L = 7; L >= 1; L--) {
         // dX_L = W_L^T dZ_L ; H-part rows of the padded input live at tiles (F_H/32 + w) for L=5
         const int tile0 = (L == 5) ? F_H / 32 : 0;
@@ -653,59 +823,44 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
             // t_emb slice (padded rows 64..95 = tile 2): narrow K-split partials -> PART
             const int mt = wave & 1, q = wave >> 1;
             f32x16 ct = zero16();
-            gemm_1m(pk + a.tL[5] / 4 + (F_TE / 32) * 32 * 64, q * 8, q * 8 + 8, lds, G_H, mt, lane, ct);
+            gemm_1m<8, 0>(pk + a.tL[5] / 4 + (F_TE / 32) * 32 * 64, q * 8, lds, G_H, mt, lane, ct, ns);
             acc_to_lds(ct, lds, G_PART + 8 * q, 0, mt, lane, nullptr, false);
         }
         Mask16 mk0, mk1;  // relu' of H_{L-1}, in flight during the GEMM
-        mask_load(mk0, a.saved + (size_t)s_h(L - 1) * a.Ns, a.Ns, p0, 0, lane, wave * 32);
-        mask_load(mk1, a.saved + (size_t)s_h(L - 1) * a.Ns, a.Ns, p0, 1, lane, wave * 32);
         f32x16 c0 = zero16(), c1 = zero16();
-        gemm_2m(pk + a.tL[L] / 4 + (tile0 + wave) * 32 * 64, 0, 32, lds, G_H, lane, c0, c1);
-        mask_apply_store(c0, mk0, a.dz + (size_t)(Z_L0 + (L - 1) * 256) * a.Ns, a.Ns, p0, 0, lane, wave * 32);
-        mask_apply_store(c1, mk1, a.dz + (size_t)(Z_L0 + (L - 1) * 256) * a.Ns, a.Ns, p0, 1, lane, wave * 32);
-        __syncthreads();
-        if (L == 5 && F.blender) {
-            for (int e = tid; e < 8 * BM; e += NTHR) {
-                int gi = e / BM, m = e % BM;
-                float4 s0 = lds[(G_PART + gi) * BM + m], s1 = lds[(G_PART + 8 + gi) * BM + m];
-                float4 s2 = lds[(G_PART + 16 + gi) * BM + m], s3 = lds[(G_PART + 24 + gi) * BM + m];
-                float4 &d = lds[(G_TE + gi) * BM + m];
-                d.x += ((s0.x + s1.x) + s2.x) + s3.x;
-                d.y += ((s0.y + s1.y) + s2.y) + s3.y;
-                d.z += ((s0.z + s1.z) + s2.z) + s3.z;
-                d.w += ((s0.w + s1.w) + s2.w) + s3.w;
-            }
-        }
+        gemm_2m<32, 1>(pk + a.tL[L] / 4 + (tile0 + wave) * 32 * 64, 0, lds, G_H, lane, c0, c1, ps,
+                       MaskPre{&mk0, &mk1, a.saved + (size_t)s_h(L - 1) * a.Ns, a.Ns, p0, lane, wave * 32});
+        ps.flush();
+        mask_apply(c0, mk0);
+        mask_apply(c1, mk1);
+        lds_barrier();
+        if (L == 5 && F.blender) sum_parts(lds, G_TE, nullptr, tid, true);
         acc_to_lds(c0, lds, G_H, wave * 32, 0, lane, nullptr, false);
         acc_to_lds(c1, lds, G_H, wave * 32, 1, lane, nullptr, false);
-        __syncthreads();
+        lds_barrier();
+        pend.set1(G_H, 64, Z_L0 + (L - 1) * 256);
     }
-    if (!F.blender) return;  // raw t PE has no parameters upstream of it
-    // layer 0: t_emb slice of W_0^T dZ_0 (narrow)
+    if (!F.blender) {
+        ps.flush();
+        return;  // raw t PE has no parameters upstream of it
+    }
+    // layer 0: t_emb slice of W_0^T dZ_0 (narrow); dZ_0 leaves under it
     {
         const int mt = wave & 1, q = wave >> 1;
         f32x16 ct = zero16();
-        gemm_1m(pk + a.tL[0] / 4 + (F_TE / 32) * 32 * 64, q * 8, q * 8 + 8, lds, G_H, mt, lane, ct);
+        gemm_1m<8, 4>(pk + a.tL[0] / 4 + (F_TE / 32) * 32 * 64, q * 8, lds, G_H, mt, lane, ct, ps);
+        ps.flush();
         acc_to_lds(ct, lds, G_PART + 8 * q, 0, mt, lane, nullptr, false);
-        __syncthreads();
-        for (int e = tid; e < 8 * BM; e += NTHR) {
-            int gi = e / BM, m = e % BM;
-            float4 s0 = lds[(G_PART + gi) * BM + m], s1 = lds[(G_PART + 8 + gi) * BM + m];
-            float4 s2 = lds[(G_PART + 16 + gi) * BM + m], s3 = lds[(G_PART + 24 + gi) * BM + m];
-            float4 &d = lds[(G_TE + gi) * BM + m];
-            d.x += ((s0.x + s1.x) + s2.x) + s3.x;
-            d.y += ((s0.y + s1.y) + s2.y) + s3.y;
-            d.z += ((s0.z + s1.z) + s2.z) + s3.z;
-            d.w += ((s0.w + s1.w) + s2.w) + s3.w;
-        }
-        __syncthreads();
+        lds_barrier();
+        sum_parts(lds, G_TE, nullptr, tid, true);
+        lds_barrier();
     }
     // dTE (30 real rows) -> global (dW of timenet.2)
     lds_to_global(lds, G_TE, 8, a.dz, Z_TE, a.Ns, p0, tid);
     // timenet.2^T: dTH = W_T2^T dTE (K = 32) -> mask TH -> dZ_T1
     {
         f32x16 c0 = zero16(), c1 = zero16();
-        gemm_2m(pk + a.tT2 / 4 + wave * 4 * 64, 0, 4, lds, G_TE, lane, c0, c1);
+        gemm_2m<4, 0>(pk + a.tT2 / 4 + wave * 4 * 64, 0, lds, G_TE, lane, c0, c1, ns);
         mask_store(c0, a.saved + (size_t)S_TH * a.Ns, a.dz + (size_t)Z_T1 * a.Ns, a.Ns, p0, 0, lane, wave * 32);
         mask_store(c1, a.saved + (size_t)S_TH * a.Ns, a.dz + (size_t)Z_T1 * a.Ns, a.Ns, p0, 1, lane, wave * 32);
     }
@@ -1043,6 +1198,12 @@ inline WPlan make_wplan(const Flags &F) {
 using namespace dgs;
 using namespace dgs::mlp;
 
+#ifdef DGS_MLP_PROFILE
+extern "C" void dgs_mlp_set_prof(unsigned long long *p) {
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(dgs::mlp::dgs_mlp_prof), &p, sizeof(p));
+}
+#endif
+
 extern "C" int dgs_deform_outputs(int flags) { return make_flags(flags).nout; }
 extern "C" int dgs_deform_num_params(int flags) { return make_plan(flags).nparams; }
 extern "C" size_t dgs_deform_packed_floats(int flags) { return (size_t)make_plan(flags).total; }
@@ -1169,7 +1330,10 @@ extern "C" int dgs_deform_forward(int flags, int N, const float *xyz, const floa
     a.flags = flags;
     {
         ScopedTimer tm("mlp_fwd", stream);
-        hipLaunchKernelGGL(k_mlp_fwd, dim3(div_up(N, BM)), dim3(NTHR), 0, stream, a);
+        if (saved)
+            hipLaunchKernelGGL(k_mlp_fwd<true>, dim3(div_up(N, BM)), dim3(NTHR), 0, stream, a);
+        else
+            hipLaunchKernelGGL(k_mlp_fwd<false>, dim3(div_up(N, BM)), dim3(NTHR), 0, stream, a);
     }
     DGS_LAUNCH_CHECK("k_mlp_fwd", false, stream);
     return DGS_OK;
