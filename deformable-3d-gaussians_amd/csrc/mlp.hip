@@ -367,15 +367,46 @@ struct NoPre {
     __device__ void operator()() const {}
 };
 
+// bias preload plus U side units (a fixed count), run after a GEMM's prologue loads
+template <int U>
+struct PreUnits;
+
+// The previous layer's output tiles of this wave (rows n0 + 8(r>>2) + 4h + (r&3), points m and
+// 32 + m), kept in registers and written to a feature-major [rows][Ns] array during the first four
+// chunks of the next GEMM: 8 plain coalesced stores per chunk, issued after that GEMM's prologue
+// loads so no A-fragment wait depends on them, with no LDS read and no index arithmetic.
+struct NoStash {
+    __device__ void store(int) const {}
+};
+
+struct Stash2 {
+    f32x16 t0, t1;
+    float *d;  // &dst[(row0 + n0 + 4h) * Ns + p0 + m]
+    int ns;
+    __device__ void store(int k) const {
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int idx = 8 * k + j, r = idx & 15;
+            const float v = (idx >> 4) ? t1[r] : t0[r];
+            d[(8 * (r >> 2) + (r & 3)) * ns + (idx >> 4) * 32] = v;
+        }
+    }
+    __device__ void store_all() const {
+#pragma unroll
+        for (int k = 0; k < 4; k++) store(k);
+    }
+};
+
 // acc0/acc1 (m-tiles 0/1) += A . X over NCH chunks starting at chunk c0 of the A image and of the
 // LDS image at group g0 (chunk c = groups g0 + 2c + h). Fully unrolled straight-line schedule (no
 // loop back-edge, so no register rotation and exact compiler vmcnt/lgkmcnt bookkeeping): per chunk
 // the A fragment 4 chunks ahead (4-deep ring, issued before this chunk's MFMAs), the next chunk's B
 // (double-buffered ds_read_b128), 8 MFMAs, and on every 4th chunk SPG side units. pre() runs after
 // the A prologue (its global loads are younger than the first fragments).
-template <int NCH, int SPG, class Side, class Pre = NoPre>
+template <int NCH, int SPG, class Side, class Pre = NoPre, class Stash = NoStash>
 __device__ inline void gemm_2m(const float4 *__restrict__ Apk, int c0, const float4 *lds, int g0, int lane,
-                               f32x16 &acc0, f32x16 &acc1, const Side &side, Pre pre = Pre(), int g_chunk_stamp = -1) {
+                               f32x16 &acc0, f32x16 &acc1, const Side &side, Pre pre = Pre(),
+                               const Stash &stash = Stash(), int g_chunk_stamp = -1) {
     static_assert(NCH >= 1, "empty GEMM");
     const int h = lane >> 5, m = lane & 31;
     const float4 *Ap = Apk + c0 * 64 + lane;
@@ -409,6 +440,7 @@ __device__ inline void gemm_2m(const float4 *__restrict__ Apk, int c0, const flo
 #pragma unroll
             for (int s_ = 0; s_ < SPG; s_++) side.unit();
         }
+        if (k < 4) stash.store(k);
 #ifdef DGS_MLP_PROFILE
         if (g_chunk_stamp >= 0 && (threadIdx.x & 63) == 0 && ((threadIdx.x >> 6) & 3) == 0)
             dgs_mlp_prof[blockIdx.x * 256 + g_chunk_stamp + (threadIdx.x >> 8) * 64 + k] = __builtin_amdgcn_s_memtime();
@@ -420,9 +452,9 @@ __device__ inline void gemm_2m(const float4 *__restrict__ Apk, int c0, const flo
 }
 
 // single m-tile variant (narrow K-split layers), same schedule
-template <int NCH, int SPG, class Side, class Pre = NoPre>
+template <int NCH, int SPG, class Side, class Pre = NoPre, class Stash = NoStash>
 __device__ inline void gemm_1m(const float4 *__restrict__ Apk, int c0, const float4 *lds, int g0, int mt, int lane,
-                               f32x16 &acc, const Side &side, Pre pre = Pre()) {
+                               f32x16 &acc, const Side &side, Pre pre = Pre(), const Stash &stash = Stash()) {
     const int h = lane >> 5, m = lane & 31;
     const float4 *Ap = Apk + c0 * 64 + lane;
     const float4 *Bp = lds + (g0 + 2 * c0 + h) * BM + mt * 32 + m;
@@ -447,6 +479,7 @@ __device__ inline void gemm_1m(const float4 *__restrict__ Apk, int c0, const flo
 #pragma unroll
             for (int s_ = 0; s_ < SPG; s_++) side.unit();
         }
+        if (k < 4) stash.store(k);
         // keep the schedule: without this fence the scheduler sinks each A load next to its use
         // (minimising registers) and every chunk waits a full L2 round trip
         __builtin_amdgcn_sched_barrier(0);
@@ -506,6 +539,28 @@ struct BiasPre {
         for (int j = 0; j < 4; j++) b->v[j] = *reinterpret_cast<const float4 *>(bias + n0 + 8 * j + 4 * h);
     }
 };
+
+template <int U>
+struct PreUnits {
+    BiasPre bp;
+    const PendingSide *ps;
+    __device__ void operator()() const {
+        bp();
+#pragma unroll
+        for (int u = 0; u < U; u++) ps->unit();
+    }
+};
+
+// acc = relu(acc + bias) in place (the values kept for the deferred store)
+__device__ inline void bias_relu(f32x16 &acc, const Bias4 &b) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        acc[4 * j] = fmaxf(acc[4 * j] + b.v[j].x, 0.f);
+        acc[4 * j + 1] = fmaxf(acc[4 * j + 1] + b.v[j].y, 0.f);
+        acc[4 * j + 2] = fmaxf(acc[4 * j + 2] + b.v[j].z, 0.f);
+        acc[4 * j + 3] = fmaxf(acc[4 * j + 3] + b.v[j].w, 0.f);
+    }
+}
 
 // accumulator + preloaded bias, relu -> LDS groups starting at gout
 __device__ inline void acc_bias_relu_to_lds(const f32x16 &acc, const Bias4 &b, float4 *lds, int gout, int n0, int mt,
@@ -578,12 +633,12 @@ __device__ inline void sum_parts(float4 *lds, int gout, const float *bias, int t
 
 // narrow layer: 1 output n-tile, K split over 8 waves (4 quarters x 2 m-tiles), fixed-order sum,
 // result (+bias) written to LDS groups gout..gout+7 (32 features)
-template <int SPG, class Side>
+template <class Stash = NoStash>
 __device__ inline void narrow_layer(const float4 *Apk, float4 *lds, int g0, int gout, const float *bias, int wave,
-                                    int lane, int tid, const Side &side) {
+                                    int lane, int tid, const Stash &stash = Stash()) {
     const int mt = wave & 1, q = wave >> 1;
     f32x16 acc = zero16();
-    gemm_1m<8, SPG>(Apk, q * 8, lds, g0, mt, lane, acc, side);  // 32 chunks = 4 quarters x 8
+    gemm_1m<8, 0>(Apk, q * 8, lds, g0, mt, lane, acc, NoSide(), NoPre(), stash);  // 32 chunks = 4 x 8
     acc_to_lds(acc, lds, G_PART + 8 * q, 0, mt, lane, nullptr, false);
     lds_barrier();
     sum_parts(lds, gout, bias, tid, false);
@@ -640,35 +695,40 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
     }
     lds_barrier();
     DGS_STAMP(1);
-    // saved activations leave LDS under the following GEMMs (every GEMM below has a non-empty
-    // pending set when SAVE: XE/TIN/TE, then each layer's output)
+    // saved activations: the network inputs (XE, TIN | TE) and T2's output leave LDS in the first
+    // trunk GEMM's prologue (fixed 4 units); every hidden layer's output is kept in registers and
+    // stored during the next GEMM (Stash2)
     Pending pend;
     pend.clear();
     const PendingSide ps{&pend, lds, a.saved, a.Ns, p0, tid};
-    const NoSide ns{};
     if (SAVE) {
         pend.add(G_XE, 16, S_XE);
         if (F.blender) pend.add(G_TIN, 4, S_TIN);
         else pend.add(G_TE, 8, S_TE);
     }
     const float *bias = a.packed;
+    const int h = lane >> 5, m32 = lane & 31;
+    const int ns32 = (int)a.Ns;
+    float *const sv_lane = a.saved + (size_t)(wave * 32 + 4 * h) * a.Ns + p0 + m32;  // + row0 * Ns
+    f32x16 k0 = zero16(), k1 = zero16();  // previous layer's activations, awaiting their store
     // ---- timenet (blender): Linear(13,256) + ReLU -> H ; Linear(256,30) -> TE ----
     if (F.blender) {
         f32x16 c0 = zero16(), c1 = zero16();
+        Bias4 bv;
+        BiasPre{&bv, bias + a.bT1, wave * 32, lane}();
         gemm_small(pk + a.fT1 / 4 + wave * 2 * 64, 2, lds, G_TIN, lane, c0, c1);
-        acc_to_lds(c0, lds, G_H, wave * 32, 0, lane, bias + a.bT1, true);
-        acc_to_lds(c1, lds, G_H, wave * 32, 1, lane, bias + a.bT1, true);
+        bias_relu(c0, bv);
+        bias_relu(c1, bv);
+        acc_to_lds(c0, lds, G_H, wave * 32, 0, lane, nullptr, false);
+        acc_to_lds(c1, lds, G_H, wave * 32, 1, lane, nullptr, false);
         lds_barrier();
         DGS_STAMP(2);
-        // XE + TIN (2.5 units) and TH (8 units) leave under T2 (2 groups x 6 units)
-        if (SAVE) {
-            pend.add(G_H, 64, S_TH);
-            narrow_layer<6>(pk + a.fT2 / 4, lds, G_H, G_TE, bias + a.bT2, wave, lane, tid, ps);
-            ps.flush();
-            pend.set1(G_TE, 8, S_TE);
-        } else {
-            narrow_layer<0>(pk + a.fT2 / 4, lds, G_H, G_TE, bias + a.bT2, wave, lane, tid, ns);
-        }
+        if (SAVE)
+            narrow_layer(pk + a.fT2 / 4, lds, G_H, G_TE, bias + a.bT2, wave, lane, tid,
+                         Stash2{c0, c1, sv_lane + (size_t)S_TH * a.Ns, ns32});
+        else
+            narrow_layer(pk + a.fT2 / 4, lds, G_H, G_TE, bias + a.bT2, wave, lane, tid);
+        if (SAVE) pend.add(G_TE, 8, S_TE);
     }
     DGS_STAMP(3);
     // ---- trunk: 8 x (Linear + ReLU), skip cat after layer 4 (time_utils.py:107-112) ----
@@ -679,40 +739,44 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
         const float4 *Aw = pk + a.fL[L] / 4 + wave * nch * 64;
         Bias4 bv;
         const BiasPre bp{&bv, bias + a.bL[L], wave * 32, lane};
-        if (nch == 32) {
-#ifdef DGS_MLP_PROFILE
-            if (SAVE) gemm_2m<32, 1>(Aw, 0, lds, g0, lane, c0, c1, ps, bp, L == 1 ? 64 : -1);
-#else
-            if (SAVE) gemm_2m<32, 1>(Aw, 0, lds, g0, lane, c0, c1, ps, bp);
-#endif
-            else gemm_2m<32, 0>(Aw, 0, lds, g0, lane, c0, c1, ns, bp);
-        } else if (nch == 12) {
-            if (SAVE) gemm_2m<12, 1>(Aw, 0, lds, g0, lane, c0, c1, ps, bp);
-            else gemm_2m<12, 0>(Aw, 0, lds, g0, lane, c0, c1, ns, bp);
+        if (L == 0) {
+            if (SAVE) gemm_2m<12, 0>(Aw, 0, lds, g0, lane, c0, c1, NoSide(), PreUnits<4>{bp, &ps});
+            else gemm_2m<12, 0>(Aw, 0, lds, g0, lane, c0, c1, NoSide(), bp);
         } else {
-            if (SAVE) gemm_2m<44, 1>(Aw, 0, lds, g0, lane, c0, c1, ps, bp);
-            else gemm_2m<44, 0>(Aw, 0, lds, g0, lane, c0, c1, ns, bp);
+            const Stash2 st{k0, k1, sv_lane + (size_t)s_h(L - 1) * a.Ns, ns32};
+            if (L == 5) {
+                if (SAVE) gemm_2m<44, 0>(Aw, 0, lds, g0, lane, c0, c1, NoSide(), bp, st);
+                else gemm_2m<44, 0>(Aw, 0, lds, g0, lane, c0, c1, NoSide(), bp);
+            } else {
+#ifdef DGS_MLP_PROFILE
+                if (SAVE) gemm_2m<32, 0>(Aw, 0, lds, g0, lane, c0, c1, NoSide(), bp, st, L == 1 ? 64 : -1);
+#else
+                if (SAVE) gemm_2m<32, 0>(Aw, 0, lds, g0, lane, c0, c1, NoSide(), bp, st);
+#endif
+                else gemm_2m<32, 0>(Aw, 0, lds, g0, lane, c0, c1, NoSide(), bp);
+            }
         }
         DGS_STAMP(4 + 3 * L);
         if (L == 1) DGS_WSTAMP(40);
         if (L == 0) DGS_WSIMD(48);
-        if (SAVE) ps.flush();
         lds_barrier();  // all waves finished reading H before it is overwritten
         DGS_STAMP(5 + 3 * L);
-        acc_bias_relu_to_lds(c0, bv, lds, G_H, wave * 32, 0, lane);
-        acc_bias_relu_to_lds(c1, bv, lds, G_H, wave * 32, 1, lane);
+        bias_relu(c0, bv);
+        bias_relu(c1, bv);
+        acc_to_lds(c0, lds, G_H, wave * 32, 0, lane, nullptr, false);
+        acc_to_lds(c1, lds, G_H, wave * 32, 1, lane, nullptr, false);
         lds_barrier();
         DGS_STAMP(6 + 3 * L);
         if (L == 0) DGS_WSTAMP(32);
-        if (SAVE) pend.set1(G_H, 64, s_h(L));
+        k0 = c0;
+        k1 = c1;
     }
     // ---- heads (no activation): [warp | branch_w, branch_v], rotation, scaling -> TE region ----
-    if (SAVE) {
-        narrow_layer<4>(pk + a.fHd / 4, lds, G_H, G_TE, bias + a.bHd, wave, lane, tid, ps);
-        ps.flush();
-    } else {
-        narrow_layer<0>(pk + a.fHd / 4, lds, G_H, G_TE, bias + a.bHd, wave, lane, tid, ns);
-    }
+    if (SAVE)
+        narrow_layer(pk + a.fHd / 4, lds, G_H, G_TE, bias + a.bHd, wave, lane, tid,
+                     Stash2{k0, k1, sv_lane + (size_t)s_h(7) * a.Ns, ns32});
+    else
+        narrow_layer(pk + a.fHd / 4, lds, G_H, G_TE, bias + a.bHd, wave, lane, tid);
     DGS_STAMP(28);
     for (int e = tid; e < F.nout * BM; e += NTHR) {
         int c = e % F.nout, m = e / F.nout;
@@ -795,27 +859,28 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
         a.dz[(size_t)(Z_G + c) * a.Ns + p] = v;
     }
     lds_barrier();
-    // dZ_i leaves LDS (G_H) under the next GEMM
-    Pending pend;
-    pend.clear();
-    const PendingSide ps{&pend, lds, a.dz, a.Ns, p0, tid};
-    const NoSide ns{};
+    // dZ_i of the trunk stays in registers and is stored during the next GEMM (Stash2)
+    const int h = lane >> 5, m32 = lane & 31;
+    const int ns32 = (int)a.Ns;
+    float *const dz_lane = a.dz + (size_t)(wave * 32 + 4 * h) * a.Ns + p0 + m32;  // + row0 * Ns
+    f32x16 k0, k1;  // dZ of the layer whose GEMM runs next
     // heads^T: dH7 = W_h^T dOut (K = 32 from TE region) -> mask H7 -> dZ7
     {
         Mask16 mk0, mk1;
         f32x16 c0 = zero16(), c1 = zero16();
-        gemm_2m<4, 0>(pk + a.tHd / 4 + wave * 4 * 64, 0, lds, G_TE, lane, c0, c1, ns,
+        gemm_2m<4, 0>(pk + a.tHd / 4 + wave * 4 * 64, 0, lds, G_TE, lane, c0, c1, NoSide(),
                       MaskPre{&mk0, &mk1, a.saved + (size_t)s_h(7) * a.Ns, a.Ns, p0, lane, wave * 32});
         mask_apply(c0, mk0);
         mask_apply(c1, mk1);
         lds_barrier();  // TE (dOut image) reads done before TE is reused for dTE
         acc_to_lds(c0, lds, G_H, wave * 32, 0, lane, nullptr, false);
         acc_to_lds(c1, lds, G_H, wave * 32, 1, lane, nullptr, false);
+        k0 = c0;
+        k1 = c1;
     }
     // zero the dTE accumulator (TE region holds dL/dt_emb from layers 5 and 0)
     for (int e = tid; e < 8 * BM; e += NTHR) lds[G_TE * BM + e] = make_float4(0.f, 0.f, 0.f, 0.f);
     lds_barrier();
-    pend.set1(G_H, 64, Z_L0 + 7 * 256);
     for (int L = 7; L >= 1; L--) {
         // dX_L = W_L^T dZ_L ; H-part rows of the padded input live at tiles (F_H/32 + w) for L=5
         const int tile0 = (L == 5) ? F_H / 32 : 0;
@@ -823,14 +888,14 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
             // t_emb slice (padded rows 64..95 = tile 2): narrow K-split partials -> PART
             const int mt = wave & 1, q = wave >> 1;
             f32x16 ct = zero16();
-            gemm_1m<8, 0>(pk + a.tL[5] / 4 + (F_TE / 32) * 32 * 64, q * 8, lds, G_H, mt, lane, ct, ns);
+            gemm_1m<8, 0>(pk + a.tL[5] / 4 + (F_TE / 32) * 32 * 64, q * 8, lds, G_H, mt, lane, ct, NoSide());
             acc_to_lds(ct, lds, G_PART + 8 * q, 0, mt, lane, nullptr, false);
         }
         Mask16 mk0, mk1;  // relu' of H_{L-1}, in flight during the GEMM
         f32x16 c0 = zero16(), c1 = zero16();
-        gemm_2m<32, 1>(pk + a.tL[L] / 4 + (tile0 + wave) * 32 * 64, 0, lds, G_H, lane, c0, c1, ps,
-                       MaskPre{&mk0, &mk1, a.saved + (size_t)s_h(L - 1) * a.Ns, a.Ns, p0, lane, wave * 32});
-        ps.flush();
+        gemm_2m<32, 0>(pk + a.tL[L] / 4 + (tile0 + wave) * 32 * 64, 0, lds, G_H, lane, c0, c1, NoSide(),
+                       MaskPre{&mk0, &mk1, a.saved + (size_t)s_h(L - 1) * a.Ns, a.Ns, p0, lane, wave * 32},
+                       Stash2{k0, k1, dz_lane + (size_t)(Z_L0 + L * 256) * a.Ns, ns32});
         mask_apply(c0, mk0);
         mask_apply(c1, mk1);
         lds_barrier();
@@ -838,18 +903,19 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
         acc_to_lds(c0, lds, G_H, wave * 32, 0, lane, nullptr, false);
         acc_to_lds(c1, lds, G_H, wave * 32, 1, lane, nullptr, false);
         lds_barrier();
-        pend.set1(G_H, 64, Z_L0 + (L - 1) * 256);
+        k0 = c0;
+        k1 = c1;
     }
+    const Stash2 dz0{k0, k1, dz_lane + (size_t)Z_L0 * a.Ns, ns32};
     if (!F.blender) {
-        ps.flush();
+        dz0.store_all();
         return;  // raw t PE has no parameters upstream of it
     }
-    // layer 0: t_emb slice of W_0^T dZ_0 (narrow); dZ_0 leaves under it
+    // layer 0: t_emb slice of W_0^T dZ_0 (narrow); dZ_0 is stored under it
     {
         const int mt = wave & 1, q = wave >> 1;
         f32x16 ct = zero16();
-        gemm_1m<8, 4>(pk + a.tL[0] / 4 + (F_TE / 32) * 32 * 64, q * 8, lds, G_H, mt, lane, ct, ps);
-        ps.flush();
+        gemm_1m<8, 0>(pk + a.tL[0] / 4 + (F_TE / 32) * 32 * 64, q * 8, lds, G_H, mt, lane, ct, NoSide(), NoPre(), dz0);
         acc_to_lds(ct, lds, G_PART + 8 * q, 0, mt, lane, nullptr, false);
         lds_barrier();
         sum_parts(lds, G_TE, nullptr, tid, true);
@@ -860,7 +926,7 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
     // timenet.2^T: dTH = W_T2^T dTE (K = 32) -> mask TH -> dZ_T1
     {
         f32x16 c0 = zero16(), c1 = zero16();
-        gemm_2m<4, 0>(pk + a.tT2 / 4 + wave * 4 * 64, 0, lds, G_TE, lane, c0, c1, ns);
+        gemm_2m<4, 0>(pk + a.tT2 / 4 + wave * 4 * 64, 0, lds, G_TE, lane, c0, c1, NoSide());
         mask_store(c0, a.saved + (size_t)S_TH * a.Ns, a.dz + (size_t)Z_T1 * a.Ns, a.Ns, p0, 0, lane, wave * 32);
         mask_store(c1, a.saved + (size_t)S_TH * a.Ns, a.dz + (size_t)Z_T1 * a.Ns, a.Ns, p0, 1, lane, wave * 32);
     }
