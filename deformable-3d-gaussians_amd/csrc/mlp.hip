@@ -427,6 +427,9 @@ __device__ inline void gemm_2m(const float4 *__restrict__ Apk, int c0, const flo
             bx[(k + 1) & 1] = Bp[2 * (k + 1) * BM];
             by[(k + 1) & 1] = Bp[2 * (k + 1) * BM + 32];
         }
+        // issue the loads before this chunk's MFMAs (else the scheduler sinks the next B read
+        // behind them and reuses the current B registers, exposing LDS latency every chunk)
+        __builtin_amdgcn_sched_barrier(0);
         const float4 b0 = bx[k & 1], b1 = by[k & 1];
         acc0 = MFMA(a.x, b0.x, acc0);
         acc1 = MFMA(a.x, b1.x, acc1);
@@ -470,6 +473,7 @@ __device__ inline void gemm_1m(const float4 *__restrict__ Apk, int c0, const flo
         const float4 a = ring[k & 3];
         if (k + 4 < NCH) ring[k & 3] = Ap[(k + 4) * 64];
         if (k + 1 < NCH) bx[(k + 1) & 1] = Bp[2 * (k + 1) * BM];
+        __builtin_amdgcn_sched_barrier(0);
         const float4 b = bx[k & 1];
         acc = MFMA(a.x, b.x, acc);
         acc = MFMA(a.y, b.y, acc);
@@ -486,12 +490,13 @@ __device__ inline void gemm_1m(const float4 *__restrict__ Apk, int c0, const flo
     }
 }
 
-// short GEMM (timenet layer 0: 2 chunks), plain loads
-__device__ inline void gemm_small(const float4 *__restrict__ Apk, int nch, const float4 *lds, int g0, int lane,
-                                  f32x16 &acc0, f32x16 &acc1) {
+// timenet layer 0 (2 chunks) with its A fragments loaded by the caller (before the PE phase)
+__device__ inline void gemm_t1(const float4 a0, const float4 a1, const float4 *lds, int g0, int lane, f32x16 &acc0,
+                               f32x16 &acc1) {
     const int h = lane >> 5, m = lane & 31;
-    for (int c = 0; c < nch; c++) {
-        const float4 a = Apk[c * 64 + lane];
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+        const float4 a = c ? a1 : a0;
         const float4 *grp = lds + (g0 + 2 * c + h) * BM;
         const float4 b0 = grp[m], b1 = grp[32 + m];
         acc0 = MFMA(a.x, b0.x, acc0);
@@ -654,6 +659,15 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
     const Flags F = make_flags(a.flags);
     const float4 *pk = reinterpret_cast<const float4 *>(a.packed);
     DGS_STAMP(0);
+    // timenet layer 0 operands, in flight during the positional encodings
+    float4 t1a0 = make_float4(0.f, 0.f, 0.f, 0.f), t1a1 = t1a0;
+    Bias4 t1b;
+    if (F.blender) {
+        const float4 *At1 = pk + a.fT1 / 4 + wave * 2 * 64 + lane;
+        t1a0 = At1[0];
+        t1a1 = At1[64];
+        BiasPre{&t1b, a.packed + a.bT1, wave * 32, lane}();
+    }
     float *lf = reinterpret_cast<float *>(lds);
     // ---- positional encodings (utils/time_utils.py:42-54) ----
     for (int e = tid; e < 64 * BM; e += NTHR) {
@@ -714,11 +728,9 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
     // ---- timenet (blender): Linear(13,256) + ReLU -> H ; Linear(256,30) -> TE ----
     if (F.blender) {
         f32x16 c0 = zero16(), c1 = zero16();
-        Bias4 bv;
-        BiasPre{&bv, bias + a.bT1, wave * 32, lane}();
-        gemm_small(pk + a.fT1 / 4 + wave * 2 * 64, 2, lds, G_TIN, lane, c0, c1);
-        bias_relu(c0, bv);
-        bias_relu(c1, bv);
+        gemm_t1(t1a0, t1a1, lds, G_TIN, lane, c0, c1);
+        bias_relu(c0, t1b);
+        bias_relu(c1, t1b);
         acc_to_lds(c0, lds, G_H, wave * 32, 0, lane, nullptr, false);
         acc_to_lds(c1, lds, G_H, wave * 32, 1, lane, nullptr, false);
         lds_barrier();

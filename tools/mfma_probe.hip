@@ -41,7 +41,7 @@ __global__ __launch_bounds__(512) void k_probe(const float4 *__restrict__ A, flo
 }
 
 template <int MODE>
-static void run(const char *name, int blocks_per_cu, int lds_extra) {
+static void run(const char *name, int blocks_per_cu, int lds_extra, int threads = 512) {
     const int cus = 256, iters = 4096;
     float4 *A;
     float *out;
@@ -49,18 +49,19 @@ static void run(const char *name, int blocks_per_cu, int lds_extra) {
     hipMemset(A, 0, 32 * 64 * sizeof(float4));
     hipMalloc(&out, 4);
     const int blocks = cus * blocks_per_cu;
-    hipLaunchKernelGGL(k_probe<MODE>, dim3(blocks), dim3(512), lds_extra, 0, A, out, iters);
+    hipLaunchKernelGGL(k_probe<MODE>, dim3(blocks), dim3(threads), lds_extra, 0, A, out, iters);
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
     hipEventRecord(e0, 0);
-    for (int r = 0; r < 5; r++) hipLaunchKernelGGL(k_probe<MODE>, dim3(blocks), dim3(512), lds_extra, 0, A, out, iters);
+    for (int r = 0; r < 5; r++) hipLaunchKernelGGL(k_probe<MODE>, dim3(blocks), dim3(threads), lds_extra, 0, A, out, iters);
     hipEventRecord(e1, 0);
     hipEventSynchronize(e1);
     float ms = 0.f;
     hipEventElapsedTime(&ms, e0, e1);
-    const double flop = 5.0 * blocks * 8.0 /*waves*/ * iters * 8.0 /*mfma*/ * 32 * 32 * 2 * 2;
-    printf("%-28s blocks/CU=%d  %.1f TFLOP/s\n", name, blocks_per_cu, flop / (ms * 1e-3) / 1e12);
+    const double flop = 5.0 * blocks * (threads / 64.0) * iters * 8.0 /*mfma*/ * 32 * 32 * 2 * 2;
+    printf("%-28s blocks/CU=%d waves/block=%d  %.1f TFLOP/s\n", name, blocks_per_cu, threads / 64,
+           flop / (ms * 1e-3) / 1e12);
     hipFree(A);
     hipFree(out);
 }
@@ -72,5 +73,8 @@ int main() {
     run<0>("mfma only", 2, 0);
     run<1>("mfma + 2 ds_read_b128", 2, 0);
     run<2>("mfma + ds_read + global A", 2, 0);
+    run<0>("mfma only", 1, 0, 256);
+    run<1>("mfma + 2 ds_read_b128", 1, 0, 256);
+    run<2>("mfma + ds_read + global A", 1, 0, 256);
     return 0;
 }
