@@ -34,11 +34,11 @@ namespace mlp {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int BM = 64;          // points per workgroup
+constexpr int BM = 32;          // points per workgroup
 constexpr int NWAVE = 8;
 constexpr int NTHR = NWAVE * 64;
-// LDS group offsets (1 group = 64 points x 4 features = 1 KiB)
-constexpr int G_XE = 0, G_TE = 16, G_H = 24, G_TIN = 88, G_PART = 92, G_TOTAL = 124;
+// LDS group offsets (1 group = 32 points x 4 features = 512 B); PART = 8 K-part slots of 8 groups
+constexpr int G_XE = 0, G_TE = 16, G_H = 24, G_TIN = 88, G_PART = 92, G_TOTAL = 156;
 // padded feature offsets of the concatenated layer input (XE|TE|H)
 constexpr int F_XE = 0, F_TE = 64, F_H = 96;
 
@@ -255,47 +255,18 @@ __global__ __launch_bounds__(256) void k_pack_map(const int *__restrict__ map, P
     packed[i] = c < 0 ? 0.f : src.p[c >> PACK_SHIFT][c & ((1 << PACK_SHIFT) - 1)];
 }
 
-#ifdef DGS_MLP_PROFILE  // diagnostic build only (tools/mlp_phase.cpp): per-phase s_memtime stamps
-__device__ unsigned long long *dgs_mlp_prof;
-#define DGS_STAMP(k)                                                                               \
-    do {                                                                                           \
-        if (threadIdx.x == 0) dgs_mlp_prof[blockIdx.x * 256 + (k)] = __builtin_amdgcn_s_memtime(); \
-    } while (0)
-// per-wave: lane 0 of every wave records (k is per wave), plus the wave's SIMD (HW_ID bits 5:4)
-#define DGS_WSTAMP(k)                                                                              \
-    do {                                                                                           \
-        if ((threadIdx.x & 63) == 0)                                                               \
-            dgs_mlp_prof[blockIdx.x * 256 + (k) + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memtime(); \
-    } while (0)
-#define DGS_WSIMD(k)                                                                               \
-    do {                                                                                           \
-        if ((threadIdx.x & 63) == 0)                                                               \
-            dgs_mlp_prof[blockIdx.x * 256 + (k) + (threadIdx.x >> 6)] =                              \
-                (__builtin_amdgcn_s_getreg(0xF804) >> 4) & 3;                                      \
-    } while (0)
-#else
-#define DGS_WSTAMP(k) \
-    do {              \
-    } while (0)
-#define DGS_WSIMD(k) \
-    do {             \
-    } while (0)
-#define DGS_STAMP(k) \
-    do {             \
-    } while (0)
-#endif
 
 // ------------------------------------------------------------------------------------------------
 // device GEMM pieces
 // ------------------------------------------------------------------------------------------------
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS traffic (lgkmcnt 0) but not
-// for its global stores. __syncthreads() also waits vmcnt(0) (release fence), which parked every
-// wave ~5 us per layer on the saved-activation stores. No wave of k_mlp_* reads global memory
-// another wave of the block wrote.
+// for its global stores (__syncthreads() also waits vmcnt(0), a release fence). No wave of
+// k_mlp_* reads global memory another wave of the block wrote.
 __device__ inline void lds_barrier() {
     __builtin_amdgcn_s_waitcnt(0xc07f);  // gfx9 encoding: vmcnt 63, expcnt 7, lgkmcnt 0
     __builtin_amdgcn_s_barrier();
 }
+
 __device__ inline f32x16 zero16() {
     f32x16 z;
 #pragma unroll
@@ -305,162 +276,110 @@ __device__ inline f32x16 zero16() {
 
 #define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_32x32x2f32((a), (b), (c), 0, 0, 0)
 
-// Deferred LDS -> HBM copy of up to three group ranges of feature-major [rows][Ns] arrays (saved
-// activations in the forward, dZ in the backward). A unit = 4 features x 1 point: one
-// ds_read_b128 + 4 coalesced 256-B wave stores. The GEMMs issue a FIXED number of units per 4-chunk
-// group, straight-line, so the compiler's vmcnt bookkeeping (stores count on gfx9) is exact and the
-// A-fragment waits never wait for these stores; a unit past the end rewrites the last unit (same
-// data to the same address).
-struct Pending {
-    int g0[3], r0[3], end[3];  // LDS group, output row, cumulative end (float4 units) per range
-    int n, pos, total;
-    __device__ void clear() {
-        n = 0; pos = 0; total = 0;
-        end[0] = end[1] = end[2] = 0x7fffffff;
-        g0[0] = g0[1] = g0[2] = 0;
-        r0[0] = r0[1] = r0[2] = 0;
-    }
-    __device__ void add(int g, int ngr, int r) {
-        g0[n] = g; r0[n] = r;
-        total += ngr * BM;
-        end[n] = total;
-        n++;
-    }
-    __device__ void set1(int g, int ngr, int r) { clear(); add(g, ngr, r); }
-};
+#ifdef DGS_MLP_PROFILE  // diagnostic build only (tools/mlp_phase.cpp): per-phase s_memtime stamps
+__device__ unsigned long long *dgs_mlp_prof;
+#define DGS_STAMP(k)                                                                                \
+    do {                                                                                            \
+        if (threadIdx.x == 0) dgs_mlp_prof[blockIdx.x * 256 + (k)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define DGS_STAMP(k) \
+    do {             \
+    } while (0)
+#endif
 
-struct PendingSide {
-    Pending *q;
+// The network inputs (positional encodings) leave LDS for the saved-activation array in the first
+// trunk GEMM's prologue: XE and TE are adjacent both in LDS (groups 0..23) and in the saved rows
+// (S_XE.. S_XE + 95), TIN (blender) is one more range. A unit = 4 features x 1 point: one
+// ds_read_b128 + 4 coalesced stores; a fixed unit count keeps the GEMM straight-line.
+struct InputStore {
     const float4 *lds;
     float *dst;
     size_t Ns;
     int p0, tid;
-    __device__ void unit() const {
-        Pending &Q = *q;
-        int e = min(tid + NTHR * Q.pos, Q.total - 1);
-        Q.pos++;
-        const bool k1 = e >= Q.end[0], k2 = e >= Q.end[1];
-        const int base = k2 ? Q.end[1] : (k1 ? Q.end[0] : 0);
-        const int g0 = k2 ? Q.g0[2] : (k1 ? Q.g0[1] : Q.g0[0]);
-        const int r0 = k2 ? Q.r0[2] : (k1 ? Q.r0[1] : Q.r0[0]);
-        e -= base;
-        const int gi = e / BM, m = e % BM;
-        const float4 v = lds[(g0 + gi) * BM + m];
-        float *d = dst + (size_t)(r0 + 4 * gi) * Ns + p0 + m;
+    bool blender;
+    __device__ void put(int g, int m, int row) const {
+        const float4 v = lds[g * BM + m];
+        float *d = dst + (size_t)row * Ns + p0 + m;
         d[0] = v.x;
         d[Ns] = v.y;
         d[2 * Ns] = v.z;
         d[3 * Ns] = v.w;
     }
-    __device__ void flush() const {
-        while (q->pos * NTHR < q->total) unit();
-        q->clear();
+    __device__ void operator()() const {
+        static_assert(G_TE == G_XE + 16 && S_TE == S_XE + 64, "XE|TE must be one range");
+#pragma unroll
+        for (int u = 0; u < 2; u++) {  // 24 groups x 32 points = 768 units over 512 threads
+            const int e = min(tid + NTHR * u, 24 * BM - 1);  // past the end: rewrite the last unit
+            put(G_XE + e / BM, e % BM, S_XE + 4 * (e / BM));
+        }
+        if (blender && tid < 4 * BM) put(G_TIN + tid / BM, tid % BM, S_TIN + 4 * (tid / BM));  // waves 0-1
     }
-};
-
-struct NoSide {
-    __device__ void unit() const {}
-    __device__ void flush() const {}
 };
 
 struct NoPre {
     __device__ void operator()() const {}
 };
 
-// bias preload plus U side units (a fixed count), run after a GEMM's prologue loads
-template <int U>
-struct PreUnits;
-
-// The previous layer's output tiles of this wave (rows n0 + 8(r>>2) + 4h + (r&3), points m and
-// 32 + m), kept in registers and written to a feature-major [rows][Ns] array during the first four
-// chunks of the next GEMM: 8 plain coalesced stores per chunk, issued after that GEMM's prologue
-// loads so no A-fragment wait depends on them, with no LDS read and no index arithmetic.
+// The previous layer's output tile of this wave (rows n0 + 8(r>>2) + 4h + (r&3), point m), kept in
+// registers and written to a feature-major [rows][Ns] array during the first two chunks of the
+// next GEMM: 8 plain coalesced stores per chunk, issued after that GEMM's prologue loads so no
+// A-fragment wait depends on them, with no LDS read and no index arithmetic.
 struct NoStash {
     __device__ void store(int) const {}
 };
 
-struct Stash2 {
-    f32x16 t0, t1;
-    float *d;  // &dst[(row0 + n0 + 4h) * Ns + p0 + m]
-    int ns;
-    __device__ void store(int k) const {
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const int idx = 8 * k + j, r = idx & 15;
-            const float v = (idx >> 4) ? t1[r] : t0[r];
-            d[(8 * (r >> 2) + (r & 3)) * ns + (idx >> 4) * 32] = v;
-        }
+// A wave's 32-row tile of a feature-major [rows][Ns] array, addressed through a buffer descriptor
+// whose base is the tile origin (wave-uniform: SGPRs): each access is one buffer instruction with
+// the lane offset in a VGPR and the row offset in an SGPR, no per-access address arithmetic (which
+// the compiler otherwise hoists into 16 live 64-bit addresses).
+struct TileAddr {
+    __amdgpu_buffer_rsrc_t rsrc;  // base = &dst[(row0 + n0) * Ns + p0]
+    int voff;                     // (4h * Ns + m) * 4 bytes
+    int ns4;                      // Ns * 4 bytes
+    __device__ static constexpr int row(int r) { return 8 * (r >> 2) + (r & 3); }
+    __device__ void st(int r, float v) const {
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc, voff, row(r) * ns4, 0);
     }
-    __device__ void store_all() const {
-#pragma unroll
-        for (int k = 0; k < 4; k++) store(k);
+    __device__ float ld(int r) const {
+        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, row(r) * ns4, 0));
     }
 };
 
-// acc0/acc1 (m-tiles 0/1) += A . X over NCH chunks starting at chunk c0 of the A image and of the
-// LDS image at group g0 (chunk c = groups g0 + 2c + h). Fully unrolled straight-line schedule (no
-// loop back-edge, so no register rotation and exact compiler vmcnt/lgkmcnt bookkeeping): per chunk
-// the A fragment 4 chunks ahead (4-deep ring, issued before this chunk's MFMAs), the next chunk's B
-// (double-buffered ds_read_b128), 8 MFMAs, and on every 4th chunk SPG side units. pre() runs after
-// the A prologue (its global loads are younger than the first fragments).
-template <int NCH, int SPG, class Side, class Pre = NoPre, class Stash = NoStash>
-__device__ inline void gemm_2m(const float4 *__restrict__ Apk, int c0, const float4 *lds, int g0, int lane,
-                               f32x16 &acc0, f32x16 &acc1, const Side &side, Pre pre = Pre(),
-                               const Stash &stash = Stash(), int g_chunk_stamp = -1) {
+__device__ inline TileAddr tile_addr(const float *dst, size_t Ns, int row0, int n0, int p0, int lane) {
+    const float *base = dst + (size_t)(row0 + n0) * Ns + p0;
+    // a 32-row tile spans 32 * Ns floats; the descriptor's record count only bounds-checks
+    return TileAddr{__builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(base), 0, 0x7fffffff, 0x00020000),
+                    (4 * (lane >> 5) * (int)Ns + (lane & 31)) * 4, (int)Ns * 4};
+}
+
+struct Stash1 {
+    f32x16 t;
+    TileAddr d;
+    __device__ void store(int k) const {
+#pragma unroll
+        for (int j = 0; j < 8; j++) d.st(8 * k + j, t[8 * k + j]);
+    }
+    __device__ void store_all() const {
+        store(0);
+        store(1);
+    }
+};
+
+// acc += A . X over NCH chunks starting at chunk c0 of the A image and of the LDS image at group g0
+// (chunk c = groups g0 + 2c + h). Fully unrolled straight-line schedule: per chunk the A fragment 4
+// chunks ahead (4-deep ring) and the next chunk's B (double-buffered ds_read_b128) are issued
+// before this chunk's 4 MFMAs (sched_barrier keeps that order; the scheduler otherwise sinks the
+// loads next to their use; the dependent MFMA chain is covered by the SIMD's other 3 waves), and
+// the stash stores in chunks 0-1. pre() runs after the A prologue (its loads are younger than the
+// first fragments).
+template <int NCH, class Pre = NoPre, class Stash = NoStash>
+__device__ inline void gemm(const float4 *__restrict__ Apk, int c0, const float4 *lds, int g0, int lane, f32x16 &acc,
+                            Pre pre = Pre(), const Stash stash = Stash()) {
     static_assert(NCH >= 1, "empty GEMM");
     const int h = lane >> 5, m = lane & 31;
     const float4 *Ap = Apk + c0 * 64 + lane;
     const float4 *Bp = lds + (g0 + 2 * c0 + h) * BM + m;
-    float4 ring[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-        if (k < NCH) ring[k] = Ap[k * 64];
-    pre();
-    float4 bx[2], by[2];
-    bx[0] = Bp[0];
-    by[0] = Bp[32];
-#pragma unroll
-    for (int k = 0; k < NCH; k++) {
-        const float4 a = ring[k & 3];
-        if (k + 4 < NCH) ring[k & 3] = Ap[(k + 4) * 64];
-        if (k + 1 < NCH) {
-            bx[(k + 1) & 1] = Bp[2 * (k + 1) * BM];
-            by[(k + 1) & 1] = Bp[2 * (k + 1) * BM + 32];
-        }
-        // issue the loads before this chunk's MFMAs (else the scheduler sinks the next B read
-        // behind them and reuses the current B registers, exposing LDS latency every chunk)
-        __builtin_amdgcn_sched_barrier(0);
-        const float4 b0 = bx[k & 1], b1 = by[k & 1];
-        acc0 = MFMA(a.x, b0.x, acc0);
-        acc1 = MFMA(a.x, b1.x, acc1);
-        acc0 = MFMA(a.y, b0.y, acc0);
-        acc1 = MFMA(a.y, b1.y, acc1);
-        acc0 = MFMA(a.z, b0.z, acc0);
-        acc1 = MFMA(a.z, b1.z, acc1);
-        acc0 = MFMA(a.w, b0.w, acc0);
-        acc1 = MFMA(a.w, b1.w, acc1);
-        if ((k & 3) == 0) {
-#pragma unroll
-            for (int s_ = 0; s_ < SPG; s_++) side.unit();
-        }
-        if (k < 4) stash.store(k);
-#ifdef DGS_MLP_PROFILE
-        if (g_chunk_stamp >= 0 && (threadIdx.x & 63) == 0 && ((threadIdx.x >> 6) & 3) == 0)
-            dgs_mlp_prof[blockIdx.x * 256 + g_chunk_stamp + (threadIdx.x >> 8) * 64 + k] = __builtin_amdgcn_s_memtime();
-#endif
-        // keep the schedule: without this fence the scheduler sinks each A load next to its use
-        // (minimising registers) and every chunk waits a full L2 round trip
-        __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
-// single m-tile variant (narrow K-split layers), same schedule
-template <int NCH, int SPG, class Side, class Pre = NoPre, class Stash = NoStash>
-__device__ inline void gemm_1m(const float4 *__restrict__ Apk, int c0, const float4 *lds, int g0, int mt, int lane,
-                               f32x16 &acc, const Side &side, Pre pre = Pre(), const Stash &stash = Stash()) {
-    const int h = lane >> 5, m = lane & 31;
-    const float4 *Ap = Apk + c0 * 64 + lane;
-    const float4 *Bp = lds + (g0 + 2 * c0 + h) * BM + mt * 32 + m;
     float4 ring[4];
 #pragma unroll
     for (int k = 0; k < 4; k++)
@@ -479,53 +398,32 @@ __device__ inline void gemm_1m(const float4 *__restrict__ Apk, int c0, const flo
         acc = MFMA(a.y, b.y, acc);
         acc = MFMA(a.z, b.z, acc);
         acc = MFMA(a.w, b.w, acc);
-        if ((k & 3) == 0) {
-#pragma unroll
-            for (int s_ = 0; s_ < SPG; s_++) side.unit();
-        }
-        if (k < 4) stash.store(k);
-        // keep the schedule: without this fence the scheduler sinks each A load next to its use
-        // (minimising registers) and every chunk waits a full L2 round trip
+        if (k < 2) stash.store(k);
         __builtin_amdgcn_sched_barrier(0);
     }
 }
 
 // timenet layer 0 (2 chunks) with its A fragments loaded by the caller (before the PE phase)
-__device__ inline void gemm_t1(const float4 a0, const float4 a1, const float4 *lds, int g0, int lane, f32x16 &acc0,
-                               f32x16 &acc1) {
+__device__ inline void gemm_t1(const float4 a0, const float4 a1, const float4 *lds, int g0, int lane, f32x16 &acc) {
     const int h = lane >> 5, m = lane & 31;
 #pragma unroll
     for (int c = 0; c < 2; c++) {
         const float4 a = c ? a1 : a0;
-        const float4 *grp = lds + (g0 + 2 * c + h) * BM;
-        const float4 b0 = grp[m], b1 = grp[32 + m];
-        acc0 = MFMA(a.x, b0.x, acc0);
-        acc1 = MFMA(a.x, b1.x, acc1);
-        acc0 = MFMA(a.y, b0.y, acc0);
-        acc1 = MFMA(a.y, b1.y, acc1);
-        acc0 = MFMA(a.z, b0.z, acc0);
-        acc1 = MFMA(a.z, b1.z, acc1);
-        acc0 = MFMA(a.w, b0.w, acc0);
-        acc1 = MFMA(a.w, b1.w, acc1);
+        const float4 b = lds[(g0 + 2 * c + h) * BM + m];
+        acc = MFMA(a.x, b.x, acc);
+        acc = MFMA(a.y, b.y, acc);
+        acc = MFMA(a.z, b.z, acc);
+        acc = MFMA(a.w, b.w, acc);
     }
 }
 
-// accumulator (n-tile base n0, m-tile mt) -> LDS groups starting at gout, with bias/relu
-__device__ inline void acc_to_lds(const f32x16 &acc, float4 *lds, int gout, int n0, int mt, int lane,
-                                  const float *bias, bool relu) {
+// accumulator (n-tile base n0) -> LDS groups starting at gout
+__device__ inline void acc_to_lds(const f32x16 &acc, float4 *lds, int gout, int n0, int lane) {
     const int h = lane >> 5, m = lane & 31;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-        int f = n0 + 8 * j + 4 * h;
-        float4 v = make_float4(acc[4 * j], acc[4 * j + 1], acc[4 * j + 2], acc[4 * j + 3]);
-        if (bias) {
-            float4 b = *reinterpret_cast<const float4 *>(bias + f);
-            v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
-        }
-        if (relu) {
-            v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
-        }
-        lds[(gout + f / 4) * BM + mt * 32 + m] = v;
+        const int f = n0 + 8 * j + 4 * h;
+        lds[(gout + f / 4) * BM + m] = make_float4(acc[4 * j], acc[4 * j + 1], acc[4 * j + 2], acc[4 * j + 3]);
     }
 }
 
@@ -534,27 +432,14 @@ struct Bias4 {
     float4 v[4];
 };
 
-struct BiasPre {
-    Bias4 *b;
-    const float *bias;
-    int n0, lane;
-    __device__ void operator()() const {
-        const int h = lane >> 5;
+__device__ inline Bias4 load_bias(const float *bias, int n0, int lane) {
+    const int h = lane >> 5;
+    Bias4 b;
 #pragma unroll
-        for (int j = 0; j < 4; j++) b->v[j] = *reinterpret_cast<const float4 *>(bias + n0 + 8 * j + 4 * h);
-    }
-};
+    for (int j = 0; j < 4; j++) b.v[j] = *reinterpret_cast<const float4 *>(bias + n0 + 8 * j + 4 * h);
+    return b;
+}
 
-template <int U>
-struct PreUnits {
-    BiasPre bp;
-    const PendingSide *ps;
-    __device__ void operator()() const {
-        bp();
-#pragma unroll
-        for (int u = 0; u < U; u++) ps->unit();
-    }
-};
 
 // acc = relu(acc + bias) in place (the values kept for the deferred store)
 __device__ inline void bias_relu(f32x16 &acc, const Bias4 &b) {
@@ -564,22 +449,6 @@ __device__ inline void bias_relu(f32x16 &acc, const Bias4 &b) {
         acc[4 * j + 1] = fmaxf(acc[4 * j + 1] + b.v[j].y, 0.f);
         acc[4 * j + 2] = fmaxf(acc[4 * j + 2] + b.v[j].z, 0.f);
         acc[4 * j + 3] = fmaxf(acc[4 * j + 3] + b.v[j].w, 0.f);
-    }
-}
-
-// accumulator + preloaded bias, relu -> LDS groups starting at gout
-__device__ inline void acc_bias_relu_to_lds(const f32x16 &acc, const Bias4 &b, float4 *lds, int gout, int n0, int mt,
-                                            int lane) {
-    const int h = lane >> 5, m = lane & 31;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const int f = n0 + 8 * j + 4 * h;
-        float4 v;
-        v.x = fmaxf(acc[4 * j] + b.v[j].x, 0.f);
-        v.y = fmaxf(acc[4 * j + 1] + b.v[j].y, 0.f);
-        v.z = fmaxf(acc[4 * j + 2] + b.v[j].z, 0.f);
-        v.w = fmaxf(acc[4 * j + 3] + b.v[j].w, 0.f);
-        lds[(gout + f / 4) * BM + mt * 32 + m] = v;
     }
 }
 
@@ -595,36 +464,18 @@ __device__ inline void lds_to_global(const float4 *lds, int g0, int ng, float *_
     }
 }
 
-// ------------------------------------------------------------------------------------------------
-// forward
-// ------------------------------------------------------------------------------------------------
-
-struct FwdArgs {
-    int N;
-    size_t Ns;
-    const float *xyz, *t;
-    const float *packed;
-    float *out;
-    float *saved;
-    int fT1, fT2, fL[8], fHd, bT1, bT2, bL[8], bHd;
-    int flags;
-};
-
-// 4 K-quarter partials (PART slots) -> sum in a fixed order (+bias) -> LDS groups gout..gout+7
+// 8 K-part partials (PART slots) -> sum in a fixed order (+bias) -> LDS groups gout..gout+7
 __device__ inline void sum_parts(float4 *lds, int gout, const float *bias, int tid, bool accumulate) {
     for (int e = tid; e < 8 * BM; e += NTHR) {
-        int gi = e / BM, m = e % BM;
-        float4 s0 = lds[(G_PART + gi) * BM + m];
-        float4 s1 = lds[(G_PART + 8 + gi) * BM + m];
-        float4 s2 = lds[(G_PART + 16 + gi) * BM + m];
-        float4 s3 = lds[(G_PART + 24 + gi) * BM + m];
-        float4 r;
-        r.x = ((s0.x + s1.x) + s2.x) + s3.x;
-        r.y = ((s0.y + s1.y) + s2.y) + s3.y;
-        r.z = ((s0.z + s1.z) + s2.z) + s3.z;
-        r.w = ((s0.w + s1.w) + s2.w) + s3.w;
+        const int gi = e / BM, m = e % BM;
+        float4 r = lds[(G_PART + gi) * BM + m];
+#pragma unroll
+        for (int q = 1; q < NWAVE; q++) {
+            const float4 v = lds[(G_PART + 8 * q + gi) * BM + m];
+            r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
+        }
         if (bias) {
-            float4 b = *reinterpret_cast<const float4 *>(bias + 4 * gi);
+            const float4 b = *reinterpret_cast<const float4 *>(bias + 4 * gi);
             r.x += b.x; r.y += b.y; r.z += b.z; r.w += b.w;
         }
         float4 &d = lds[(gout + gi) * BM + m];
@@ -636,39 +487,55 @@ __device__ inline void sum_parts(float4 *lds, int gout, const float *bias, int t
     }
 }
 
-// narrow layer: 1 output n-tile, K split over 8 waves (4 quarters x 2 m-tiles), fixed-order sum,
-// result (+bias) written to LDS groups gout..gout+7 (32 features)
+// narrow layer (32 output rows): K (32 chunks) split over the 8 waves, 4 chunks each, partials
+// summed in a fixed order (+bias) into LDS groups gout..gout+7
 template <class Stash = NoStash>
 __device__ inline void narrow_layer(const float4 *Apk, float4 *lds, int g0, int gout, const float *bias, int wave,
-                                    int lane, int tid, const Stash &stash = Stash()) {
-    const int mt = wave & 1, q = wave >> 1;
+                                    int lane, int tid, const Stash stash = Stash()) {
     f32x16 acc = zero16();
-    gemm_1m<8, 0>(Apk, q * 8, lds, g0, mt, lane, acc, NoSide(), NoPre(), stash);  // 32 chunks = 4 x 8
-    acc_to_lds(acc, lds, G_PART + 8 * q, 0, mt, lane, nullptr, false);
+    gemm<4>(Apk, wave * 4, lds, g0, lane, acc, NoPre(), stash);
+    acc_to_lds(acc, lds, G_PART + 8 * wave, 0, lane);
     lds_barrier();
     sum_parts(lds, gout, bias, tid, false);
     lds_barrier();
 }
 
+// ------------------------------------------------------------------------------------------------
+// forward
+// ------------------------------------------------------------------------------------------------
+struct FwdArgs {
+    int N;
+    size_t Ns;
+    const float *xyz, *t;
+    const float *packed;
+    float *out;
+    float *saved;
+    int fT1, fT2, fL[8], fHd, bT1, bT2, bL[8], bHd;
+    int flags;
+};
+
+// Workgroup = 32 points x 8 waves (wave w owns output rows 32w..32w+31 of every 256-wide layer);
+// 80 KB of LDS, so two workgroups share a CU (4 waves per SIMD): one block's barrier waits and
+// epilogues run under the other's MFMAs, and a partial last round of blocks runs at full rate.
 template <bool SAVE>
-__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_mlp_fwd(FwdArgs a) {
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_mlp_fwd(FwdArgs a) {
     __shared__ float4 lds[G_TOTAL * BM];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform (scalar branches)
     const int p0 = blockIdx.x * BM;
     const Flags F = make_flags(a.flags);
     const float4 *pk = reinterpret_cast<const float4 *>(a.packed);
+    float *lf = reinterpret_cast<float *>(lds);
     DGS_STAMP(0);
     // timenet layer 0 operands, in flight during the positional encodings
     float4 t1a0 = make_float4(0.f, 0.f, 0.f, 0.f), t1a1 = t1a0;
-    Bias4 t1b;
+    Bias4 t1b{};
     if (F.blender) {
         const float4 *At1 = pk + a.fT1 / 4 + wave * 2 * 64 + lane;
         t1a0 = At1[0];
         t1a1 = At1[64];
-        BiasPre{&t1b, a.packed + a.bT1, wave * 32, lane}();
+        t1b = load_bias(a.packed + a.bT1, wave * 32, lane);
     }
-    float *lf = reinterpret_cast<float *>(lds);
     // ---- positional encodings (utils/time_utils.py:42-54) ----
     for (int e = tid; e < 64 * BM; e += NTHR) {
         int m = e % BM, f = e / BM;
@@ -709,84 +576,59 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
     }
     lds_barrier();
     DGS_STAMP(1);
-    // saved activations: the network inputs (XE, TIN | TE) and T2's output leave LDS in the first
-    // trunk GEMM's prologue (fixed 4 units); every hidden layer's output is kept in registers and
-    // stored during the next GEMM (Stash2)
-    Pending pend;
-    pend.clear();
-    const PendingSide ps{&pend, lds, a.saved, a.Ns, p0, tid};
-    if (SAVE) {
-        pend.add(G_XE, 16, S_XE);
-        if (F.blender) pend.add(G_TIN, 4, S_TIN);
-        else pend.add(G_TE, 8, S_TE);
-    }
+    // saved activations: the network inputs (XE|TE, TIN) leave LDS in the first trunk GEMM's
+    // prologue (InputStore); every hidden layer's output is kept in registers and stored during the
+    // next GEMM (Stash1)
     const float *bias = a.packed;
-    const int h = lane >> 5, m32 = lane & 31;
-    const int ns32 = (int)a.Ns;
-    float *const sv_lane = a.saved + (size_t)(wave * 32 + 4 * h) * a.Ns + p0 + m32;  // + row0 * Ns
-    f32x16 k0 = zero16(), k1 = zero16();  // previous layer's activations, awaiting their store
+    f32x16 kt = zero16();  // previous layer's activations, awaiting their store
     // ---- timenet (blender): Linear(13,256) + ReLU -> H ; Linear(256,30) -> TE ----
     if (F.blender) {
-        f32x16 c0 = zero16(), c1 = zero16();
-        gemm_t1(t1a0, t1a1, lds, G_TIN, lane, c0, c1);
-        bias_relu(c0, t1b);
-        bias_relu(c1, t1b);
-        acc_to_lds(c0, lds, G_H, wave * 32, 0, lane, nullptr, false);
-        acc_to_lds(c1, lds, G_H, wave * 32, 1, lane, nullptr, false);
+        f32x16 c = zero16();
+        gemm_t1(t1a0, t1a1, lds, G_TIN, lane, c);
+        bias_relu(c, t1b);
+        acc_to_lds(c, lds, G_H, wave * 32, lane);
         lds_barrier();
         DGS_STAMP(2);
         if (SAVE)
             narrow_layer(pk + a.fT2 / 4, lds, G_H, G_TE, bias + a.bT2, wave, lane, tid,
-                         Stash2{c0, c1, sv_lane + (size_t)S_TH * a.Ns, ns32});
+                         Stash1{c, tile_addr(a.saved, a.Ns, S_TH, wave * 32, p0, lane)});
         else
             narrow_layer(pk + a.fT2 / 4, lds, G_H, G_TE, bias + a.bT2, wave, lane, tid);
-        if (SAVE) pend.add(G_TE, 8, S_TE);
     }
     DGS_STAMP(3);
     // ---- trunk: 8 x (Linear + ReLU), skip cat after layer 4 (time_utils.py:107-112) ----
     for (int L = 0; L < 8; L++) {
         const int g0 = (L == 0 || L == 5) ? G_XE : G_H;
         const int nch = layer_kpad(L) / 8;
-        f32x16 c0 = zero16(), c1 = zero16();
+        f32x16 c = zero16();
         const float4 *Aw = pk + a.fL[L] / 4 + wave * nch * 64;
-        Bias4 bv;
-        const BiasPre bp{&bv, bias + a.bL[L], wave * 32, lane};
+        const Bias4 bv = load_bias(bias + a.bL[L], wave * 32, lane);
         if (L == 0) {
-            if (SAVE) gemm_2m<12, 0>(Aw, 0, lds, g0, lane, c0, c1, NoSide(), PreUnits<4>{bp, &ps});
-            else gemm_2m<12, 0>(Aw, 0, lds, g0, lane, c0, c1, NoSide(), bp);
+            if (SAVE) gemm<12>(Aw, 0, lds, g0, lane, c, InputStore{lds, a.saved, a.Ns, p0, tid, F.blender});
+            else gemm<12>(Aw, 0, lds, g0, lane, c);
         } else {
-            const Stash2 st{k0, k1, sv_lane + (size_t)s_h(L - 1) * a.Ns, ns32};
+            const Stash1 st{kt, tile_addr(a.saved, a.Ns, s_h(L - 1), wave * 32, p0, lane)};
             if (L == 5) {
-                if (SAVE) gemm_2m<44, 0>(Aw, 0, lds, g0, lane, c0, c1, NoSide(), bp, st);
-                else gemm_2m<44, 0>(Aw, 0, lds, g0, lane, c0, c1, NoSide(), bp);
+                if (SAVE) gemm<44>(Aw, 0, lds, g0, lane, c, NoPre(), st);
+                else gemm<44>(Aw, 0, lds, g0, lane, c);
             } else {
-#ifdef DGS_MLP_PROFILE
-                if (SAVE) gemm_2m<32, 0>(Aw, 0, lds, g0, lane, c0, c1, NoSide(), bp, st, L == 1 ? 64 : -1);
-#else
-                if (SAVE) gemm_2m<32, 0>(Aw, 0, lds, g0, lane, c0, c1, NoSide(), bp, st);
-#endif
-                else gemm_2m<32, 0>(Aw, 0, lds, g0, lane, c0, c1, NoSide(), bp);
+                if (SAVE) gemm<32>(Aw, 0, lds, g0, lane, c, NoPre(), st);
+                else gemm<32>(Aw, 0, lds, g0, lane, c);
             }
         }
         DGS_STAMP(4 + 3 * L);
-        if (L == 1) DGS_WSTAMP(40);
-        if (L == 0) DGS_WSIMD(48);
         lds_barrier();  // all waves finished reading H before it is overwritten
         DGS_STAMP(5 + 3 * L);
-        bias_relu(c0, bv);
-        bias_relu(c1, bv);
-        acc_to_lds(c0, lds, G_H, wave * 32, 0, lane, nullptr, false);
-        acc_to_lds(c1, lds, G_H, wave * 32, 1, lane, nullptr, false);
+        bias_relu(c, bv);
+        acc_to_lds(c, lds, G_H, wave * 32, lane);
         lds_barrier();
         DGS_STAMP(6 + 3 * L);
-        if (L == 0) DGS_WSTAMP(32);
-        k0 = c0;
-        k1 = c1;
+        kt = c;
     }
     // ---- heads (no activation): [warp | branch_w, branch_v], rotation, scaling -> TE region ----
     if (SAVE)
         narrow_layer(pk + a.fHd / 4, lds, G_H, G_TE, bias + a.bHd, wave, lane, tid,
-                     Stash2{k0, k1, sv_lane + (size_t)s_h(7) * a.Ns, ns32});
+                     Stash1{kt, tile_addr(a.saved, a.Ns, s_h(7), wave * 32, p0, lane)});
     else
         narrow_layer(pk + a.fHd / 4, lds, G_H, G_TE, bias + a.bHd, wave, lane, tid);
     DGS_STAMP(28);
@@ -812,18 +654,15 @@ struct BwdArgs {
     int flags;
 };
 
-// relu' mask rows of one 32x32 accumulator tile (the saved activations of the layer input)
+// relu' mask rows of this wave's 32x32 accumulator tile (the saved activations of the layer input)
 struct Mask16 {
     float v[16];
 };
 
-__device__ inline void mask_load(Mask16 &mk, const float *__restrict__ saved_rows, size_t Ns, int p0, int mt, int lane,
-                                 int n0) {
-    const int h = lane >> 5, m = lane & 31;
-    const float *sv = saved_rows + (size_t)(n0 + 4 * h) * Ns + p0 + mt * 32 + m;
-    const int ns = (int)Ns;  // a 32-row tile spans < 2^31 floats
+__device__ inline void mask_load(Mask16 &mk, const float *__restrict__ saved_rows, size_t Ns, int p0, int lane, int n0) {
+    const TileAddr t = tile_addr(saved_rows, Ns, 0, n0, p0, lane);
 #pragma unroll
-    for (int r = 0; r < 16; r++) mk.v[r] = sv[(8 * (r >> 2) + (r & 3)) * ns];
+    for (int r = 0; r < 16; r++) mk.v[r] = t.ld(r);
 }
 
 __device__ inline void mask_apply(f32x16 &acc, const Mask16 &mk) {
@@ -831,30 +670,15 @@ __device__ inline void mask_apply(f32x16 &acc, const Mask16 &mk) {
     for (int r = 0; r < 16; r++) acc[r] = mk.v[r] > 0.f ? acc[r] : 0.f;
 }
 
-__device__ inline void mask_store(f32x16 &acc, const float *__restrict__ saved_rows, float *__restrict__ dz_rows,
-                                  size_t Ns, int p0, int mt, int lane, int n0) {
-    Mask16 mk;
-    mask_load(mk, saved_rows, Ns, p0, mt, lane, n0);
-    mask_apply(acc, mk);
-    const int h = lane >> 5, m = lane & 31;
-    float *dz = dz_rows + (size_t)(n0 + 4 * h) * Ns + p0 + mt * 32 + m;
-    const int ns = (int)Ns;
-#pragma unroll
-    for (int r = 0; r < 16; r++) dz[(8 * (r >> 2) + (r & 3)) * ns] = acc[r];
-}
-
-struct MaskPre {  // both m-tiles' relu' masks, issued after the GEMM prologue
-    Mask16 *mk0, *mk1;
+struct MaskPre {  // the tile's relu' mask, issued after the GEMM prologue
+    Mask16 *mk;
     const float *rows;
     size_t Ns;
     int p0, lane, n0;
-    __device__ void operator()() const {
-        mask_load(*mk0, rows, Ns, p0, 0, lane, n0);
-        mask_load(*mk1, rows, Ns, p0, 1, lane, n0);
-    }
+    __device__ void operator()() const { mask_load(*mk, rows, Ns, p0, lane, n0); }
 };
 
-__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_mlp_bwd(BwdArgs a) {
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_mlp_bwd(BwdArgs a) {
     __shared__ float4 lds[G_TOTAL * BM];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform (scalar branches)
@@ -871,24 +695,18 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
         a.dz[(size_t)(Z_G + c) * a.Ns + p] = v;
     }
     lds_barrier();
-    // dZ_i of the trunk stays in registers and is stored during the next GEMM (Stash2)
-    const int h = lane >> 5, m32 = lane & 31;
-    const int ns32 = (int)a.Ns;
-    float *const dz_lane = a.dz + (size_t)(wave * 32 + 4 * h) * a.Ns + p0 + m32;  // + row0 * Ns
-    f32x16 k0, k1;  // dZ of the layer whose GEMM runs next
+    // dZ_i of the trunk stays in registers and is stored during the next GEMM (Stash1)
+    f32x16 kt;  // dZ of the layer whose GEMM runs next
     // heads^T: dH7 = W_h^T dOut (K = 32 from TE region) -> mask H7 -> dZ7
     {
-        Mask16 mk0, mk1;
-        f32x16 c0 = zero16(), c1 = zero16();
-        gemm_2m<4, 0>(pk + a.tHd / 4 + wave * 4 * 64, 0, lds, G_TE, lane, c0, c1, NoSide(),
-                      MaskPre{&mk0, &mk1, a.saved + (size_t)s_h(7) * a.Ns, a.Ns, p0, lane, wave * 32});
-        mask_apply(c0, mk0);
-        mask_apply(c1, mk1);
+        Mask16 mk;
+        f32x16 c = zero16();
+        gemm<4>(pk + a.tHd / 4 + wave * 4 * 64, 0, lds, G_TE, lane, c,
+                MaskPre{&mk, a.saved + (size_t)s_h(7) * a.Ns, a.Ns, p0, lane, wave * 32});
+        mask_apply(c, mk);
         lds_barrier();  // TE (dOut image) reads done before TE is reused for dTE
-        acc_to_lds(c0, lds, G_H, wave * 32, 0, lane, nullptr, false);
-        acc_to_lds(c1, lds, G_H, wave * 32, 1, lane, nullptr, false);
-        k0 = c0;
-        k1 = c1;
+        acc_to_lds(c, lds, G_H, wave * 32, lane);
+        kt = c;
     }
     // zero the dTE accumulator (TE region holds dL/dt_emb from layers 5 and 0)
     for (int e = tid; e < 8 * BM; e += NTHR) lds[G_TE * BM + e] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -897,38 +715,33 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
         // dX_L = W_L^T dZ_L ; H-part rows of the padded input live at tiles (F_H/32 + w) for L=5
         const int tile0 = (L == 5) ? F_H / 32 : 0;
         if (L == 5 && F.blender) {
-            // t_emb slice (padded rows 64..95 = tile 2): narrow K-split partials -> PART
-            const int mt = wave & 1, q = wave >> 1;
+            // t_emb slice (padded rows 64..95 = tile 2): K split over the 8 waves -> PART
             f32x16 ct = zero16();
-            gemm_1m<8, 0>(pk + a.tL[5] / 4 + (F_TE / 32) * 32 * 64, q * 8, lds, G_H, mt, lane, ct, NoSide());
-            acc_to_lds(ct, lds, G_PART + 8 * q, 0, mt, lane, nullptr, false);
+            gemm<4>(pk + a.tL[5] / 4 + (F_TE / 32) * 32 * 64, wave * 4, lds, G_H, lane, ct);
+            acc_to_lds(ct, lds, G_PART + 8 * wave, 0, lane);
         }
-        Mask16 mk0, mk1;  // relu' of H_{L-1}, in flight during the GEMM
-        f32x16 c0 = zero16(), c1 = zero16();
-        gemm_2m<32, 0>(pk + a.tL[L] / 4 + (tile0 + wave) * 32 * 64, 0, lds, G_H, lane, c0, c1, NoSide(),
-                       MaskPre{&mk0, &mk1, a.saved + (size_t)s_h(L - 1) * a.Ns, a.Ns, p0, lane, wave * 32},
-                       Stash2{k0, k1, dz_lane + (size_t)(Z_L0 + L * 256) * a.Ns, ns32});
-        mask_apply(c0, mk0);
-        mask_apply(c1, mk1);
+        Mask16 mk;  // relu' of H_{L-1}, in flight during the GEMM
+        f32x16 c = zero16();
+        gemm<32>(pk + a.tL[L] / 4 + (tile0 + wave) * 32 * 64, 0, lds, G_H, lane, c,
+                 MaskPre{&mk, a.saved + (size_t)s_h(L - 1) * a.Ns, a.Ns, p0, lane, wave * 32},
+                 Stash1{kt, tile_addr(a.dz, a.Ns, Z_L0 + L * 256, wave * 32, p0, lane)});
+        mask_apply(c, mk);
         lds_barrier();
         if (L == 5 && F.blender) sum_parts(lds, G_TE, nullptr, tid, true);
-        acc_to_lds(c0, lds, G_H, wave * 32, 0, lane, nullptr, false);
-        acc_to_lds(c1, lds, G_H, wave * 32, 1, lane, nullptr, false);
+        acc_to_lds(c, lds, G_H, wave * 32, lane);
         lds_barrier();
-        k0 = c0;
-        k1 = c1;
+        kt = c;
     }
-    const Stash2 dz0{k0, k1, dz_lane + (size_t)Z_L0 * a.Ns, ns32};
+    const Stash1 dz0{kt, tile_addr(a.dz, a.Ns, Z_L0, wave * 32, p0, lane)};
     if (!F.blender) {
         dz0.store_all();
         return;  // raw t PE has no parameters upstream of it
     }
-    // layer 0: t_emb slice of W_0^T dZ_0 (narrow); dZ_0 is stored under it
+    // layer 0: t_emb slice of W_0^T dZ_0 (K split over the waves); dZ_0 is stored under it
     {
-        const int mt = wave & 1, q = wave >> 1;
         f32x16 ct = zero16();
-        gemm_1m<8, 0>(pk + a.tL[0] / 4 + (F_TE / 32) * 32 * 64, q * 8, lds, G_H, mt, lane, ct, NoSide(), NoPre(), dz0);
-        acc_to_lds(ct, lds, G_PART + 8 * q, 0, mt, lane, nullptr, false);
+        gemm<4>(pk + a.tL[0] / 4 + (F_TE / 32) * 32 * 64, wave * 4, lds, G_H, lane, ct, NoPre(), dz0);
+        acc_to_lds(ct, lds, G_PART + 8 * wave, 0, lane);
         lds_barrier();
         sum_parts(lds, G_TE, nullptr, tid, true);
         lds_barrier();
@@ -937,10 +750,12 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
     lds_to_global(lds, G_TE, 8, a.dz, Z_TE, a.Ns, p0, tid);
     // timenet.2^T: dTH = W_T2^T dTE (K = 32) -> mask TH -> dZ_T1
     {
-        f32x16 c0 = zero16(), c1 = zero16();
-        gemm_2m<4, 0>(pk + a.tT2 / 4 + wave * 4 * 64, 0, lds, G_TE, lane, c0, c1, NoSide());
-        mask_store(c0, a.saved + (size_t)S_TH * a.Ns, a.dz + (size_t)Z_T1 * a.Ns, a.Ns, p0, 0, lane, wave * 32);
-        mask_store(c1, a.saved + (size_t)S_TH * a.Ns, a.dz + (size_t)Z_T1 * a.Ns, a.Ns, p0, 1, lane, wave * 32);
+        Mask16 mk;
+        f32x16 c = zero16();
+        gemm<4>(pk + a.tT2 / 4 + wave * 4 * 64, 0, lds, G_TE, lane, c,
+                MaskPre{&mk, a.saved + (size_t)S_TH * a.Ns, a.Ns, p0, lane, wave * 32});
+        mask_apply(c, mk);
+        Stash1{c, tile_addr(a.dz, a.Ns, Z_T1, wave * 32, p0, lane)}.store_all();
     }
 }
 

@@ -32,7 +32,7 @@ int main(int argc, char **argv) {
     hipMemcpy(pk, h.data(), npk * 4, hipMemcpyHostToDevice);
     hipMemcpy(x, hx.data(), hx.size() * 4, hipMemcpyHostToDevice);
     hipMemcpy(t, ht.data(), ht.size() * 4, hipMemcpyHostToDevice);
-    const int blocks = (N + 63) / 64;
+    const int blocks = (N + 31) / 32;  // BM = 32
     unsigned long long *prof;
     hipMalloc(&prof, (size_t)blocks * 256 * 8);
     hipMemset(prof, 0, (size_t)blocks * 256 * 8);
