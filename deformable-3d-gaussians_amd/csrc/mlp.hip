@@ -23,6 +23,7 @@
 //    split-N MFMA GEMM + fixed-order slab reduction (deterministic).
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <map>
 #include <mutex>
 #include <vector>
@@ -917,8 +918,16 @@ __device__ __forceinline__ void dw_tile(const WJob &J, size_t Ns, const float *_
                 }
             }
         }
+#ifdef DGS_MLP_PROFILE
+        if ((c - c0) >= 4 && (c - c0) < 8 && (tid & 63) == 0)
+            dgs_mlp_prof[blockIdx.x * 256 + 64 + ((c - c0) - 4) * 16 + wave] = __builtin_amdgcn_s_memtime();
+#endif
         if (more) DW_LSTORE(buf ^ 1);
         __syncthreads();
+#ifdef DGS_MLP_PROFILE
+        if ((c - c0) >= 3 && (c - c0) < 8 && tid == 0)
+            dgs_mlp_prof[blockIdx.x * 256 + 160 + ((c - c0) - 3)] = __builtin_amdgcn_s_memtime();
+#endif
     }
 #undef DW_GLOAD
 #undef DW_LSTORE
@@ -972,12 +981,23 @@ __global__ __launch_bounds__(DW_THREADS) void k_dw(WJobs JT, size_t Ns, const fl
 #pragma unroll
     for (int q = 1; q < MAXJ; q++)
         if (q < JT.n && (int)blockIdx.x >= JT.j[q].block0) J = JT.j[q];
+#ifdef DGS_MLP_PROFILE
+    if (threadIdx.x == 0) dgs_mlp_prof[blockIdx.x * 256 + 200] = __builtin_amdgcn_s_memtime();
+#endif
     // the two wave layouts are separate code regions (a runtime switch inside one loop makes the
     // register allocator spill the accumulators)
     if (J.narrow)
         dw_tile<true>(J, Ns, dz, saved, slabs, reinterpret_cast<float *>(dw_lds));
     else
         dw_tile<false>(J, Ns, dz, saved, slabs, reinterpret_cast<float *>(dw_lds));
+#ifdef DGS_MLP_PROFILE
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        dgs_mlp_prof[blockIdx.x * 256 + 201] = __builtin_amdgcn_s_memtime();
+        dgs_mlp_prof[blockIdx.x * 256 + 202] = (unsigned long long)(J.zrow * 10000 + J.xrow);
+        dgs_mlp_prof[blockIdx.x * 256 + 203] = (unsigned long long)J.nsplit;
+    }
+#endif
 }
 
 struct RJob {
@@ -1051,8 +1071,9 @@ inline WPlan make_wplan(const Flags &F) {
         raw[nr++] = Raw{Z_TE, 32, S_TH, 256, 10, 0};
     }
     for (int l = 0; l < 11; l++) W.layer_job[l][0] = W.layer_job[l][1] = -1;
-    // per-chunk cost = the busiest SIMD's MFMA tiles (waves w and w + 4 share SIMD w % 4), floored
-    // at the load latency a chunk cannot hide (~5 tiles of MFMA time)
+    // per-chunk cost = the busiest SIMD's MFMA tiles (waves w and w + 4 share SIMD w % 4) plus the
+    // per-chunk staging/barrier cost, floored; calibrated with tools/dw_phase.cpp (full 256 x 256
+    // tile 16 + 1.5 units ~ 18.9k cycles, narrow 6 + 1.5 ~ 8.3k, 32-row jobs ~ 4.2k)
     double cost[MAXJ], total = 0;
     for (int q = 0; q < nr; q++) {
         const bool nar = raw[q].krows <= 128;
@@ -1069,13 +1090,25 @@ inline WPlan make_wplan(const Flags &F) {
             simd[w & 3] += tr * tc;
         }
         int crit = max(max(simd[0], simd[1]), max(simd[2], simd[3]));
-        cost[q] = (double)max(crit, 5);
+        cost[q] = fmax(crit + 1.5, 4.0);
         total += cost[q];
+    }
+    // splits: the smallest per-workgroup time T (in unit-chunks) whose ceil(cost * nch / T) fit the
+    // target grid (whole jobs never straddle: each workgroup runs per = ceil(nch / ns) chunks)
+    const int nch = 1 << 20;  // relative scale only (the chunk count cancels)
+    double T = total * nch / DW_TARGET_BLOCKS;
+    int nsq[MAXJ];
+    for (int it = 0; it < 400; it++, T *= 1.005) {
+        int sum = 0;
+        for (int q = 0; q < nr; q++) {
+            nsq[q] = max(1, (int)ceil(cost[q] * nch / T - 1e-9));
+            sum += nsq[q];
+        }
+        if (sum <= DW_TARGET_BLOCKS) break;
     }
     int b = 0;
     for (int q = 0; q < nr; q++) {
-        int ns = (int)(DW_TARGET_BLOCKS * cost[q] / total + 0.5);
-        if (ns < 1) ns = 1;
+        const int ns = nsq[q];
         W.jobs.j[q] = WJob{raw[q].zrow, raw[q].nrows, raw[q].xrow, raw[q].krows, ns, b, raw[q].krows <= 128 ? 1 : 0};
         W.layer_job[raw[q].layer][raw[q].kt] = q;
         b += ns;
