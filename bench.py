@@ -165,7 +165,17 @@ def main():
     pipe = PipelineParams()
     bg = torch.zeros(3, device=dev)
     cams = [synth_camera(R, R, index=rank * 97 + k, fid=((rank * 97 + k) % 30) / 30.0, device=dev) for k in range(8)]
-    gt = torch.rand((3, R, R), device=dev, generator=torch.Generator(device=dev).manual_seed(100 + rank))
+    # targets: each camera's initial render plus noise (sigma 0.02), i.e. a model near convergence as
+    # in steady-state training; a random target would drag the Gaussians (and the pair count) along
+    # during the run and make the workload depend on --steps
+    from deformgs.renderer import render
+    gts = []
+    gen = torch.Generator(device=dev).manual_seed(100 + rank)
+    with torch.no_grad():
+        for cam in cams:
+            d = deform.step(gaussians.get_xyz.detach(), cam.fid.unsqueeze(0).expand(N, -1))
+            img = render(cam, gaussians, pipe, bg, d[0], d[1], d[2])["render"]
+            gts.append((img + 0.02 * torch.randn(img.shape, device=dev, generator=gen)).clamp_(0.0, 1.0))
     allreduce = GradAllReduce(lambda: list(deform.deform.parameters()) + [
         gaussians._xyz, gaussians._features_dc, gaussians._features_rest, gaussians._scaling, gaussians._rotation,
         gaussians._opacity])
@@ -174,7 +184,7 @@ def main():
 
     def step(k):
         cam = cams[k % len(cams)]
-        loss, pkg = forward_backward(gaussians, deform, cam, gt, pipe, bg)
+        loss, pkg = forward_backward(gaussians, deform, cam, gts[k % len(cams)], pipe, bg)
         allreduce()
         if not args.no_adam:
             optimizer_step(gaussians, deform, state["it"])
@@ -202,7 +212,6 @@ def main():
     elapsed = float(el.item())
 
     # pair count of one render (for the raster rooflines), measured once outside the timed region
-    from deformgs.renderer import render
     with torch.no_grad():
         d = deform.step(gaussians.get_xyz.detach(), cams[0].fid.unsqueeze(0).expand(N, -1))
     import diff_gaussian_rasterization as dgr
@@ -254,7 +263,7 @@ def main():
         "metric": "train iters/s (deform+raster fwd+bwd), 100k Gaussians @ 800x800",
         "value": value, "unit": "iters/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "fp32", "data": "synthetic (synth-100k, random-init weights)",
+        "vs_baseline": None, "dtype": "fp32", "data": "synthetic (synth-100k, random-init weights, targets = initial renders + noise)",
         "config": {"workload": f"synth-100k: {N} Gaussians, {R}x{R}, blender DeformNetworkBaseline, SH3"
                    + (" (raw-init heads)" if args.raw_init else " (heads at 1/100 init: steady-state deltas)"),
                    "global_batch": world, "includes_adam": not args.no_adam, "pairs_per_render": P_pairs,
