@@ -67,7 +67,9 @@ def kernel_algorithmic(name, N, P, HW):
     if name == "blend_bwd":
         return 44.0 * P + 24.0 * HW + 48.0 * N, "byte", "hbm"
     if name == "sort":
-        return 24.0 * P, "byte", "hbm"
+        return 24.0 * P, "byte", "hbm"       # 2 passes x (read + write) x (2-B key + 4-B id)
+    if name == "depth_sort":
+        return 64.0 * N, "byte", "hbm"       # 4 passes x (read + write) x (4-B key + 4-B id)
     if name == "duplicate":
         return 20.0 * N + 12.0 * P, "byte", "hbm"
     if name == "ranges":
@@ -79,7 +81,8 @@ def kernel_algorithmic(name, N, P, HW):
     return None
 
 
-KERNEL_CLASSES = ["mlp_fwd", "mlp_bwd", "mlp_dw", "mlp_dw_reduce", "preprocess_fwd", "duplicate", "sort", "ranges",
+KERNEL_CLASSES = ["mlp_fwd", "mlp_bwd", "mlp_dw", "mlp_dw_reduce", "preprocess_fwd", "depth_sort", "duplicate", "sort",
+                  "ranges",
                   "blend_fwd", "blend_bwd", "preprocess_bwd", "ssim_fwd", "ssim_bwd"]
 
 

@@ -5,20 +5,25 @@
 // contract of gaussian_renderer/__init__.py:53-124.
 //
 // Pipeline (one HIP stream, all buffers in HBM, SoA per-Gaussian geometry):
-//   k_preprocess   1 thread / Gaussian: cull, Sigma3D, EWA Sigma2D, conic, radius, tile rect, SH->RGB
-//   scan           hipcub inclusive sum of tiles_touched -> pair offsets (P_pairs read back to host)
-//   k_duplicate    emit (tile<<32 | depth_bits, id) pairs, Gaussian-index order
-//   radix sort     hipcub onesweep over bits [0, 32+bits(tiles)) (stable: ties stay in index order)
-//   k_ranges       [start,end) per tile
+//   k_preprocess   1 thread / Gaussian: cull, Sigma3D, EWA Sigma2D, conic, radius, tile rect, SH->RGB,
+//                  depth key (float bits; culled -> all-ones)
+//   depth sort     hipcub radix sort of the N Gaussians by depth (stable: ties in index order)
+//   scan           inclusive sum of tiles_touched in depth order -> pair offsets; the pair count
+//                  is copied to pinned host memory behind an event (speculative binning, below)
+//   k_duplicate    emit (tile, id) pairs in depth order into the speculative capacity
+//   radix sort     stable, on the tile bits only (16-bit keys): same final order as upstream's
+//                  sort of (tile << 32 | depth_bits) keys over Gaussian-index-ordered pairs
+//   k_ranges       [start,end) per tile (pair count read on the device)
 //   k_blend_fwd    1 workgroup (4 waves) / 16x16 tile, LDS-staged 256-Gaussian batches, block-wide
 //                  early exit; writes colour, depth, final T, last contributor
-//   k_blend_bwd    back-to-front replay from the block's max contributor; per-Gaussian gradients
-//                  summed across the wave with DPP (row_shr / row_bcast) and added with ONE atomic
-//                  wave-instruction of 12 contiguous floats per (wave, Gaussian)
+//   k_blend_bwd    back-to-front replay from the block's max contributor; the 12 per-Gaussian
+//                  gradient sums reduce-scattered across the wave (permlane32/16 swaps + DPP) and
+//                  added with 3 four-lane atomics per (wave, Gaussian)
 //   k_preprocess_bwd 1 thread / Gaussian: conic->Sigma2D->(Sigma3D, mean), projection, SH, Sigma3D->(s,q)
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -37,13 +42,16 @@ __global__ __launch_bounds__(256) void k_preprocess(
     const float *__restrict__ shs, const float *__restrict__ colors_pre, const float *view,
     const float *proj, const float *campos, int W, int H, float tanx, float tany, float fx, float fy,
     int gx, int gy, int *__restrict__ radii, float2 *__restrict__ xy, float4 *__restrict__ conic_o,
-    float4 *__restrict__ rgbd, uint32_t *__restrict__ tiles, uint8_t *__restrict__ clamped) {
+    float4 *__restrict__ rgbd, uint32_t *__restrict__ tiles, uint8_t *__restrict__ clamped,
+    uint32_t *__restrict__ dkey, uint32_t *__restrict__ gid) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P) return;
     Cam cam;
     load_cam(cam, view, proj, campos);
     radii[i] = 0;
     tiles[i] = 0;
+    dkey[i] = 0xffffffffu;  // culled: sorts last, emits no pairs
+    gid[i] = (uint32_t)i;
     float3 p = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
     float3 pv = xform43(cam.v, p);
     if (pv.z <= 0.2f) return;
@@ -116,44 +124,55 @@ __global__ __launch_bounds__(256) void k_preprocess(
     rgbd[i] = make_float4(rgb.x, rgb.y, rgb.z, pv.z);
     tiles[i] = (uint32_t)area;
     clamped[i] = cl;
+    dkey[i] = __float_as_uint(pv.z);  // depth > 0.2: float bits order as the values
 }
 
-__global__ __launch_bounds__(256) void k_duplicate(int P, const float2 *__restrict__ xy,
-                                                   const int *__restrict__ radii,
-                                                   const float4 *__restrict__ rgbd,
+// Pairs are emitted in depth order (Gaussians pre-sorted by depth, stable on the index), so a
+// stable sort on the tile id alone yields the reference's (tile, depth) key order, ties on the
+// Gaussian index included: 2 radix passes over 16-bit keys instead of 6 over 64-bit ones.
+__global__ __launch_bounds__(256) void k_gather_tiles(int P, const uint32_t *__restrict__ order,
+                                                      const uint32_t *__restrict__ tiles,
+                                                      uint32_t *__restrict__ tiles_sorted) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < P) tiles_sorted[j] = tiles[order[j]];
+}
+
+template <class KT>
+__global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t *__restrict__ order,
+                                                   const float2 *__restrict__ xy, const int *__restrict__ radii,
                                                    const uint32_t *__restrict__ offsets, int gx, int gy,
-                                                   uint64_t *__restrict__ keys,
-                                                   uint32_t *__restrict__ vals, uint32_t cap) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P) return;
-    int r = radii[i];
+                                                   KT *__restrict__ keys, uint32_t *__restrict__ vals, uint32_t cap) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= P) return;
+    const uint32_t g = order[j];
+    const int r = radii[g];
     if (r <= 0) return;
-    uint32_t off = (i == 0) ? 0u : offsets[i - 1];
-    float2 c = xy[i];
+    uint32_t off = (j == 0) ? 0u : offsets[j - 1];
+    const float2 c = xy[g];
     int x0, y0, x1, y1;
     tile_rect(c.x, c.y, r, gx, gy, x0, y0, x1, y1);
-    uint64_t db = (uint64_t)__float_as_uint(rgbd[i].w);
     for (int y = y0; y < y1; y++)
         for (int x = x0; x < x1; x++) {
             if (off < cap) {  // speculative capacity: an overflowing launch is redone by the host
-                keys[off] = ((uint64_t)(y * gx + x) << 32) | db;
-                vals[off] = (uint32_t)i;
+                keys[off] = (KT)(y * gx + x);
+                vals[off] = g;
             }
             off++;
         }
 }
 
 // L (the pair count) is read on the device: the grid covers the speculative capacity
-__global__ __launch_bounds__(256) void k_ranges(const uint32_t *__restrict__ count, const uint64_t *__restrict__ keys,
+template <class KT>
+__global__ __launch_bounds__(256) void k_ranges(const uint32_t *__restrict__ count, const KT *__restrict__ keys,
                                                 uint2 *__restrict__ ranges) {
     int idx = blockIdx.x * blockDim.x + threadIdx.x;
     const int L = (int)*count;
     if (idx >= L) return;
-    uint32_t t = (uint32_t)(keys[idx] >> 32);
+    uint32_t t = (uint32_t)keys[idx];
     if (idx == 0) {
         ranges[t].x = 0;
     } else {
-        uint32_t prev = (uint32_t)(keys[idx - 1] >> 32);
+        uint32_t prev = (uint32_t)keys[idx - 1];
         if (t != prev) {
             ranges[prev].y = idx;
             ranges[t].x = idx;
@@ -644,9 +663,9 @@ struct dgs_raster_ctx {
     // carved views
     float2 *xy = nullptr;
     float4 *conic_o = nullptr, *rgbd = nullptr;
-    uint32_t *tiles = nullptr, *offsets = nullptr;
+    uint32_t *tiles = nullptr, *offsets = nullptr;  // offsets: inclusive scan in depth order
+    uint32_t *dkey = nullptr, *dkey_alt = nullptr, *gid = nullptr, *order = nullptr, *tiles_sorted = nullptr;
     uint8_t *clamped = nullptr;
-    uint64_t *keys = nullptr;
     uint32_t *vals = nullptr;
     uint2 *ranges = nullptr;
     float *final_T = nullptr;
@@ -721,13 +740,15 @@ hipError_t scan_tmp_bytes(int device, int P, hipStream_t stream, size_t &bytes) 
     return e;
 }
 
+// radix-sort temp bytes for (KT keys, u32 values), cached per (key type, device, size class, bits)
+template <class KT>
 hipError_t sort_tmp_bytes(int device, int n, int end_bit, hipStream_t stream, size_t &bytes) {
     const int cls = size_class(n);
     std::lock_guard<std::mutex> lk(g_tmp_mu);
-    auto key = std::make_tuple(1, device, cls, end_bit);
+    auto key = std::make_tuple((int)sizeof(KT), device, cls, end_bit);
     auto it = g_tmp_sizes.find(key);
     if (it != g_tmp_sizes.end()) { bytes = it->second; return hipSuccess; }
-    hipcub::DoubleBuffer<uint64_t> kb(nullptr, nullptr);
+    hipcub::DoubleBuffer<KT> kb(nullptr, nullptr);
     hipcub::DoubleBuffer<uint32_t> vb(nullptr, nullptr);
     hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, kb, vb, class_upper(cls), 0, end_bit, stream);
     if (e == hipSuccess) g_tmp_sizes[key] = bytes;
@@ -767,47 +788,55 @@ dgs_raster_ctx *ctx_acquire(int device, hipStream_t stream) {
 }
 }  // namespace
 
-// Binning for `cap` pairs (>= num_rendered, or the speculative capacity) + the blend: key buffer
-// pre-filled with all-ones (past every tile id in the sorted bits, so the unused tail sorts last and
-// leaves the stable order of the real pairs untouched), bounded duplicate, radix sort of cap items,
-// ranges from the device-side count, forward blend.
+// Binning for `cap` pairs (>= num_rendered, or the speculative capacity) + the blend: the key
+// buffer is pre-filled with all-ones (past every tile id, so the unused tail sorts last and leaves
+// the stable order of the real pairs untouched), bounded duplicate in depth order, stable radix sort
+// of cap items on the tile bits, ranges from the device-side count, forward blend.
+template <class KT>
+static int bin_tiles(dgs_raster_ctx *c, int cap, int P, int device, hipStream_t stream, bool dbg) {
+    const int T = c->gx * c->gy;
+    const int end_bit = bits_for((uint32_t)T);
+    size_t sort_tmp = 0;
+    DGS_HIP_CHECK(sort_tmp_bytes<KT>(device, cap, end_bit, stream, sort_tmp));
+    size_t o_k0 = 0, o_k1 = align_up(sizeof(KT) * cap), o_v0 = align_up(o_k1 + sizeof(KT) * cap),
+           o_v1 = align_up(o_v0 + 4ull * cap), o_t = align_up(o_v1 + 4ull * cap);
+    if (int rc = c->bin.ensure(o_t + sort_tmp + 256)) return rc;
+    char *b = (char *)c->bin.p;
+    KT *k0 = (KT *)(b + o_k0), *k1 = (KT *)(b + o_k1);
+    uint32_t *v0 = (uint32_t *)(b + o_v0), *v1 = (uint32_t *)(b + o_v1);
+    {
+        ScopedTimer tm("duplicate", stream);
+        DGS_HIP_CHECK(hipMemsetAsync(k0, 0xff, sizeof(KT) * cap, stream));
+        hipLaunchKernelGGL(k_duplicate<KT>, dim3(div_up(P, 256)), dim3(256), 0, stream, P, c->order, c->xy, c->radii,
+                           c->offsets, c->gx, c->gy, k0, v0, (uint32_t)cap);
+    }
+    DGS_LAUNCH_CHECK("k_duplicate", dbg, stream);
+    hipcub::DoubleBuffer<KT> kbuf(k0, k1);
+    hipcub::DoubleBuffer<uint32_t> vbuf(v0, v1);
+    {
+        ScopedTimer tm("sort", stream);
+        DGS_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(b + o_t, sort_tmp, kbuf, vbuf, cap, 0, end_bit, stream));
+    }
+    c->vals = vbuf.Current();
+    {
+        ScopedTimer tm("ranges", stream);
+        hipLaunchKernelGGL(k_ranges<KT>, dim3(div_up(cap, 256)), dim3(256), 0, stream, c->offsets + (P - 1),
+                           kbuf.Current(), c->ranges);
+    }
+    DGS_LAUNCH_CHECK("k_ranges", dbg, stream);
+    return DGS_OK;
+}
+
 static int bin_and_blend(dgs_raster_ctx *c, int cap, int P, int device, hipStream_t stream, bool dbg, float *out_color,
                          float *out_depth) {
     const int T = c->gx * c->gy;
     DGS_HIP_CHECK(hipMemsetAsync(c->ranges, 0, 8ull * T, stream));
     if (cap > 0) {
-        const int end_bit = 32 + bits_for((uint32_t)T);
-        size_t sort_tmp = 0;
-        DGS_HIP_CHECK(sort_tmp_bytes(device, cap, end_bit, stream, sort_tmp));
-        size_t o_k0 = 0, o_k1 = align_up(8ull * cap), o_v0 = align_up(o_k1 + 8ull * cap),
-               o_v1 = align_up(o_v0 + 4ull * cap), o_t = align_up(o_v1 + 4ull * cap);
-        if (int rc = c->bin.ensure(o_t + sort_tmp + 256)) return rc;
-        char *b = (char *)c->bin.p;
-        uint64_t *k0 = (uint64_t *)(b + o_k0), *k1 = (uint64_t *)(b + o_k1);
-        uint32_t *v0 = (uint32_t *)(b + o_v0), *v1 = (uint32_t *)(b + o_v1);
-        {
-            ScopedTimer tm("duplicate", stream);
-            DGS_HIP_CHECK(hipMemsetAsync(k0, 0xff, 8ull * cap, stream));
-            hipLaunchKernelGGL(k_duplicate, dim3(div_up(P, 256)), dim3(256), 0, stream, P, c->xy, c->radii, c->rgbd,
-                               c->offsets, c->gx, c->gy, k0, v0, (uint32_t)cap);
-        }
-        DGS_LAUNCH_CHECK("k_duplicate", dbg, stream);
-        hipcub::DoubleBuffer<uint64_t> kbuf(k0, k1);
-        hipcub::DoubleBuffer<uint32_t> vbuf(v0, v1);
-        {
-            ScopedTimer tm("sort", stream);
-            DGS_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(b + o_t, sort_tmp, kbuf, vbuf, cap, 0, end_bit, stream));
-        }
-        c->keys = kbuf.Current();
-        c->vals = vbuf.Current();
-        {
-            ScopedTimer tm("ranges", stream);
-            hipLaunchKernelGGL(k_ranges, dim3(div_up(cap, 256)), dim3(256), 0, stream, c->offsets + (P - 1), c->keys,
-                               c->ranges);
-        }
-        DGS_LAUNCH_CHECK("k_ranges", dbg, stream);
+        // 16-bit tile keys up to 65535 tiles (4080 x 4080 pixels), 32-bit beyond
+        const int rc = T < 65535 ? bin_tiles<uint16_t>(c, cap, P, device, stream, dbg)
+                                 : bin_tiles<uint32_t>(c, cap, P, device, stream, dbg);
+        if (rc) return rc;
     } else {
-        c->keys = nullptr;
         c->vals = nullptr;
     }
     {
@@ -866,10 +895,15 @@ extern "C" int dgs_raster_forward(const dgs_raster_settings *s, int P, int M, co
     // geometry
     size_t off_xy = 0, off_co = align_up(off_xy + 8ull * P), off_cd = align_up(off_co + 16ull * P),
            off_t = align_up(off_cd + 16ull * P), off_o = align_up(off_t + 4ull * P), off_cl = align_up(off_o + 4ull * P);
-    size_t scan_tmp = 0;
-    if (P > 0) DGS_HIP_CHECK(scan_tmp_bytes(device, P, stream, scan_tmp));
-    size_t off_st = align_up(off_cl + P);
-    if (int rc = c->geom.ensure(off_st + scan_tmp + 256)) { ctx_out[0] = nullptr; delete c; return rc; }
+    size_t off_dk = align_up(off_cl + P), off_dk2 = align_up(off_dk + 4ull * P), off_gid = align_up(off_dk2 + 4ull * P),
+           off_ord = align_up(off_gid + 4ull * P), off_ts = align_up(off_ord + 4ull * P);
+    size_t scan_tmp = 0, dsort_tmp = 0;
+    if (P > 0) {
+        DGS_HIP_CHECK(scan_tmp_bytes(device, P, stream, scan_tmp));
+        DGS_HIP_CHECK(sort_tmp_bytes<uint32_t>(device, P, 32, stream, dsort_tmp));
+    }
+    size_t off_st = align_up(off_ts + 4ull * P);
+    if (int rc = c->geom.ensure(off_st + std::max(scan_tmp, dsort_tmp) + 256)) { ctx_out[0] = nullptr; delete c; return rc; }
     char *g = (char *)c->geom.p;
     c->xy = (float2 *)(g + off_xy);
     c->conic_o = (float4 *)(g + off_co);
@@ -877,6 +911,11 @@ extern "C" int dgs_raster_forward(const dgs_raster_settings *s, int P, int M, co
     c->tiles = (uint32_t *)(g + off_t);
     c->offsets = (uint32_t *)(g + off_o);
     c->clamped = (uint8_t *)(g + off_cl);
+    c->dkey = (uint32_t *)(g + off_dk);
+    c->dkey_alt = (uint32_t *)(g + off_dk2);
+    c->gid = (uint32_t *)(g + off_gid);
+    c->order = (uint32_t *)(g + off_ord);
+    c->tiles_sorted = (uint32_t *)(g + off_ts);
     // image state
     size_t off_r = 0, off_T = align_up(off_r + 8ull * T), off_n = align_up(off_T + 4ull * HW);
     if (int rc = c->img.ensure(off_n + 4ull * HW)) { delete c; return rc; }
@@ -893,10 +932,20 @@ extern "C" int dgs_raster_forward(const dgs_raster_settings *s, int P, int M, co
             hipLaunchKernelGGL(k_preprocess, dim3(div_up(P, 256)), dim3(256), 0, stream, P, s->sh_degree, M, means3D, scales,
                                s->scale_modifier, rotations, cov3D_precomp, opacities, shs, colors_precomp, s->viewmatrix,
                                s->projmatrix, s->campos, c->W, c->H, s->tanfovx, s->tanfovy, fx, fy, c->gx, c->gy, out_radii,
-                               c->xy, c->conic_o, c->rgbd, c->tiles, c->clamped);
+                               c->xy, c->conic_o, c->rgbd, c->tiles, c->clamped, c->dkey, c->gid);
         }
         DGS_LAUNCH_CHECK("k_preprocess", dbg, stream);
-        DGS_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(g + off_st, scan_tmp, c->tiles, c->offsets, P, stream));
+        {
+            // Gaussians by depth (stable on the index), then the pair offsets in that order
+            ScopedTimer tm("depth_sort", stream);
+            hipcub::DoubleBuffer<uint32_t> kb(c->dkey, c->dkey_alt), vb(c->gid, c->order);
+            DGS_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(g + off_st, dsort_tmp, kb, vb, P, 0, 32, stream));
+            c->order = vb.Current();  // either buffer, per the pass count
+            hipLaunchKernelGGL(k_gather_tiles, dim3(div_up(P, 256)), dim3(256), 0, stream, P, c->order, c->tiles,
+                               c->tiles_sorted);
+        }
+        DGS_LAUNCH_CHECK("k_gather_tiles", dbg, stream);
+        DGS_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(g + off_st, scan_tmp, c->tiles_sorted, c->offsets, P, stream));
         if (!c->h_total) DGS_HIP_CHECK(hipHostMalloc((void **)&c->h_total, sizeof(uint32_t), hipHostMallocDefault));
         if (!c->count_ev) DGS_HIP_CHECK(hipEventCreateWithFlags(&c->count_ev, hipEventDisableTiming));
         DGS_HIP_CHECK(hipMemcpyAsync(c->h_total, c->offsets + (P - 1), 4, hipMemcpyDeviceToHost, stream));
