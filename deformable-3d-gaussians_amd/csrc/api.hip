@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <map>
+#include <set>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -13,6 +14,7 @@ namespace {
 thread_local std::string g_err;
 std::mutex g_tmu;
 bool g_timing = false;
+std::set<std::string> g_timing_sel;  // empty = every class
 struct Pending {
     std::string name;
     hipEvent_t a, b;
@@ -52,6 +54,7 @@ void set_error(const std::string &msg) { g_err = msg; }
 ScopedTimer::ScopedTimer(const char *n, hipStream_t s) : name(n), stream(s), ev0(nullptr) {
     if (!g_timing) return;
     std::lock_guard<std::mutex> lk(g_tmu);
+    if (!g_timing_sel.empty() && !g_timing_sel.count(n)) return;
     hipEvent_t e = take_event();
     (void)hipEventRecord(e, stream);
     ev0 = (void *)e;
@@ -74,6 +77,22 @@ extern "C" const char *dgs_version(void) { return "libdgs_hip 0.1 (gfx950)"; }
 extern "C" void dgs_timing_enable(int on) {
     std::lock_guard<std::mutex> lk(dgs::g_tmu);
     dgs::g_timing = on != 0;
+}
+
+extern "C" void dgs_timing_select(const char *csv) {
+    std::lock_guard<std::mutex> lk(dgs::g_tmu);
+    dgs::g_timing_sel.clear();
+    if (!csv) return;
+    std::string cur;
+    for (const char *p = csv;; p++) {
+        if (*p == ',' || *p == 0) {
+            if (!cur.empty()) dgs::g_timing_sel.insert(cur);
+            cur.clear();
+            if (*p == 0) break;
+        } else {
+            cur += *p;
+        }
+    }
 }
 
 extern "C" double dgs_timing_query(const char *name, int *launches) {

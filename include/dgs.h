@@ -92,6 +92,8 @@ int dgs_mark_visible(int P, const float *means3D, const float *viewmatrix, const
 
 /* ---- timing hooks (bench.py): per-kernel-class HIP event accumulation on the launch stream ---- */
 void dgs_timing_enable(int on);
+/* Restrict timing to the comma-separated kernel classes in `csv` (host string; NULL or "" = all). */
+void dgs_timing_select(const char *csv);
 /* Returns accumulated ms for kernel class `name` and its launch count (host); syncs those events. */
 double dgs_timing_query(const char *name, int *launches);
 void dgs_timing_reset(void);
