@@ -537,42 +537,42 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) vo
         t1a1 = At1[64];
         t1b = load_bias(a.packed + a.bT1, wave * 32, lane);
     }
-    // ---- positional encodings (utils/time_utils.py:42-54) ----
-    for (int e = tid; e < 64 * BM; e += NTHR) {
-        int m = e % BM, f = e / BM;
-        int p = p0 + m;
-        float v = 0.f;
-        if (p < a.N && f < 63) {
-            int d = f % 3, band = f / 3;  // band 0: identity; then (sin, cos) per frequency
-            float x = a.xyz[3 * p + d];
-            if (band == 0) {
-                v = x;
+    // ---- positional encodings (utils/time_utils.py:42-54): feature 3 band + d, band 0 = x,
+    // band 1 + 2i = sin(2^i x), band 2 + 2i = cos(2^i x); one sincosf per (point, dim, frequency) ----
+    {
+        auto put = [&](int g0, int f, int m, float v) { lf[((g0 + f / 4) * BM + m) * 4 + (f & 3)] = v; };
+        for (int e = tid; e < BM * 3 * 11; e += NTHR) {
+            const int m = e % BM, r = e / BM, d = r % 3, i = r / 3;  // i = 10: identity band
+            const int p = p0 + m;
+            const float x = p < a.N ? a.xyz[3 * p + d] : 0.f;
+            if (i == 10) {
+                put(G_XE, d, m, p < a.N ? x : 0.f);
             } else {
-                int fi = (band - 1) >> 1;
-                float arg = x * (float)(1 << fi);
-                v = ((band - 1) & 1) ? cosf(arg) : sinf(arg);
+                float sv, cv;
+                sincosf(x * (float)(1 << i), &sv, &cv);
+                put(G_XE, 3 * (1 + 2 * i) + d, m, p < a.N ? sv : 0.f);
+                put(G_XE, 3 * (2 + 2 * i) + d, m, p < a.N ? cv : 0.f);
             }
         }
-        lf[((G_XE + f / 4) * BM + m) * 4 + (f & 3)] = v;
-    }
-    {
+        for (int m = tid; m < BM; m += NTHR) put(G_XE, 63, m, 0.f);  // padding feature
         const int tg = F.blender ? G_TIN : G_TE;
-        const int ng = F.blender ? 4 : 8;
-        for (int e = tid; e < ng * 4 * BM; e += NTHR) {
-            int m = e % BM, f = e / BM;
-            int p = p0 + m;
-            float v = 0.f;
-            if (p < a.N && f < F.tin) {
-                float x = a.t[p];
-                if (f == 0) {
-                    v = x;
-                } else {
-                    int fi = (f - 1) >> 1;
-                    float arg = x * (float)(1 << fi);
-                    v = ((f - 1) & 1) ? cosf(arg) : sinf(arg);
-                }
+        const int nfreq = (F.tin - 1) / 2, ng = F.blender ? 4 : 8;
+        for (int e = tid; e < BM * 4 * ng; e += NTHR) {  // zero the whole t image (padding)
+            const int m = e % BM, f = e / BM;
+            if (f >= F.tin) put(tg, f, m, 0.f);
+        }
+        for (int e = tid; e < BM * (nfreq + 1); e += NTHR) {
+            const int m = e % BM, i = e / BM;  // i = nfreq: identity
+            const int p = p0 + m;
+            const float x = p < a.N ? a.t[p] : 0.f;
+            if (i == nfreq) {
+                put(tg, 0, m, x);
+            } else {
+                float sv, cv;
+                sincosf(x * (float)(1 << i), &sv, &cv);
+                put(tg, 1 + 2 * i, m, p < a.N ? sv : 0.f);
+                put(tg, 2 + 2 * i, m, p < a.N ? cv : 0.f);
             }
-            lf[((tg + f / 4) * BM + m) * 4 + (f & 3)] = v;
         }
     }
     lds_barrier();
