@@ -350,7 +350,8 @@ __global__ __launch_bounds__(256) void k_blend_bwd(const uint2 *__restrict__ ran
             float v_r = 0.f, v_g = 0.f, v_b = 0.f, v_d = 0.f;
             if (act) {
                 float4 cd = s_cd[j];
-                T = T / (1.f - alpha);
+                const float inv1ma = 1.f / (1.f - alpha);  // one IEEE division for both uses
+                T = T * inv1ma;
                 float w = alpha * T;
                 acc0 = last_alpha * lc0 + (1.f - last_alpha) * acc0;
                 acc1 = last_alpha * lc1 + (1.f - last_alpha) * acc1;
@@ -364,7 +365,7 @@ __global__ __launch_bounds__(256) void k_blend_bwd(const uint2 *__restrict__ ran
                 v_d = w * ddep;
                 dLda *= T;
                 last_alpha = alpha;
-                dLda += (-Tfinal / (1.f - alpha)) * bgdot;
+                dLda += (-Tfinal * inv1ma) * bgdot;
                 float dLdG = co.w * dLda;
                 float gdx = G * dx, gdy = G * dy;
                 float dGdx = -gdx * co.x - gdy * co.y;
