@@ -46,6 +46,9 @@ constexpr int F_XE = 0, F_TE = 64, F_H = 96;
 // saved-activation row offsets ([rows][Ns], feature-major); order keeps each layer input contiguous
 constexpr int S_H0 = 0, S_XE = 1024, S_TE = 1088, S_H4 = 1120, S_TIN = 2144, S_TH = 2160;
 __host__ __device__ constexpr int s_h(int i) { return i < 4 ? S_H0 + 256 * i : S_H4 + 256 * (i - 4); }
+// relu' bit-mask rows: H0..H7 then TH (blender)
+__host__ __device__ constexpr int m_h(int i) { return 256 * i; }
+constexpr int M_TH = 2048;
 // dZ scratch rows
 constexpr int Z_L0 = 0, Z_G = 2048, Z_TE = 2080, Z_T1 = 2112;
 
@@ -54,6 +57,7 @@ struct Flags {
     int nout;     // head outputs: 10 or 13
     int tin;      // raw t PE channels: 13 (L=6) or 21 (L=10)
     int nsaved;   // saved rows
+    int nmask;    // relu' bit-mask rows (one u32 word = 32 points per row and block)
     int nz;       // dZ rows
 };
 
@@ -65,6 +69,7 @@ __host__ __device__ inline Flags make_flags(int f) {
     F.nout = F.sixdof ? 13 : 10;
     F.tin = F.blender ? 13 : 21;
     F.nsaved = F.blender ? 2416 : 2144;
+    F.nmask = F.blender ? 2304 : 2048;
     F.nz = F.blender ? 2368 : 2080;
     return F;
 }
@@ -511,9 +516,21 @@ struct FwdArgs {
     const float *packed;
     float *out;
     float *saved;
+    uint32_t *mask;  // relu' bits, [block][nmask] words (after the saved rows)
     int fT1, fT2, fL[8], fHd, bT1, bT2, bL[8], bHd;
     int flags;
 };
+
+// relu' of this wave's 32x32 output tile as bits, kept in the accumulator's own lane layout:
+// lane (m, h) packs bit r = [value of row 8(r>>2)+4h+(r&3), point m > 0] into a u16. The backward's
+// GEMM over the same 32-row tile has the identical lane layout, so no transpose is needed either way.
+// Signed clamp of the float bits: -0.0 and +0.0 give 0, positive values 1.
+__device__ inline void store_mask_bits(const f32x16 &c, __amdgpu_buffer_rsrc_t mrsrc, int srow, int lane) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int r = 0; r < 16; r++) w |= (uint32_t)min(max(__float_as_int(c[r]), 0), 1) << r;
+    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)w, mrsrc, lane * 2, srow * 4, 0);
+}
 
 // Workgroup = 32 points x 8 waves (wave w owns output rows 32w..32w+31 of every 256-wide layer);
 // 80 KB of LDS, so two workgroups share a CU (4 waves per SIMD): one block's barrier waits and
@@ -527,6 +544,8 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) vo
     const Flags F = make_flags(a.flags);
     const float4 *pk = reinterpret_cast<const float4 *>(a.packed);
     float *lf = reinterpret_cast<float *>(lds);
+    const __amdgpu_buffer_rsrc_t mrsrc =
+        __builtin_amdgcn_make_buffer_rsrc(a.mask + (SAVE ? (size_t)blockIdx.x * F.nmask : 0), 0, 0x7fffffff, 0x00020000);
     DGS_STAMP(0);
     // timenet layer 0 operands, in flight during the positional encodings
     float4 t1a0 = make_float4(0.f, 0.f, 0.f, 0.f), t1a1 = t1a0;
@@ -587,6 +606,7 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) vo
         f32x16 c = zero16();
         gemm_t1(t1a0, t1a1, lds, G_TIN, lane, c);
         bias_relu(c, t1b);
+        if (SAVE) store_mask_bits(c, mrsrc, M_TH + wave * 32, lane);
         acc_to_lds(c, lds, G_H, wave * 32, lane);
         lds_barrier();
         DGS_STAMP(2);
@@ -621,6 +641,7 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) vo
         lds_barrier();  // all waves finished reading H before it is overwritten
         DGS_STAMP(5 + 3 * L);
         bias_relu(c, bv);
+        if (SAVE) store_mask_bits(c, mrsrc, m_h(L) + wave * 32, lane);
         acc_to_lds(c, lds, G_H, wave * 32, lane);
         lds_barrier();
         DGS_STAMP(6 + 3 * L);
@@ -649,35 +670,37 @@ struct BwdArgs {
     size_t Ns;
     const float *packed;
     const float *saved;
+    const uint32_t *mask;
     const float *dout;
     float *dz;
     int tHd, tL[8], tT2;
     int flags;
 };
 
-// relu' mask rows of this wave's 32x32 accumulator tile (the saved activations of the layer input)
-struct Mask16 {
-    float v[16];
+// relu' of the layer input for this wave's 32x32 tile: the forward's 16 bits per lane (same lane
+// layout), one u16 load per lane ahead of the GEMM instead of 16 activation loads
+struct MaskBits {
+    uint32_t w;
 };
 
-__device__ inline void mask_load(Mask16 &mk, const float *__restrict__ saved_rows, size_t Ns, int p0, int lane, int n0) {
-    const TileAddr t = tile_addr(saved_rows, Ns, 0, n0, p0, lane);
-#pragma unroll
-    for (int r = 0; r < 16; r++) mk.v[r] = t.ld(r);
-}
-
-__device__ inline void mask_apply(f32x16 &acc, const Mask16 &mk) {
-#pragma unroll
-    for (int r = 0; r < 16; r++) acc[r] = mk.v[r] > 0.f ? acc[r] : 0.f;
-}
-
-struct MaskPre {  // the tile's relu' mask, issued after the GEMM prologue
-    Mask16 *mk;
-    const float *rows;
-    size_t Ns;
-    int p0, lane, n0;
-    __device__ void operator()() const { mask_load(*mk, rows, Ns, p0, lane, n0); }
+struct MaskPre {
+    MaskBits *mk;
+    const uint32_t *words;  // &mask[block][mrow0 + n0]: 64 u16, one per lane
+    int lane;
+    __device__ void operator()() const {
+#ifdef DGS_DIAG_NO_MASK  // timing experiment only: masks all-ones, no loads (wrong gradients)
+        mk->w = 0xffffu;
+#else
+        mk->w = reinterpret_cast<const unsigned short *>(words)[lane];
+#endif
+    }
 };
+
+__device__ inline void mask_apply(f32x16 &acc, const MaskBits &mk) {
+#pragma unroll
+    for (int r = 0; r < 16; r++)  // bit r sign-extended to 0 / all-ones
+        acc[r] = __int_as_float(__float_as_int(acc[r]) & __builtin_amdgcn_sbfe((int)mk.w, r, 1));
+}
 
 __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_mlp_bwd(BwdArgs a) {
     __shared__ float4 lds[G_TOTAL * BM];
@@ -687,6 +710,7 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) vo
     const Flags F = make_flags(a.flags);
     const float4 *pk = reinterpret_cast<const float4 *>(a.packed);
     float *lf = reinterpret_cast<float *>(lds);
+    const uint32_t *mwords = a.mask + (size_t)blockIdx.x * F.nmask + wave * 32;  // + mask row
     // dOut -> LDS TE region (the head-gradient image G) and dz rows Z_G
     for (int e = tid; e < 32 * BM; e += NTHR) {
         int m = e % BM, c = e / BM;
@@ -700,10 +724,9 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) vo
     f32x16 kt;  // dZ of the layer whose GEMM runs next
     // heads^T: dH7 = W_h^T dOut (K = 32 from TE region) -> mask H7 -> dZ7
     {
-        Mask16 mk;
+        MaskBits mk;
         f32x16 c = zero16();
-        gemm<4>(pk + a.tHd / 4 + wave * 4 * 64, 0, lds, G_TE, lane, c,
-                MaskPre{&mk, a.saved + (size_t)s_h(7) * a.Ns, a.Ns, p0, lane, wave * 32});
+        gemm<4>(pk + a.tHd / 4 + wave * 4 * 64, 0, lds, G_TE, lane, c, MaskPre{&mk, mwords + m_h(7), lane});
         mask_apply(c, mk);
         lds_barrier();  // TE (dOut image) reads done before TE is reused for dTE
         acc_to_lds(c, lds, G_H, wave * 32, lane);
@@ -721,10 +744,9 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) vo
             gemm<4>(pk + a.tL[5] / 4 + (F_TE / 32) * 32 * 64, wave * 4, lds, G_H, lane, ct);
             acc_to_lds(ct, lds, G_PART + 8 * wave, 0, lane);
         }
-        Mask16 mk;  // relu' of H_{L-1}, in flight during the GEMM
+        MaskBits mk;  // relu' of H_{L-1}, in flight during the GEMM
         f32x16 c = zero16();
-        gemm<32>(pk + a.tL[L] / 4 + (tile0 + wave) * 32 * 64, 0, lds, G_H, lane, c,
-                 MaskPre{&mk, a.saved + (size_t)s_h(L - 1) * a.Ns, a.Ns, p0, lane, wave * 32},
+        gemm<32>(pk + a.tL[L] / 4 + (tile0 + wave) * 32 * 64, 0, lds, G_H, lane, c, MaskPre{&mk, mwords + m_h(L - 1), lane},
                  Stash1{kt, tile_addr(a.dz, a.Ns, Z_L0 + L * 256, wave * 32, p0, lane)});
         mask_apply(c, mk);
         lds_barrier();
@@ -751,10 +773,9 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) vo
     lds_to_global(lds, G_TE, 8, a.dz, Z_TE, a.Ns, p0, tid);
     // timenet.2^T: dTH = W_T2^T dTE (K = 32) -> mask TH -> dZ_T1
     {
-        Mask16 mk;
+        MaskBits mk;
         f32x16 c = zero16();
-        gemm<4>(pk + a.tT2 / 4 + wave * 4 * 64, 0, lds, G_TE, lane, c,
-                MaskPre{&mk, a.saved + (size_t)S_TH * a.Ns, a.Ns, p0, lane, wave * 32});
+        gemm<4>(pk + a.tT2 / 4 + wave * 4 * 64, 0, lds, G_TE, lane, c, MaskPre{&mk, mwords + M_TH, lane});
         mask_apply(c, mk);
         Stash1{c, tile_addr(a.dz, a.Ns, Z_T1, wave * 32, p0, lane)}.store_all();
     }
@@ -1134,7 +1155,11 @@ extern "C" int dgs_deform_outputs(int flags) { return make_flags(flags).nout; }
 extern "C" int dgs_deform_num_params(int flags) { return make_plan(flags).nparams; }
 extern "C" size_t dgs_deform_packed_floats(int flags) { return (size_t)make_plan(flags).total; }
 static size_t padded_points(int N) { return (size_t)div_up(N, BM) * BM; }
-extern "C" size_t dgs_deform_saved_floats(int flags, int N) { return (size_t)make_flags(flags).nsaved * padded_points(N); }
+// saved activations [nsaved][Ns] floats, then the relu' bits [Ns / 32 blocks][nmask] u32 words
+extern "C" size_t dgs_deform_saved_floats(int flags, int N) {
+    const Flags F = make_flags(flags);
+    return (size_t)F.nsaved * padded_points(N) + (size_t)F.nmask * (padded_points(N) / BM);
+}
 
 extern "C" size_t dgs_deform_scratch_floats(int flags, int N) {
     Flags F = make_flags(flags);
@@ -1251,6 +1276,7 @@ extern "C" int dgs_deform_forward(int flags, int N, const float *xyz, const floa
     a.N = N;
     a.Ns = padded_points(N);
     a.xyz = xyz; a.t = t; a.packed = packed; a.out = out; a.saved = saved;
+    a.mask = saved ? reinterpret_cast<uint32_t *>(saved + (size_t)P.F.nsaved * a.Ns) : nullptr;
     a.fT1 = P.fT1; a.fT2 = P.fT2; a.fHd = P.fHd; a.bT1 = P.bT1; a.bT2 = P.bT2; a.bHd = P.bHd;
     for (int i = 0; i < 8; i++) { a.fL[i] = P.fL[i]; a.bL[i] = P.bL[i]; }
     a.flags = flags;
@@ -1287,6 +1313,7 @@ extern "C" int dgs_deform_backward(int flags, int N, const float *packed, const 
     float *slabs = scratch + (size_t)F.nz * Ns;
     BwdArgs b{};
     b.N = N; b.Ns = Ns; b.packed = packed; b.saved = saved; b.dout = dout; b.dz = dz;
+    b.mask = reinterpret_cast<const uint32_t *>(saved + (size_t)F.nsaved * Ns);
     b.tHd = P.tHd; b.tT2 = P.tT2;
     for (int i = 0; i < 8; i++) b.tL[i] = P.tL[i];
     b.flags = flags;
