@@ -46,6 +46,9 @@ constexpr int F_XE = 0, F_TE = 64, F_H = 96;
 // saved-activation row offsets ([rows][Ns], feature-major); order keeps each layer input contiguous
 constexpr int S_H0 = 0, S_XE = 1024, S_TE = 1088, S_H4 = 1120, S_TIN = 2144, S_TH = 2160;
 __host__ __device__ constexpr int s_h(int i) { return i < 4 ? S_H0 + 256 * i : S_H4 + 256 * (i - 4); }
+// timenet of a frame-uniform t (blender), evaluated once per launch by k_timenet into the tail of
+// the saved buffer: [t0 | TIN (16) | TE (32) | TH (256)]
+constexpr int TC_T = 0, TC_TIN = 16, TC_TE = 32, TC_TH = 64, TC_FLOATS = 512;
 // relu' bit-mask rows: H0..H7 then TH (blender)
 __host__ __device__ constexpr int m_h(int i) { return 256 * i; }
 constexpr int M_TH = 2048;
@@ -517,6 +520,7 @@ struct FwdArgs {
     float *out;
     float *saved;
     uint32_t *mask;  // relu' bits, [block][nmask] words (after the saved rows)
+    float *tc;       // timenet of t[0] (k_timenet), or nullptr
     int fT1, fT2, fL[8], fHd, bT1, bT2, bL[8], bHd;
     int flags;
 };
@@ -530,6 +534,62 @@ __device__ inline void store_mask_bits(const f32x16 &c, __amdgpu_buffer_rsrc_t m
 #pragma unroll
     for (int r = 0; r < 16; r++) w |= (uint32_t)min(max(__float_as_int(c[r]), 0), 1) << r;
     __builtin_amdgcn_raw_buffer_store_b16((unsigned short)w, mrsrc, lane * 2, srow * 4, 0);
+}
+
+// The reference feeds every Gaussian the same frame time (render(): fid.unsqueeze(0).expand(N, 1),
+// train_baseline.py:107-108), so the timenet (time_utils.py:74-76, 13 -> 256 -> 30) has one value
+// per launch. k_timenet evaluates it for t[0] (fp32, one workgroup); a k_mlp_fwd block whose points
+// all carry that t broadcasts TE / TH instead of running T1, T2 and the t encodings per point.
+__global__ __launch_bounds__(256) void k_timenet(FwdArgs a) {
+    __shared__ float tin[16], th[256];
+    const int j = threadIdx.x;
+    const float t0 = a.t[0];
+    const int tinF = 13;  // blender: t, sin / cos of 2^i t, i < 6
+    if (j < 16) {
+        float v = 0.f;
+        if (j == 0) {
+            v = t0;
+        } else if (j < tinF) {
+            float sv, cv;
+            sincosf(t0 * (float)(1 << ((j - 1) >> 1)), &sv, &cv);
+            v = (j & 1) ? sv : cv;
+        }
+        tin[j] = v;
+        a.tc[TC_TIN + j] = v;
+    }
+    if (j == 0) a.tc[TC_T] = t0;
+    __syncthreads();
+    {  // TH[j]: A image element [tile j/32][chunk c][lane 32h + j%32] = W_T1[j][8c + 4h .. +3]
+        const float4 *A = reinterpret_cast<const float4 *>(a.packed + a.fT1) + (j >> 5) * 2 * 64 + (j & 31);
+        float acc = a.packed[a.bT1 + j];
+#pragma unroll
+        for (int c = 0; c < 2; c++)
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const float4 w = A[c * 64 + h * 32];
+                const int f = 8 * c + 4 * h;
+                acc += w.x * tin[f] + w.y * tin[f + 1] + w.z * tin[f + 2] + w.w * tin[f + 3];
+            }
+        acc = fmaxf(acc, 0.f);
+        th[j] = acc;
+        a.tc[TC_TH + j] = acc;
+    }
+    __syncthreads();
+    {  // TE[k], k < 32 (rows 30, 31 are zero padding): 8 lanes per output, 32 features each
+        const int k = j >> 3, q = j & 7;
+        const float4 *A = reinterpret_cast<const float4 *>(a.packed + a.fT2);
+        float acc = 0.f;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {  // features 32q + 4u .. +3: chunk (32q + 4u) / 8, half u & 1
+            const int f = 32 * q + 4 * u;
+            const float4 w = A[(f >> 3) * 64 + ((f >> 2) & 1) * 32 + k];
+            acc += w.x * th[f] + w.y * th[f + 1] + w.z * th[f + 2] + w.w * th[f + 3];
+        }
+        acc += __shfl_xor(acc, 1);
+        acc += __shfl_xor(acc, 2);
+        acc += __shfl_xor(acc, 4);
+        if (q == 0) a.tc[TC_TE + k] = acc + a.packed[a.bT2 + k];
+    }
 }
 
 // Workgroup = 32 points x 8 waves (wave w owns output rows 32w..32w+31 of every 256-wide layer);
@@ -547,6 +607,19 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) vo
     const __amdgpu_buffer_rsrc_t mrsrc =
         __builtin_amdgcn_make_buffer_rsrc(a.mask + (SAVE ? (size_t)blockIdx.x * F.nmask : 0), 0, 0x7fffffff, 0x00020000);
     DGS_STAMP(0);
+#ifdef DGS_MLP_PROFILE
+    if (threadIdx.x == 0) {
+        dgs_mlp_prof[blockIdx.x * 256 + 252] = __builtin_amdgcn_s_memrealtime();
+        dgs_mlp_prof[blockIdx.x * 256 + 253] = __builtin_amdgcn_s_memtime();
+    }
+#endif
+    // frame-uniform t: every valid point of the block carries k_timenet's t0 (wave-local check on the
+    // same 32 values in every wave, so the branch is block-uniform without a barrier)
+    float tv_own = 0.f, tc_t0 = 1.f;
+    if (SAVE && F.blender && a.tc) {
+        tc_t0 = a.tc[TC_T];
+        tv_own = (lane < BM && p0 + lane < a.N) ? a.t[p0 + lane] : tc_t0;
+    }
     // timenet layer 0 operands, in flight during the positional encodings
     float4 t1a0 = make_float4(0.f, 0.f, 0.f, 0.f), t1a1 = t1a0;
     Bias4 t1b{};
@@ -558,8 +631,9 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) vo
     }
     // ---- positional encodings (utils/time_utils.py:42-54): feature 3 band + d, band 0 = x,
     // band 1 + 2i = sin(2^i x), band 2 + 2i = cos(2^i x); one sincosf per (point, dim, frequency) ----
+    bool uniform_t = false;
+    auto put = [&](int g0, int f, int m, float v) { lf[((g0 + f / 4) * BM + m) * 4 + (f & 3)] = v; };
     {
-        auto put = [&](int g0, int f, int m, float v) { lf[((g0 + f / 4) * BM + m) * 4 + (f & 3)] = v; };
         for (int e = tid; e < BM * 3 * 11; e += NTHR) {
             const int m = e % BM, r = e / BM, d = r % 3, i = r / 3;  // i = 10: identity band
             const int p = p0 + m;
@@ -574,6 +648,16 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) vo
             }
         }
         for (int m = tid; m < BM; m += NTHR) put(G_XE, 63, m, 0.f);  // padding feature
+        uniform_t = SAVE && F.blender && a.tc && __ballot(tv_own != tc_t0) == 0;
+    }
+    if (uniform_t) {  // TE and TIN images: k_timenet's values broadcast over the 32 points
+        const float4 *tc4 = reinterpret_cast<const float4 *>(a.tc);
+        for (int e = tid; e < 12 * BM; e += NTHR) {
+            const int gi = e / BM, m = e % BM;
+            if (gi < 8) lds[(G_TE + gi) * BM + m] = tc4[TC_TE / 4 + gi];
+            else lds[(G_TIN + gi - 8) * BM + m] = tc4[TC_TIN / 4 + gi - 8];
+        }
+    } else {
         const int tg = F.blender ? G_TIN : G_TE;
         const int nfreq = (F.tin - 1) / 2, ng = F.blender ? 4 : 8;
         for (int e = tid; e < BM * 4 * ng; e += NTHR) {  // zero the whole t image (padding)
@@ -602,7 +686,20 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) vo
     const float *bias = a.packed;
     f32x16 kt = zero16();  // previous layer's activations, awaiting their store
     // ---- timenet (blender): Linear(13,256) + ReLU -> H ; Linear(256,30) -> TE ----
-    if (F.blender) {
+    if (uniform_t) {  // TH tile of this wave from k_timenet: relu' bits and the saved rows
+        const Bias4 th = load_bias(a.tc + TC_TH, wave * 32, lane);
+        f32x16 c;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            c[4 * j] = th.v[j].x;
+            c[4 * j + 1] = th.v[j].y;
+            c[4 * j + 2] = th.v[j].z;
+            c[4 * j + 3] = th.v[j].w;
+        }
+        store_mask_bits(c, mrsrc, M_TH + wave * 32, lane);
+        Stash1{c, tile_addr(a.saved, a.Ns, S_TH, wave * 32, p0, lane)}.store_all();
+        DGS_STAMP(2);
+    } else if (F.blender) {
         f32x16 c = zero16();
         gemm_t1(t1a0, t1a1, lds, G_TIN, lane, c);
         bias_relu(c, t1b);
@@ -660,6 +757,12 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) vo
         if (p < a.N) a.out[(size_t)p * F.nout + c] = lf[((G_TE + c / 4) * BM + m) * 4 + (c & 3)];
     }
     DGS_STAMP(29);
+#ifdef DGS_MLP_PROFILE
+    if (threadIdx.x == 0) {  // shader-clock rate: s_memtime vs the 100 MHz s_memrealtime
+        dgs_mlp_prof[blockIdx.x * 256 + 254] = __builtin_amdgcn_s_memrealtime();
+        dgs_mlp_prof[blockIdx.x * 256 + 255] = __builtin_amdgcn_s_memtime();
+    }
+#endif
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1155,10 +1258,11 @@ extern "C" int dgs_deform_outputs(int flags) { return make_flags(flags).nout; }
 extern "C" int dgs_deform_num_params(int flags) { return make_plan(flags).nparams; }
 extern "C" size_t dgs_deform_packed_floats(int flags) { return (size_t)make_plan(flags).total; }
 static size_t padded_points(int N) { return (size_t)div_up(N, BM) * BM; }
-// saved activations [nsaved][Ns] floats, then the relu' bits [Ns / 32 blocks][nmask] u32 words
+// saved activations [nsaved][Ns] floats, then the relu' bits [Ns / 32 blocks][nmask] u32 words, then
+// the frame-uniform timenet values (TC_FLOATS)
 extern "C" size_t dgs_deform_saved_floats(int flags, int N) {
     const Flags F = make_flags(flags);
-    return (size_t)F.nsaved * padded_points(N) + (size_t)F.nmask * (padded_points(N) / BM);
+    return (size_t)F.nsaved * padded_points(N) + (size_t)F.nmask * (padded_points(N) / BM) + TC_FLOATS;
 }
 
 extern "C" size_t dgs_deform_scratch_floats(int flags, int N) {
@@ -1282,6 +1386,10 @@ extern "C" int dgs_deform_forward(int flags, int N, const float *xyz, const floa
     a.flags = flags;
     {
         ScopedTimer tm("mlp_fwd", stream);
+        if (saved && P.F.blender) {
+            a.tc = saved + (size_t)P.F.nsaved * a.Ns + (size_t)P.F.nmask * (a.Ns / BM);
+            hipLaunchKernelGGL(k_timenet, dim3(1), dim3(256), 0, stream, a);
+        }
         if (saved)
             hipLaunchKernelGGL(k_mlp_fwd<true>, dim3(div_up(N, BM)), dim3(NTHR), 0, stream, a);
         else

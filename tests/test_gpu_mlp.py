@@ -57,14 +57,25 @@ def test_mlp_golden(name, golden_dir):
             assert np.abs(g).max() == 0.0, k  # unused heads of the fork variant
 
 
-@pytest.mark.parametrize("name", ["blender", "nonblender"])
+def _times(rng, N, mode):
+    if mode == "random":
+        return rng.uniform(0, 1, (N, 1)).astype(np.float32)
+    t = np.full((N, 1), 0.37, np.float32)  # one frame time (train_baseline.py:107-110)
+    if mode == "mixed":  # a few 32-point blocks carry other times: per-point timenet there
+        t[min(37, N - 1)] = 0.81
+        t[N // 2:N // 2 + 40] = rng.uniform(0, 1, (min(40, N - N // 2), 1)).astype(np.float32)
+    return t
+
+
+@pytest.mark.parametrize("name,tmode", [("blender", "random"), ("nonblender", "random"), ("blender", "uniform"),
+                                        ("blender", "mixed"), ("nonblender", "uniform")])
 @pytest.mark.parametrize("N", [1, 63, 1000, 4099])
-def test_mlp_vs_oracle_ragged(name, N):
+def test_mlp_vs_oracle_ragged(name, tmode, N):
     bl, d6, fork = VARIANTS[name]
     net, w = _net(name, 77)
     rng = np.random.default_rng(N)
     x = rng.uniform(-1.3, 1.3, (N, 3)).astype(np.float32)
-    t = rng.uniform(0, 1, (N, 1)).astype(np.float32)
+    t = _times(rng, N, tmode)
     out, c = mlp_ref.forward(w, x, t, bl, d6)
     d_xyz, d_rot, d_scale = net(torch.from_numpy(x).cuda(), torch.from_numpy(t).cuda())
     for a, b in ((d_xyz, out["d_xyz"]), (d_rot, out["d_rot"]), (d_scale, out["d_scale"])):

@@ -60,6 +60,15 @@ int main(int argc, char **argv) {
         total += (double)(s[29] - s[0]);
     }
     printf("mean cycles per block: %.0f\n", total / blocks);
+    {
+        double rt = 0, ck = 0;
+        for (int b = 0; b < blocks; b++) {
+            const unsigned long long *s = &hp[(size_t)b * 256];
+            rt += (double)(s[254] - s[252]);
+            ck += (double)(s[255] - s[253]);
+        }
+        printf("s_memtime rate: %.3f GHz (vs 100 MHz s_memrealtime)\n", 0.1 * ck / rt);
+    }
     for (int k = 1; k < 30; k++) {
         char buf[32];
         const char *nm = names[k - 1];

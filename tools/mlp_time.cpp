@@ -1,15 +1,16 @@
-// Diagnostic: event-timed k_mlp_fwd / k_mlp_bwd / k_dw at N = 100k (random weights).
+// Diagnostic: event-timed k_mlp_fwd / k_mlp_bwd / k_dw at N points (argv[1], default 100k).
 // Build: hipcc -O3 --offload-arch=gfx950 -munsafe-fp-atomics -I include tools/mlp_time.cpp \
 //        deformable-3d-gaussians_amd/csrc/mlp.hip deformable-3d-gaussians_amd/csrc/api.hip -o tools/mlp_time.bin
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include <vector>
 
 #include "dgs.h"
 
-int main() {
-    const int N = 100000, flags = DGS_MLP_BLENDER;
+int main(int argc, char **argv) {
+    const int N = argc > 1 ? atoi(argv[1]) : 100000, flags = DGS_MLP_BLENDER;
     const size_t npk = dgs_deform_packed_floats(flags), nsv = dgs_deform_saved_floats(flags, N);
     const size_t nsc = dgs_deform_scratch_floats(flags, N);
     float *pk, *x, *t, *out, *saved, *dout, *scratch, *gbuf;
@@ -46,7 +47,7 @@ int main() {
     for (const char *n : names) {
         int l = 0;
         double ms = dgs_timing_query(n, &l);
-        printf("%-14s %.4f ms\n", n, l ? ms / l : 0.0);
+        printf("N=%-7d %-14s %.4f ms\n", N, n, l ? ms / l : 0.0);
     }
     return 0;
 }
