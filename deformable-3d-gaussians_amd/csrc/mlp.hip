@@ -29,9 +29,12 @@
 #include <vector>
 
 #include "dgs_common.h"
+#include "mlp_shared.h"
 
 namespace dgs {
 namespace mlp {
+
+using namespace mlpc;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -40,49 +43,9 @@ constexpr int NWAVE = 8;
 constexpr int NTHR = NWAVE * 64;
 // LDS group offsets (1 group = 32 points x 4 features = 512 B); PART = 8 K-part slots of 8 groups
 constexpr int G_XE = 0, G_TE = 16, G_H = 24, G_TIN = 88, G_PART = 92, G_TOTAL = 156;
-// padded feature offsets of the concatenated layer input (XE|TE|H)
-constexpr int F_XE = 0, F_TE = 64, F_H = 96;
-
-// saved-activation row offsets ([rows][Ns], feature-major); order keeps each layer input contiguous
-constexpr int S_H0 = 0, S_XE = 1024, S_TE = 1088, S_H4 = 1120, S_TIN = 2144, S_TH = 2160;
-__host__ __device__ constexpr int s_h(int i) { return i < 4 ? S_H0 + 256 * i : S_H4 + 256 * (i - 4); }
-// timenet of a frame-uniform t (blender), evaluated once per launch by k_timenet into the tail of
-// the saved buffer: [t0 | TIN (16) | TE (32) | TH (256)]
-constexpr int TC_T = 0, TC_TIN = 16, TC_TE = 32, TC_TH = 64, TC_FLOATS = 512;
-// relu' bit-mask rows: H0..H7 then TH (blender)
-__host__ __device__ constexpr int m_h(int i) { return 256 * i; }
-constexpr int M_TH = 2048;
-// dZ scratch rows
-constexpr int Z_L0 = 0, Z_G = 2048, Z_TE = 2080, Z_T1 = 2112;
-
-struct Flags {
-    bool blender, sixdof, norotscale;
-    int nout;     // head outputs: 10 or 13
-    int tin;      // raw t PE channels: 13 (L=6) or 21 (L=10)
-    int nsaved;   // saved rows
-    int nmask;    // relu' bit-mask rows (one u32 word = 32 points per row and block)
-    int nz;       // dZ rows
-};
-
-__host__ __device__ inline Flags make_flags(int f) {
-    Flags F;
-    F.blender = f & DGS_MLP_BLENDER;
-    F.sixdof = f & DGS_MLP_6DOF;
-    F.norotscale = f & DGS_MLP_NO_ROTSCALE;
-    F.nout = F.sixdof ? 13 : 10;
-    F.tin = F.blender ? 13 : 21;
-    F.nsaved = F.blender ? 2416 : 2144;
-    F.nmask = F.blender ? 2304 : 2048;
-    F.nz = F.blender ? 2368 : 2080;
-    return F;
-}
-
 // ------------------------------------------------------------------------------------------------
 // packing plan (host): which A-operand images exist and where
 // ------------------------------------------------------------------------------------------------
-struct Seg {  // padded index range [p0, p0+len) <- source index s0 + (p - p0)
-    int p0, len, s0;
-};
 struct PackJob {
     int src;            // parameter index (weight)
     int transpose;      // 0: A[n][f] = W[n][f]; 1: A[n][f] = W[f][n] (n over input features)
@@ -99,13 +62,8 @@ struct BiasJob {
     int off;
 };
 
-struct Plan {
+struct Plan : Params {
     Flags F;
-    int nparams;
-    // parameter indices (state_dict order)
-    int pT0w = -1, pT0b = -1, pT2w = -1, pT2b = -1, pLw[8], pLb[8];
-    int nheads;               // number of head linears (3 or 4)
-    int pHw[4], pHb[4], hrows[4];
     std::vector<PackJob> jobs;
     std::vector<BiasJob> biases;
     // forward A images
@@ -117,49 +75,11 @@ struct Plan {
     int total;
 };
 
-inline Seg seg(int p0, int len, int s0) { return Seg{p0, len, s0}; }
-
-// input-feature segments of the concatenated trunk inputs
-inline int layer_in_segs(const Flags &F, int layer, Seg *s) {
-    const int te = F.blender ? 30 : F.tin;
-    if (layer == 0) {
-        s[0] = seg(F_XE, 63, 0);
-        s[1] = seg(F_TE, te, 63);
-        return 2;
-    }
-    if (layer == 5) {
-        s[0] = seg(F_XE, 63, 0);
-        s[1] = seg(F_TE, te, 63);
-        s[2] = seg(F_H, 256, 63 + te);
-        return 3;
-    }
-    s[0] = seg(0, 256, 0);
-    return 1;
-}
-
-__host__ __device__ inline int layer_kpad(int layer) { return layer == 0 ? 96 : layer == 5 ? 352 : 256; }
-
 Plan make_plan(int flags) {
     Plan P;
     P.F = make_flags(flags);
     const Flags &F = P.F;
-    int k = 0;
-    if (F.blender) {
-        P.pT0w = k++; P.pT0b = k++; P.pT2w = k++; P.pT2b = k++;
-    }
-    for (int i = 0; i < 8; i++) {
-        P.pLw[i] = k++;
-        P.pLb[i] = k++;
-    }
-    P.nheads = F.sixdof ? 4 : 3;
-    int hr[4] = {3, 3, 4, 3};
-    int hr3[3] = {3, 4, 3};
-    for (int h = 0; h < P.nheads; h++) {
-        P.pHw[h] = k++;
-        P.pHb[h] = k++;
-        P.hrows[h] = F.sixdof ? hr[h] : hr3[h];
-    }
-    P.nparams = k;
+    static_cast<Params &>(P) = make_params(F);
     int off = 0;
     auto add_job = [&](int src, int tr, int ntiles, int nchunks, int nsn, const Seg *sn, int nsf, const Seg *sf) {
         PackJob j{};
@@ -241,13 +161,6 @@ Plan make_plan(int flags) {
     return P;
 }
 
-// source index of padded index p under segments (or -1 = zero padding)
-__host__ __device__ inline int seg_lookup(const Seg *s, int ns, int p) {
-    for (int q = 0; q < ns; q++)
-        if (p >= s[q].p0 && p < s[q].p0 + s[q].len) return s[q].s0 + (p - s[q].p0);
-    return -1;
-}
-
 // Packing is one gather launch: map[i] = (parameter << 22) | element for packed float i, or -1 for
 // zero padding. The map depends only on the flags (built once on the host, cached on the device).
 constexpr int PACK_MAXP = 32;
@@ -268,14 +181,6 @@ __global__ __launch_bounds__(256) void k_pack_map(const int *__restrict__ map, P
 // ------------------------------------------------------------------------------------------------
 // device GEMM pieces
 // ------------------------------------------------------------------------------------------------
-// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS traffic (lgkmcnt 0) but not
-// for its global stores (__syncthreads() also waits vmcnt(0), a release fence). No wave of
-// k_mlp_* reads global memory another wave of the block wrote.
-__device__ inline void lds_barrier() {
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // gfx9 encoding: vmcnt 63, expcnt 7, lgkmcnt 0
-    __builtin_amdgcn_s_barrier();
-}
-
 __device__ inline f32x16 zero16() {
     f32x16 z;
 #pragma unroll
@@ -337,30 +242,6 @@ struct NoPre {
 struct NoStash {
     __device__ void store(int) const {}
 };
-
-// A wave's 32-row tile of a feature-major [rows][Ns] array, addressed through a buffer descriptor
-// whose base is the tile origin (wave-uniform: SGPRs): each access is one buffer instruction with
-// the lane offset in a VGPR and the row offset in an SGPR, no per-access address arithmetic (which
-// the compiler otherwise hoists into 16 live 64-bit addresses).
-struct TileAddr {
-    __amdgpu_buffer_rsrc_t rsrc;  // base = &dst[(row0 + n0) * Ns + p0]
-    int voff;                     // (4h * Ns + m) * 4 bytes
-    int ns4;                      // Ns * 4 bytes
-    __device__ static constexpr int row(int r) { return 8 * (r >> 2) + (r & 3); }
-    __device__ void st(int r, float v) const {
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc, voff, row(r) * ns4, 0);
-    }
-    __device__ float ld(int r) const {
-        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, row(r) * ns4, 0));
-    }
-};
-
-__device__ inline TileAddr tile_addr(const float *dst, size_t Ns, int row0, int n0, int p0, int lane) {
-    const float *base = dst + (size_t)(row0 + n0) * Ns + p0;
-    // a 32-row tile spans 32 * Ns floats; the descriptor's record count only bounds-checks
-    return TileAddr{__builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(base), 0, 0x7fffffff, 0x00020000),
-                    (4 * (lane >> 5) * (int)Ns + (lane & 31)) * 4, (int)Ns * 4};
-}
 
 struct Stash1 {
     f32x16 t;
@@ -525,17 +406,6 @@ struct FwdArgs {
     int flags;
 };
 
-// relu' of this wave's 32x32 output tile as bits, kept in the accumulator's own lane layout:
-// lane (m, h) packs bit r = [value of row 8(r>>2)+4h+(r&3), point m > 0] into a u16. The backward's
-// GEMM over the same 32-row tile has the identical lane layout, so no transpose is needed either way.
-// Signed clamp of the float bits: -0.0 and +0.0 give 0, positive values 1.
-__device__ inline void store_mask_bits(const f32x16 &c, __amdgpu_buffer_rsrc_t mrsrc, int srow, int lane) {
-    uint32_t w = 0;
-#pragma unroll
-    for (int r = 0; r < 16; r++) w |= (uint32_t)min(max(__float_as_int(c[r]), 0), 1) << r;
-    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)w, mrsrc, lane * 2, srow * 4, 0);
-}
-
 // The reference feeds every Gaussian the same frame time (render(): fid.unsqueeze(0).expand(N, 1),
 // train_baseline.py:107-108), so the timenet (time_utils.py:74-76, 13 -> 256 -> 30) has one value
 // per launch. k_timenet evaluates it for t[0] (fp32, one workgroup); a k_mlp_fwd block whose points
@@ -696,14 +566,14 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) vo
             c[4 * j + 2] = th.v[j].z;
             c[4 * j + 3] = th.v[j].w;
         }
-        store_mask_bits(c, mrsrc, M_TH + wave * 32, lane);
+        store_mask_bits(c, mrsrc, (M_TH + wave * 32) * 4, lane);
         Stash1{c, tile_addr(a.saved, a.Ns, S_TH, wave * 32, p0, lane)}.store_all();
         DGS_STAMP(2);
     } else if (F.blender) {
         f32x16 c = zero16();
         gemm_t1(t1a0, t1a1, lds, G_TIN, lane, c);
         bias_relu(c, t1b);
-        if (SAVE) store_mask_bits(c, mrsrc, M_TH + wave * 32, lane);
+        if (SAVE) store_mask_bits(c, mrsrc, (M_TH + wave * 32) * 4, lane);
         acc_to_lds(c, lds, G_H, wave * 32, lane);
         lds_barrier();
         DGS_STAMP(2);
@@ -738,7 +608,7 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) vo
         lds_barrier();  // all waves finished reading H before it is overwritten
         DGS_STAMP(5 + 3 * L);
         bias_relu(c, bv);
-        if (SAVE) store_mask_bits(c, mrsrc, m_h(L) + wave * 32, lane);
+        if (SAVE) store_mask_bits(c, mrsrc, (m_h(L) + wave * 32) * 4, lane);
         acc_to_lds(c, lds, G_H, wave * 32, lane);
         lds_barrier();
         DGS_STAMP(6 + 3 * L);
@@ -799,12 +669,6 @@ struct MaskPre {
     }
 };
 
-__device__ inline void mask_apply(f32x16 &acc, const MaskBits &mk) {
-#pragma unroll
-    for (int r = 0; r < 16; r++)  // bit r sign-extended to 0 / all-ones
-        acc[r] = __int_as_float(__float_as_int(acc[r]) & __builtin_amdgcn_sbfe((int)mk.w, r, 1));
-}
-
 __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_mlp_bwd(BwdArgs a) {
     __shared__ float4 lds[G_TOTAL * BM];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -830,7 +694,7 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) vo
         MaskBits mk;
         f32x16 c = zero16();
         gemm<4>(pk + a.tHd / 4 + wave * 4 * 64, 0, lds, G_TE, lane, c, MaskPre{&mk, mwords + m_h(7), lane});
-        mask_apply(c, mk);
+        mask_apply(c, mk.w);
         lds_barrier();  // TE (dOut image) reads done before TE is reused for dTE
         acc_to_lds(c, lds, G_H, wave * 32, lane);
         kt = c;
@@ -851,7 +715,7 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) vo
         f32x16 c = zero16();
         gemm<32>(pk + a.tL[L] / 4 + (tile0 + wave) * 32 * 64, 0, lds, G_H, lane, c, MaskPre{&mk, mwords + m_h(L - 1), lane},
                  Stash1{kt, tile_addr(a.dz, a.Ns, Z_L0 + L * 256, wave * 32, p0, lane)});
-        mask_apply(c, mk);
+        mask_apply(c, mk.w);
         lds_barrier();
         if (L == 5 && F.blender) sum_parts(lds, G_TE, nullptr, tid, true);
         acc_to_lds(c, lds, G_H, wave * 32, lane);
@@ -879,7 +743,7 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) vo
         MaskBits mk;
         f32x16 c = zero16();
         gemm<4>(pk + a.tT2 / 4 + wave * 4 * 64, 0, lds, G_TE, lane, c, MaskPre{&mk, mwords + M_TH, lane});
-        mask_apply(c, mk);
+        mask_apply(c, mk.w);
         Stash1{c, tile_addr(a.dz, a.Ns, Z_T1, wave * 32, p0, lane)}.store_all();
     }
 }
@@ -889,30 +753,14 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) vo
 // the point axis in proportion to each tile's work so ~one workgroup per CU finishes together;
 // fixed-order slab reduction (deterministic).
 // ------------------------------------------------------------------------------------------------
-constexpr int WT = 256;            // tile edge (rows of dZ, rows of X)
-constexpr int SLAB = WT * WT + WT; // tile + bias row sums
 constexpr int PC = 32;             // points per LDS chunk
 constexpr int LDA = PC + 4;        // padded LDS row (floats)
-constexpr int MAXJ = 12;
 constexpr int DW_THREADS = 512;    // 8 waves: 2 (n) x 4 (k), 128 x 64 per wave
 
 // component-wise select (a select of the float4 struct itself can be lowered through scratch)
 __device__ inline float4 zsel4(float4 v, bool ok) {
     return make_float4(ok ? v.x : 0.f, ok ? v.y : 0.f, ok ? v.z : 0.f, ok ? v.w : 0.f);
 }
-
-struct WJob {
-    int zrow, nrows;   // dZ rows [zrow, zrow + nrows) (padded layer outputs, <= 256)
-    int xrow, krows;   // X rows [xrow, xrow + krows) in saved (<= 256)
-    int nsplit;        // workgroups over the point axis
-    int block0;        // first workgroup (= first slab) of this job
-    int narrow;        // wave layout: 0 = 2 (rows) x 4 (cols) waves of 128 x 64; 1 = 8 x 1 waves of
-                       // 32 x 128 (jobs with krows <= 128: every wave has work)
-};
-struct WJobs {
-    WJob j[MAXJ];
-    int n;
-};
 
 template <bool NARROW>
 __device__ __forceinline__ void dw_tile(const WJob &J, size_t Ns, const float *__restrict__ dz,
@@ -1167,129 +1015,25 @@ __global__ __launch_bounds__(256) void k_dw_reduce(RJobs R, const float *__restr
     J.dst[idx] = s;
 }
 
-// dW job list for the flags (host): layers L0..L7 (L5 as two k-tiles), heads, T1, T2
-struct WPlan {
-    WJobs jobs;
-    int layer_job[11][2];  // job index of k-tile 0/1 per layer (-1 if none)
-    int nblocks;
-};
+// fp32 dW split plan: per-chunk cost units calibrated with tools/dw_phase.cpp (full 256 x 256 tile
+// 16 + 1.5 units ~ 18.9k cycles, narrow 6 + 1.5 ~ 8.3k, 32-row jobs ~ 4.2k); one 8-wave workgroup per
+// CU (LDS 147 KiB)
+static WPlan fp32_wplan(const Flags &F) { return make_wplan(F, 256, 1.5, 4.0); }
 
-constexpr int DW_TARGET_BLOCKS = 256;  // one 8-wave workgroup per CU (LDS 147 KiB)
-
-inline WPlan make_wplan(const Flags &F) {
-    WPlan W{};
-    struct Raw {
-        int zrow, nrows, xrow, krows, layer, kt;
-    };
-    Raw raw[MAXJ];
-    int nr = 0;
-    for (int i = 0; i < 8; i++) {
-        int xrow = (i == 0 || i == 5) ? S_XE : s_h(i - 1);
-        int kp = layer_kpad(i);
-        for (int kt = 0; kt * WT < kp; kt++)
-            raw[nr++] = Raw{Z_L0 + 256 * i, 256, xrow + kt * WT, min(WT, kp - kt * WT), i, kt};
-    }
-    raw[nr++] = Raw{Z_G, 32, s_h(7), 256, 8, 0};
-    if (F.blender) {
-        raw[nr++] = Raw{Z_T1, 256, S_TIN, 16, 9, 0};
-        raw[nr++] = Raw{Z_TE, 32, S_TH, 256, 10, 0};
-    }
-    for (int l = 0; l < 11; l++) W.layer_job[l][0] = W.layer_job[l][1] = -1;
-    // per-chunk cost = the busiest SIMD's MFMA tiles (waves w and w + 4 share SIMD w % 4) plus the
-    // per-chunk staging/barrier cost, floored; calibrated with tools/dw_phase.cpp (full 256 x 256
-    // tile 16 + 1.5 units ~ 18.9k cycles, narrow 6 + 1.5 ~ 8.3k, 32-row jobs ~ 4.2k)
-    double cost[MAXJ], total = 0;
-    for (int q = 0; q < nr; q++) {
-        const bool nar = raw[q].krows <= 128;
-        int simd[4] = {0, 0, 0, 0};
-        for (int w = 0; w < 8; w++) {
-            int tr, tc;
-            if (nar) {
-                tr = 32 * w < raw[q].nrows ? 1 : 0;
-                tc = min(4, div_up(raw[q].krows, 32));
-            } else {
-                tr = min(4, max(0, div_up(raw[q].nrows - 128 * (w >> 2), 32)));
-                tc = min(2, max(0, div_up(raw[q].krows - 64 * (w & 3), 32)));
-            }
-            simd[w & 3] += tr * tc;
-        }
-        int crit = max(max(simd[0], simd[1]), max(simd[2], simd[3]));
-        cost[q] = fmax(crit + 1.5, 4.0);
-        total += cost[q];
-    }
-    // splits: the smallest per-workgroup time T (in unit-chunks) whose ceil(cost * nch / T) fit the
-    // target grid (whole jobs never straddle: each workgroup runs per = ceil(nch / ns) chunks)
-    const int nch = 1 << 20;  // relative scale only (the chunk count cancels)
-    double T = total * nch / DW_TARGET_BLOCKS;
-    int nsq[MAXJ];
-    for (int it = 0; it < 400; it++, T *= 1.005) {
-        int sum = 0;
-        for (int q = 0; q < nr; q++) {
-            nsq[q] = max(1, (int)ceil(cost[q] * nch / T - 1e-9));
-            sum += nsq[q];
-        }
-        if (sum <= DW_TARGET_BLOCKS) break;
-    }
-    int b = 0;
-    for (int q = 0; q < nr; q++) {
-        const int ns = nsq[q];
-        W.jobs.j[q] = WJob{raw[q].zrow, raw[q].nrows, raw[q].xrow, raw[q].krows, ns, b, raw[q].krows <= 128 ? 1 : 0};
-        W.layer_job[raw[q].layer][raw[q].kt] = q;
-        b += ns;
-    }
-    W.jobs.n = nr;
-    W.nblocks = b;
-    return W;
-}
-
-}  // namespace mlp
-}  // namespace dgs
-
-using namespace dgs;
-using namespace dgs::mlp;
-
-#ifdef DGS_MLP_PROFILE
-extern "C" void dgs_mlp_set_prof(unsigned long long *p) {
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(dgs::mlp::dgs_mlp_prof), &p, sizeof(p));
-}
-#endif
-
-extern "C" int dgs_deform_outputs(int flags) { return make_flags(flags).nout; }
-extern "C" int dgs_deform_num_params(int flags) { return make_plan(flags).nparams; }
-extern "C" size_t dgs_deform_packed_floats(int flags) { return (size_t)make_plan(flags).total; }
 static size_t padded_points(int N) { return (size_t)div_up(N, BM) * BM; }
+
+size_t packed_floats(int flags) { return (size_t)make_plan(flags).total; }
 // saved activations [nsaved][Ns] floats, then the relu' bits [Ns / 32 blocks][nmask] u32 words, then
 // the frame-uniform timenet values (TC_FLOATS)
-extern "C" size_t dgs_deform_saved_floats(int flags, int N) {
+size_t saved_floats(int flags, int N) {
     const Flags F = make_flags(flags);
     return (size_t)F.nsaved * padded_points(N) + (size_t)F.nmask * (padded_points(N) / BM) + TC_FLOATS;
 }
 
-extern "C" size_t dgs_deform_scratch_floats(int flags, int N) {
+size_t scratch_floats(int flags, int N) {
     Flags F = make_flags(flags);
-    WPlan W = make_wplan(F);
+    WPlan W = fp32_wplan(F);
     return (size_t)F.nz * padded_points(N) + (size_t)W.nblocks * SLAB;
-}
-
-static int param_shape(const Plan &P, int idx, int &rows, int &cols) {
-    const Flags &F = P.F;
-    rows = cols = 0;
-    if (F.blender) {
-        if (idx == P.pT0w) { rows = 256; cols = F.tin; return 0; }
-        if (idx == P.pT0b) { rows = 256; return 0; }
-        if (idx == P.pT2w) { rows = 30; cols = 256; return 0; }
-        if (idx == P.pT2b) { rows = 30; return 0; }
-    }
-    const int te = F.blender ? 30 : F.tin;
-    for (int i = 0; i < 8; i++) {
-        if (idx == P.pLw[i]) { rows = 256; cols = i == 0 ? 63 + te : i == 5 ? 256 + 63 + te : 256; return 0; }
-        if (idx == P.pLb[i]) { rows = 256; return 0; }
-    }
-    for (int h = 0; h < P.nheads; h++) {
-        if (idx == P.pHw[h]) { rows = P.hrows[h]; cols = 256; return 0; }
-        if (idx == P.pHb[h]) { rows = P.hrows[h]; return 0; }
-    }
-    return -1;
 }
 
 // host emulation of the packed-image layout (forward A images, transposed backward images, biases)
@@ -1297,7 +1041,7 @@ static std::vector<int> build_pack_map(const Plan &P) {
     std::vector<int> map((size_t)P.total, -1);
     for (const PackJob &j : P.jobs) {
         int r, c;
-        param_shape(P, j.src, r, c);
+        param_shape(P.F, P, j.src, r, c);
         const bool head = (j.off == P.fHd || j.off == P.tHd);  // head images are shared by several jobs
         const int total = j.ntiles * j.nchunks * 256;
         for (int idx = 0; idx < total; idx++) {
@@ -1342,8 +1086,7 @@ static int *pack_map_for(const Plan &P, int flags) {
     return d;
 }
 
-extern "C" int dgs_deform_pack(int flags, const float *const *params, float *packed, void *stream_) {
-    hipStream_t stream = (hipStream_t)stream_;
+int pack(int flags, const float *const *params, float *packed, hipStream_t stream) {
     Plan P = make_plan(flags);
     if (P.nparams > PACK_MAXP) {
         set_error("dgs_deform_pack: too many parameters");
@@ -1367,9 +1110,8 @@ extern "C" int dgs_deform_pack(int flags, const float *const *params, float *pac
     return DGS_OK;
 }
 
-extern "C" int dgs_deform_forward(int flags, int N, const float *xyz, const float *t, const float *packed, float *out,
-                                  float *saved, void *stream_) {
-    hipStream_t stream = (hipStream_t)stream_;
+int forward(int flags, int N, const float *xyz, const float *t, const float *packed, float *out, float *saved,
+            hipStream_t stream) {
     if (N < 0 || (N > 0 && (!xyz || !t || !packed || !out))) {
         set_error("dgs_deform_forward: null argument");
         return DGS_ERR_ARGS;
@@ -1399,9 +1141,8 @@ extern "C" int dgs_deform_forward(int flags, int N, const float *xyz, const floa
     return DGS_OK;
 }
 
-extern "C" int dgs_deform_backward(int flags, int N, const float *packed, const float *saved, const float *dout,
-                                   float *scratch, float *const *grads, void *stream_) {
-    hipStream_t stream = (hipStream_t)stream_;
+int backward(int flags, int N, const float *packed, const float *saved, const float *dout, float *scratch,
+             float *const *grads, hipStream_t stream) {
     if (N < 0 || (N > 0 && (!packed || !saved || !dout || !scratch || !grads))) {
         set_error("dgs_deform_backward: null argument");
         return DGS_ERR_ARGS;
@@ -1411,7 +1152,7 @@ extern "C" int dgs_deform_backward(int flags, int N, const float *packed, const 
     if (N == 0) {
         for (int k = 0; k < P.nparams; k++) {
             int r, c;
-            param_shape(P, k, r, c);
+            param_shape(F, P, k, r, c);
             DGS_HIP_CHECK(hipMemsetAsync(grads[k], 0, sizeof(float) * r * (c ? c : 1), stream));
         }
         return DGS_OK;
@@ -1430,7 +1171,16 @@ extern "C" int dgs_deform_backward(int flags, int N, const float *packed, const 
         hipLaunchKernelGGL(k_mlp_bwd, dim3(div_up(N, BM)), dim3(NTHR), 0, stream, b);
     }
     DGS_LAUNCH_CHECK("k_mlp_bwd", false, stream);
-    WPlan W = make_wplan(F);
+    return dw_fp32(F, Ns, dz, saved, slabs, grads, stream);
+}
+
+// dW on fp32-input MFMA (k_dw) + the fixed-order slab reduction; shared with the split-bf16 path,
+// whose dZ / saved-activation arrays have the same [rows][Ns] layout (Ns a multiple of 32)
+size_t dw_fp32_slab_floats(int flags) { return (size_t)fp32_wplan(make_flags(flags)).nblocks * SLAB; }
+
+int dw_fp32(const Flags &F, size_t Ns, const float *dz, const float *saved, float *slabs, float *const *grads,
+            hipStream_t stream) {
+    WPlan W = fp32_wplan(F);
     {
         static bool attr_set = false;  // 147 KiB dynamic LDS
         const size_t lds_bytes = sizeof(float) * 2 * 2 * WT * LDA;
@@ -1442,13 +1192,20 @@ extern "C" int dgs_deform_backward(int flags, int N, const float *packed, const 
         hipLaunchKernelGGL(k_dw, dim3(W.nblocks), dim3(DW_THREADS), lds_bytes, stream, W.jobs, Ns, dz, saved, slabs);
     }
     DGS_LAUNCH_CHECK("k_dw", false, stream);
-    // one batched reduction launch into every parameter gradient
-    RJobs R{};
+    return launch_dw_reduce(F, W, slabs, grads, stream);
+}
+
+}  // namespace mlp
+
+namespace mlpc {
+int launch_dw_reduce(const Flags &F, const WPlan &W, const float *slabs, float *const *grads, hipStream_t stream) {
+    const Params P = make_params(F);
+    mlp::RJobs R{};
     int total = 0;
     auto add = [&](int pidx, int rowpad0, int ns, const Seg *sg, int layer, bool bias) {
         int r, c;
-        param_shape(P, pidx, r, c);
-        RJob &J = R.j[R.n];
+        param_shape(F, P, pidx, r, c);
+        mlp::RJob &J = R.j[R.n];
         J.dst = grads[pidx]; J.rows = r; J.cols = bias ? 0 : c; J.rowpad0 = rowpad0; J.nseg = ns;
         for (int q = 0; q < ns; q++) J.seg[q] = sg[q];
         for (int kt = 0; kt < 2; kt++) {
@@ -1485,8 +1242,16 @@ extern "C" int dgs_deform_backward(int flags, int N, const float *packed, const 
     R.begin[R.n] = total;
     {
         ScopedTimer tm("mlp_dw_reduce", stream);
-        hipLaunchKernelGGL(k_dw_reduce, dim3(div_up(total, 256)), dim3(256), 0, stream, R, slabs);
+        hipLaunchKernelGGL(mlp::k_dw_reduce, dim3(div_up(total, 256)), dim3(256), 0, stream, R, slabs);
     }
     DGS_LAUNCH_CHECK("k_dw_reduce", false, stream);
     return DGS_OK;
 }
+}  // namespace mlpc
+}  // namespace dgs
+
+#ifdef DGS_MLP_PROFILE
+extern "C" void dgs_mlp_set_prof(unsigned long long *p) {
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(dgs::mlp::dgs_mlp_prof), &p, sizeof(p));
+}
+#endif

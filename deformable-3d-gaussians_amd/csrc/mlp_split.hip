@@ -1,0 +1,1210 @@
+// Fused deformation MLP (positional encoding + timenet + 8x256 trunk with skip + heads) on bf16 MFMA
+// with an exact three-way operand split: the default path of dgs_deform_* (the fp32-MFMA kernels of
+// mlp.hip run instead under DGS_MLP_EXACT_FP32).
+//
+// Replaces DeformNetworkBaseline.forward and its autograd backward (utils/time_utils.py:56-127;
+// DeformNetwork :129-201 via DGS_MLP_NO_ROTSCALE; 6-DoF heads :114-121 emitted raw, exp_se3 stays in
+// the host glue).
+//
+// Numerics ("bf16x6"). Every fp32 operand x is split EXACTLY into three bf16 values
+//   hi = bf16(x), mid = bf16(x - hi), lo = x - hi - mid        (round to nearest)
+// (x - hi is exact in fp32 and has at most 16 significant bits, so lo has at most 8: x = hi+mid+lo,
+// |mid| <= 2^-8 |x|, |lo| <= 2^-16 |x|). A product a*b is accumulated as the six bf16 x bf16 products
+// hh + hm + mh + hl + lh + mm, each exact in the fp32 accumulator of v_mfma_f32_32x32x16_bf16; the
+// dropped ml + lm + ll are below 2^-23 |ab| (fp32's own rounding of a product is up to 2^-24 |ab|).
+// The GEMMs therefore keep fp32 accuracy (tests/test_gpu_mlp.py holds them to the same tolerances
+// as the exact-fp32 path) at 16/6 = 2.67x the fp32-MFMA rate (MI355X: bf16 MFMA = 16x f32 MFMA per
+// clock, MI355X_MICROARCH.md). Additions, biases, ReLU, PE and all reductions stay fp32.
+//
+// Layout ("transposed" formulation, Y^T = W X^T: features on MFMA rows, points on MFMA columns):
+//  * One workgroup = 64 points (two 32-point column tiles) x 16 waves (4 per SIMD): wave (w, ct)
+//    owns output rows 32w..32w+31 of every 256-wide layer for column tile ct; the two waves of an
+//    n-tile fetch the same weight fragments (L1-shared when they run close together).
+//  * Activations live in LDS split into hi/mid/lo bf16 images of 16-byte units (8 features x 1
+//    point), [8-feature group][split][64 points]: the B operand of a k-step (16 features) is one
+//    ds_read_b128 per split and column tile, and an accumulator's rows 8j + 4h + 0..3 are one 8-byte
+//    store per split into the next layer's image. XE | TE | H groups are contiguous, so
+//    cat(x_emb, t_emb) and cat(x_emb, t_emb, h) are plain group ranges (141 KB of LDS: one block per
+//    CU).
+//  * Weights are packed every call (they change every optimizer step) by one gather + split launch
+//    into A-fragment images [n-tile][k-step][split][64 lanes][8 bf16] (3 KiB per wave k-step).
+//  * Saved activations / dZ stay fp32 feature-major [rows][Ns] (mlp_shared.h row map), the dW
+//    GEMM splits them while staging its LDS tiles; relu' masks are 16-bit lane masks per 32x32 tile
+//    (same layout as the fp32 path). Every reduction is in a fixed order: bitwise deterministic.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <algorithm>
+#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <vector>
+
+#include "dgs_common.h"
+#include "mlp_shared.h"
+
+namespace dgs {
+namespace mlps {
+
+using namespace mlpc;
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BM = 64;            // points per workgroup
+constexpr int NT = 2;             // 32-point column tiles per workgroup
+constexpr int NWAVE = 16;         // 8 n-tiles x 2 column tiles
+constexpr int NTHR = NWAVE * 64;
+constexpr int NSPLIT = 3;         // hi, mid, lo
+constexpr int UG = NSPLIT * BM;   // 16-B units per 8-feature group (all splits, all points)
+constexpr int KSLOT = 3 * 64;     // units per (n-tile, k-step) of an A image: 3 splits x 64 lanes
+// forward LDS groups: XE (64 features) | TE (32) | H (256) | TIN (16)
+constexpr int G_XE = 0, G_TE = 8, G_H = 12, G_TIN = 44, G_FWD = 46;
+// backward LDS groups: H (dZ, 256) | G (dOut / dTE, 32)
+constexpr int G_BH = 0, G_BG = 32, G_BWD = 36;
+// fp32 staging rows (inside the H region): XE 0..63 | TE 64..95 | TIN 96..111
+constexpr int ST_TE = 64, ST_TIN = 96;
+
+static_assert(G_TE == G_XE + 8 && G_H == G_TE + 4, "XE|TE|H must be contiguous");
+static_assert(G_FWD * UG * 16 <= 160 * 1024 && G_BWD * UG * 16 <= 160 * 1024, "LDS");
+// PART (8 K-part slots x 32 rows x 64 points fp32) and the fp32 staging alias the H region
+constexpr int NPART = 8;
+static_assert(NPART * 32 * BM * 4 <= 32 * UG * 16, "PART must fit the H region");
+
+// ------------------------------------------------------------------------------------------------
+// exact three-way split
+// ------------------------------------------------------------------------------------------------
+struct Split4 {
+    bf16x4 h, m, l;
+};
+
+__device__ inline Split4 split4(float a, float b, float c, float d) {
+    Split4 s;
+    const float x[4] = {a, b, c, d};
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const __bf16 hb = (__bf16)x[j];
+        const float r = x[j] - (float)hb;
+        const __bf16 mb = (__bf16)r;
+        s.h[j] = hb;
+        s.m[j] = mb;
+        s.l[j] = (__bf16)(r - (float)mb);
+    }
+    return s;
+}
+
+// 8 consecutive features of one point -> the three 16-B units of group g (LDS image [g][split][BM])
+__device__ inline void put_unit8(bf16x8 *lds, int g, int m, const float (&v)[8]) {
+    const Split4 a = split4(v[0], v[1], v[2], v[3]);
+    const Split4 b = split4(v[4], v[5], v[6], v[7]);
+    bf16x8 *u = lds + g * UG + m;
+    u[0] = __builtin_shufflevector(a.h, b.h, 0, 1, 2, 3, 4, 5, 6, 7);
+    u[BM] = __builtin_shufflevector(a.m, b.m, 0, 1, 2, 3, 4, 5, 6, 7);
+    u[2 * BM] = __builtin_shufflevector(a.l, b.l, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// ------------------------------------------------------------------------------------------------
+// GEMM pieces: acc[ct] (32 rows of this wave x 32 points of column tile ct) += A . X
+// ------------------------------------------------------------------------------------------------
+#define MFMA16(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
+
+struct AFrag {  // one operand fragment in its three split parts
+    bf16x8 h, m, l;
+};
+
+__device__ inline AFrag load_a(const bf16x8 *p) { return AFrag{p[0], p[64], p[128]}; }
+
+// B fragment of column tile ct from the LDS image (p: this lane's unit of split 0, column tile 0)
+__device__ inline AFrag load_b(const bf16x8 *p, int ct) { return AFrag{p[32 * ct], p[BM + 32 * ct], p[2 * BM + 32 * ct]}; }
+
+// The six split products: hh into `hi`, the five corrections (mm, hl, lh, hm, mh: |.| <= 2^-8 |hh|)
+// into `lo`, summed in fp32 once at the end. An MFMA aligns its 16 products and C to the largest
+// term inside a limited window (tools/mfma_round_probe.hip: C = 1 plus 2^-30 minus 1 gives 0), so
+// corrections added into a running C of the hh magnitude would lose their low bits, with a slight
+// bias that long point sums (dW over 10^4-10^5 points) expose; in their own accumulator they keep
+// them. (Dependent 32x32x16 MFMAs issue back to back at full rate: MI355X_MICROARCH.md.)
+__device__ inline void mma6_2(const AFrag &a, const AFrag &b, f32x16 &hi, f32x16 &lo) {
+    lo = MFMA16(a.m, b.m, lo);
+    lo = MFMA16(a.h, b.l, lo);
+    lo = MFMA16(a.l, b.h, lo);
+    lo = MFMA16(a.h, b.m, lo);
+    lo = MFMA16(a.m, b.h, lo);
+    hi = MFMA16(a.h, b.h, hi);
+}
+
+// the six split products into one accumulator, smallest first
+__device__ inline void mma6_1(const AFrag &a, const AFrag &b, f32x16 &c) {
+    c = MFMA16(a.m, b.m, c);
+    c = MFMA16(a.h, b.l, c);
+    c = MFMA16(a.l, b.h, c);
+    c = MFMA16(a.h, b.m, c);
+    c = MFMA16(a.m, b.h, c);
+    c = MFMA16(a.h, b.h, c);
+}
+
+__device__ inline f32x16 zero16() {
+    f32x16 z;
+#pragma unroll
+    for (int i = 0; i < 16; i++) z[i] = 0.f;
+    return z;
+}
+
+#ifdef DGS_MLP_PROFILE  // diagnostic build only (tools/mlp_phase.py): per-phase s_memtime stamps
+__device__ unsigned long long *dgs_mlps_prof;
+#define DGS_STAMP(k)                                                                                   \
+    do {                                                                                               \
+        if (threadIdx.x == 0) dgs_mlps_prof[blockIdx.x * 64 + (k)] = __builtin_amdgcn_s_memtime();     \
+    } while (0)
+#else
+#define DGS_STAMP(k) \
+    do {             \
+    } while (0)
+#endif
+
+struct NoPre {
+    __device__ void operator()() const {}
+};
+struct NoStash {
+    __device__ void store(int) const {}
+};
+
+// The previous layer's output tile of this wave (16 values per lane), kept in registers and
+// written to a feature-major [rows][Ns] array during the first two k-steps of the next GEMM (8
+// coalesced stores per k-step, issued after that GEMM's prologue loads).
+struct Stash {
+    f32x16 t;
+    TileAddr d;
+    __device__ void store(int k) const {
+#pragma unroll
+        for (int j = 0; j < 8; j++) d.st(8 * k + j, t[8 * k + j]);
+    }
+    __device__ void store_all() const {
+        store(0);
+        store(1);
+    }
+};
+
+// acc += A . X over NK k-steps starting at k-step c0 of this wave's A image (Aw: unit pointer of
+// its n-tile at k-step 0) and of column tile ct of the LDS image at group g0 (k-step c = groups
+// g0 + 2c + h). Fully unrolled; per k-step: the six MFMAs (mma6_2), then the next k-step's B into
+// the same registers and the A fragment RING k-steps ahead (register ring; the A stream comes from
+// L2, 3 KiB per wave k-step), and the stash stores in k-steps 0-1 (sched_barrier keeps that order;
+// the three other waves of the SIMD cover the B reload latency). pre() runs after the A prologue.
+template <int NK, class Pre = NoPre, class St = NoStash>
+__device__ inline void gemm(const bf16x8 *__restrict__ Aw, int c0, const bf16x8 *lds, int g0, int ct, int lane,
+                            f32x16 &acc, Pre pre = Pre(), const St stash = St()) {
+    static_assert(NK >= 1, "empty GEMM");
+    const int h = lane >> 5, m = lane & 31;
+    const bf16x8 *Ap = Aw + c0 * KSLOT + lane;
+    const bf16x8 *Bp = lds + (g0 + 2 * c0 + h) * UG + 32 * ct + m;
+#ifdef DGS_DIAG_A_STATIC  // timing experiment only (wrong results): every k-step re-reads k-step 0's A
+    constexpr int AK = 0;
+#else
+    constexpr int AK = KSLOT;
+#endif
+#ifdef DGS_DIAG_B_STATIC  // timing experiment only (wrong results): every k-step re-reads k-step 0's B
+    constexpr int BK = 0;
+#else
+    constexpr int BK = 2 * UG;
+#endif
+    constexpr int RING = 2;
+    AFrag ring[RING];
+#pragma unroll
+    for (int k = 0; k < RING; k++)
+        if (k < NK) ring[k] = load_a(Ap + k * AK);
+    pre();
+    AFrag b = load_b(Bp, 0);
+    f32x16 lo = zero16();  // the correction products (mma6_2)
+#pragma unroll
+    for (int k = 0; k < NK; k++) {
+        __builtin_amdgcn_sched_barrier(0);
+        mma6_2(ring[k % RING], b, acc, lo);
+        if (k + 1 < NK) b = load_b(Bp + (k + 1) * BK, 0);  // B of the next k-step into the same registers
+        if (k + RING < NK) ring[k % RING] = load_a(Ap + (k + RING) * AK);
+        if (k < 2) stash.store(k);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int k = NK; k < 2; k++) stash.store(k);
+#pragma unroll
+    for (int i = 0; i < 16; i++) acc[i] += lo[i];
+}
+
+// accumulator tile ct (rows n0.. of this wave) -> split units of groups gbase + j (j < 4)
+__device__ inline void acc_to_lds(const f32x16 &acc, bf16x8 *lds, int gbase, int ct, int lane) {
+    const int h = lane >> 5, m = lane & 31;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const Split4 s = split4(acc[4 * j], acc[4 * j + 1], acc[4 * j + 2], acc[4 * j + 3]);
+        bf16x4 *u = reinterpret_cast<bf16x4 *>(lds + (gbase + j) * UG + 32 * ct + m) + h;
+        u[0] = s.h;
+        u[2 * BM] = s.m;  // bf16x4 units: one 16-B unit = 2 of them
+        u[4 * BM] = s.l;
+    }
+}
+
+// PART slot q (fp32 [32 rows][BM points]), column tile ct <- this wave's accumulator tile
+__device__ inline void acc_to_part(const f32x16 &acc, float *part, int q, int ct, int lane) {
+    const int h = lane >> 5, m = lane & 31;
+#pragma unroll
+    for (int r = 0; r < 16; r++) part[(q * 32 + TileAddr::row(r) + 4 * h) * BM + 32 * ct + m] = acc[r];
+}
+
+
+// bias of this lane's accumulator rows (n0 + 8j + 4h .. +3, j < 4), loaded ahead of the GEMM
+struct Bias4 {
+    float4 v[4];
+};
+
+__device__ inline Bias4 load_bias(const float *bias, int n0, int lane) {
+    const int h = lane >> 5;
+    Bias4 b;
+#pragma unroll
+    for (int j = 0; j < 4; j++) b.v[j] = *reinterpret_cast<const float4 *>(bias + n0 + 8 * j + 4 * h);
+    return b;
+}
+
+__device__ inline void bias_relu(f32x16 &acc, const Bias4 &b) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        acc[4 * j] = fmaxf(acc[4 * j] + b.v[j].x, 0.f);
+        acc[4 * j + 1] = fmaxf(acc[4 * j + 1] + b.v[j].y, 0.f);
+        acc[4 * j + 2] = fmaxf(acc[4 * j + 2] + b.v[j].z, 0.f);
+        acc[4 * j + 3] = fmaxf(acc[4 * j + 3] + b.v[j].w, 0.f);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// forward
+// ------------------------------------------------------------------------------------------------
+struct FwdArgs {
+    int N;
+    size_t Ns;
+    const float *xyz, *t;
+    const bf16x8 *img;  // A images
+    const float *fp;    // fp32 region: biases, timenet weights
+    float *out;
+    float *saved;
+    uint32_t *mask;     // relu' bits, [32-point tile][nmask] words (after the saved rows)
+    float *tc;          // timenet of t[0] (k_timenet), or nullptr
+    int fT1, fT2, fL[8], fHd;      // image k-slots
+    int bT1, bT2, bL[8], bHd;      // fp32 offsets
+    int wT1, wT2;                  // fp32 timenet weights [256][16], [32][256]
+    int flags;
+};
+
+// The reference feeds every Gaussian the same frame time (train_baseline.py:107-110), so the
+// timenet (time_utils.py:74-76, 13 -> 256 -> 30) has one value per launch: evaluated here once in
+// fp32 (one workgroup); a k_fwd block whose points all carry that t broadcasts TE / TH.
+__global__ __launch_bounds__(256) void k_timenet(FwdArgs a) {
+    __shared__ float tin[16], th[256];
+    const int j = threadIdx.x;
+    const float t0 = a.t[0];
+    if (j < 16) {
+        float v = 0.f;
+        if (j == 0) {
+            v = t0;
+        } else if (j < 13) {  // blender: t, sin / cos of 2^i t, i < 6
+            float sv, cv;
+            sincosf(t0 * (float)(1 << ((j - 1) >> 1)), &sv, &cv);
+            v = (j & 1) ? sv : cv;
+        }
+        tin[j] = v;
+        a.tc[TC_TIN + j] = v;
+    }
+    if (j == 0) a.tc[TC_T] = t0;
+    __syncthreads();
+    {
+        const float *w = a.fp + a.wT1 + j * 16;
+        float acc = a.fp[a.bT1 + j];
+#pragma unroll
+        for (int f = 0; f < 16; f++) acc = fmaf(w[f], tin[f], acc);
+        acc = fmaxf(acc, 0.f);
+        th[j] = acc;
+        a.tc[TC_TH + j] = acc;
+    }
+    __syncthreads();
+    {  // TE[k], k < 32 (rows 30, 31 are zero padding): 8 lanes per output, 32 features each
+        const int k = j >> 3, q = j & 7;
+        const float *w = a.fp + a.wT2 + k * 256 + 32 * q;
+        float acc = 0.f;
+#pragma unroll
+        for (int f = 0; f < 32; f++) acc = fmaf(w[f], th[32 * q + f], acc);
+        acc += __shfl_xor(acc, 1);
+        acc += __shfl_xor(acc, 2);
+        acc += __shfl_xor(acc, 4);
+        if (q == 0) a.tc[TC_TE + k] = acc + a.fp[a.bT2 + k];
+    }
+}
+
+template <bool SAVE>
+__global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
+    __shared__ bf16x8 lds[G_FWD * UG];
+    float *lf = reinterpret_cast<float *>(lds);
+    float *stage = lf + G_H * UG * 4;  // fp32 [112][BM] feature staging (H region, before the trunk)
+    float *part = stage;               // PART slots alias the H region too
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform
+    const int w = wave & 7, ct = wave >> 3;                      // n-tile, column tile
+    const int p0 = blockIdx.x * BM;
+    const Flags F = make_flags(a.flags);
+    const size_t Ns = a.Ns;
+    const __amdgpu_buffer_rsrc_t mrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        a.mask + (SAVE ? (size_t)(blockIdx.x * NT + ct) * F.nmask : 0), 0, 0x7fffffff, 0x00020000);
+    const int pw = p0 + 32 * ct;  // first point of this wave's column tile
+    DGS_STAMP(0);
+    // frame-uniform t: all 64 points of the block carry k_timenet's t0 (every wave checks the same
+    // 64 values, so the branch is block-uniform without a barrier)
+    bool uniform_t = false;
+    if (F.blender && a.tc) {
+        const float t0 = a.tc[TC_T];
+        const int p = p0 + lane;
+        const float tv = p < a.N ? a.t[p] : t0;
+        uniform_t = __ballot(tv != t0) == 0;
+    }
+    // ---- positional encodings (utils/time_utils.py:42-54) into fp32 staging: feature 3 band + d,
+    // band 0 = x, band 1 + 2i = sin(2^i x), band 2 + 2i = cos(2^i x) ----
+    for (int e = tid; e < BM * 3 * 11; e += NTHR) {
+        const int m = e % BM, r = e / BM, d = r % 3, i = r / 3;  // i = 10: identity band
+        const int p = p0 + m;
+        const bool ok = p < a.N;
+        const float x = ok ? a.xyz[3 * p + d] : 0.f;
+        if (i == 10) {
+            stage[d * BM + m] = x;
+        } else {
+            float sv, cv;
+            sincosf(x * (float)(1 << i), &sv, &cv);
+            stage[(3 * (1 + 2 * i) + d) * BM + m] = ok ? sv : 0.f;
+            stage[(3 * (2 + 2 * i) + d) * BM + m] = ok ? cv : 0.f;
+        }
+    }
+    if (tid < BM) stage[63 * BM + tid] = 0.f;  // padding feature
+    if (uniform_t) {  // TE and TIN: k_timenet's values broadcast over the points
+        for (int e = tid; e < 48 * BM; e += NTHR) {
+            const int f = e / BM, m = e % BM;
+            stage[(ST_TE + f) * BM + m] = f < 32 ? a.tc[TC_TE + f] : a.tc[TC_TIN + f - 32];
+        }
+    } else {  // per-point t encodings: TIN (blender, 16 rows) or the raw t PE as TE (32 rows)
+        const int row0 = F.blender ? ST_TIN : ST_TE, nrow = F.blender ? 16 : 32;
+        for (int e = tid; e < nrow * BM; e += NTHR) {
+            const int f = e / BM, m = e % BM;
+            const int p = p0 + m;
+            const float x = p < a.N ? a.t[p] : 0.f;
+            float v = 0.f;
+            if (p < a.N && f < F.tin) {
+                if (f == 0) {
+                    v = x;
+                } else {
+                    float sv, cv;
+                    sincosf(x * (float)(1 << ((f - 1) >> 1)), &sv, &cv);
+                    v = (f & 1) ? sv : cv;
+                }
+            }
+            stage[(row0 + f) * BM + m] = v;
+        }
+    }
+    __syncthreads();
+    // saved network inputs (fp32, coalesced) and their split LDS images
+    const bool te_ready = uniform_t || !F.blender;
+    if (SAVE) {
+        const int nrow = te_ready ? 96 : 64;  // XE | TE rows are adjacent in saved (S_TE = S_XE + 64)
+        for (int e = tid; e < nrow * BM; e += NTHR) {
+            const int f = e / BM, m = e % BM;
+            a.saved[(size_t)(S_XE + f) * Ns + p0 + m] = stage[f * BM + m];
+        }
+        if (F.blender)
+            for (int e = tid; e < 16 * BM; e += NTHR) {
+                const int f = e / BM, m = e % BM;
+                a.saved[(size_t)(S_TIN + f) * Ns + p0 + m] = stage[(ST_TIN + f) * BM + m];
+            }
+    }
+    {
+        const int ngrp = F.blender ? 14 : 12;  // staging groups: XE 0-7 | TE 8-11 | TIN 12-13
+        for (int u = tid; u < ngrp * BM; u += NTHR) {
+            const int g = u / BM, m = u % BM;
+            if (g >= G_TE && g < G_H && !te_ready) continue;  // TE comes from the per-point timenet
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) v[j] = stage[(8 * g + j) * BM + m];
+            put_unit8(lds, g < 12 ? g : G_TIN + g - 12, m, v);
+        }
+    }
+    lds_barrier();
+    DGS_STAMP(1);
+    f32x16 kt = zero16();  // previous layer's activations, awaiting their store
+    if (SAVE && uniform_t) {  // TH tile of this wave from k_timenet: relu' bits and the saved rows
+        const Bias4 th = load_bias(a.tc + TC_TH, w * 32, lane);
+        f32x16 c;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            c[4 * j] = th.v[j].x;
+            c[4 * j + 1] = th.v[j].y;
+            c[4 * j + 2] = th.v[j].z;
+            c[4 * j + 3] = th.v[j].w;
+        }
+        store_mask_bits(c, mrsrc, (M_TH + w * 32) * 4, lane);
+        Stash{c, tile_addr(a.saved, Ns, S_TH, w * 32, pw, lane)}.store_all();
+    }
+    // ---- per-point timenet (blender, t not frame-uniform): Linear(13,256)+ReLU -> H; Linear(256,30) -> TE
+    if (F.blender && !uniform_t) {
+        f32x16 c = zero16();
+        const Bias4 tb = load_bias(a.fp + a.bT1, w * 32, lane);
+        gemm<1>(a.img + (size_t)(a.fT1 + w) * KSLOT, 0, lds, G_TIN, ct, lane, c);
+        bias_relu(c, tb);
+        if (SAVE) store_mask_bits(c, mrsrc, (M_TH + w * 32) * 4, lane);
+        acc_to_lds(c, lds, G_H + 4 * w, ct, lane);
+        lds_barrier();
+        f32x16 c2 = zero16();
+        if (SAVE)
+            gemm<2>(a.img + (size_t)a.fT2 * KSLOT, 2 * w, lds, G_H, ct, lane, c2, NoPre(),
+                    Stash{c, tile_addr(a.saved, Ns, S_TH, w * 32, pw, lane)});
+        else
+            gemm<2>(a.img + (size_t)a.fT2 * KSLOT, 2 * w, lds, G_H, ct, lane, c2);
+        lds_barrier();  // every wave finished reading TH
+        acc_to_part(c2, part, w, ct, lane);
+        lds_barrier();
+        for (int u = tid; u < 4 * BM; u += NTHR) {  // TE = sum of the 8 K-parts + bias
+            const int g = u / BM, m = u % BM;
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const int row = 8 * g + j;
+                float s = part[row * BM + m];
+#pragma unroll
+                for (int q = 1; q < NPART; q++) s += part[(q * 32 + row) * BM + m];
+                v[j] = s + a.fp[a.bT2 + row];
+                if (SAVE) a.saved[(size_t)(S_TE + row) * Ns + p0 + m] = v[j];
+            }
+            put_unit8(lds, G_TE + g, m, v);
+        }
+        lds_barrier();
+    }
+    // ---- trunk: 8 x (Linear + ReLU), skip cat after layer 4 (time_utils.py:107-112) ----
+#pragma unroll 1
+    for (int L = 0; L < 8; L++) {
+        const int g0 = (L == 0 || L == 5) ? G_XE : G_H;
+        const int nk = layer_kpad(L) / 16;
+        f32x16 c = zero16();
+        const bf16x8 *Aw = a.img + (size_t)(a.fL[L] + w * nk) * KSLOT;
+        if (L == 0) {
+            gemm<6>(Aw, 0, lds, g0, ct, lane, c);
+        } else {
+            const Stash st{kt, tile_addr(a.saved, Ns, s_h(L - 1), w * 32, pw, lane)};
+            if (L == 5) {
+                if (SAVE) gemm<22>(Aw, 0, lds, g0, ct, lane, c, NoPre(), st);
+                else gemm<22>(Aw, 0, lds, g0, ct, lane, c);
+            } else {
+                if (SAVE) gemm<16>(Aw, 0, lds, g0, ct, lane, c, NoPre(), st);
+                else gemm<16>(Aw, 0, lds, g0, ct, lane, c);
+            }
+        }
+        DGS_STAMP(4 + 2 * L);
+        const Bias4 bv = load_bias(a.fp + a.bL[L], w * 32, lane);  // in flight across the barrier
+        lds_barrier();  // all waves finished reading H before it is overwritten
+#ifndef DGS_DIAG_NO_EPI  // timing experiment only (wrong results): no bias/relu/mask/split epilogue
+        bias_relu(c, bv);
+        if (SAVE) store_mask_bits(c, mrsrc, (m_h(L) + w * 32) * 4, lane);
+        acc_to_lds(c, lds, G_H + 4 * w, ct, lane);
+#endif
+        lds_barrier();
+        DGS_STAMP(5 + 2 * L);
+        kt = c;
+    }
+    // ---- heads (no activation): [warp | branch_w, branch_v], rotation, scaling; K split over waves ----
+    {
+        f32x16 c = zero16();
+        if (SAVE)
+            gemm<2>(a.img + (size_t)a.fHd * KSLOT, 2 * w, lds, G_H, ct, lane, c, NoPre(),
+                    Stash{kt, tile_addr(a.saved, Ns, s_h(7), w * 32, pw, lane)});
+        else
+            gemm<2>(a.img + (size_t)a.fHd * KSLOT, 2 * w, lds, G_H, ct, lane, c);
+        lds_barrier();
+        acc_to_part(c, part, w, ct, lane);
+        lds_barrier();
+    }
+    DGS_STAMP(20);
+    for (int e = tid; e < F.nout * BM; e += NTHR) {
+        const int cc = e % F.nout, m = e / F.nout;
+        const int p = p0 + m;
+        float s = part[cc * BM + m];
+#pragma unroll
+        for (int q = 1; q < NPART; q++) s += part[(q * 32 + cc) * BM + m];
+        if (p < a.N) a.out[(size_t)p * F.nout + cc] = s + a.fp[a.bHd + cc];
+    }
+    DGS_STAMP(21);
+#ifdef DGS_MLP_PROFILE
+    if (threadIdx.x == 0) {  // shader-clock rate: s_memtime vs the 100 MHz s_memrealtime
+        dgs_mlps_prof[blockIdx.x * 64 + 60] = __builtin_amdgcn_s_memrealtime();
+        dgs_mlps_prof[blockIdx.x * 64 + 61] = __builtin_amdgcn_s_memtime();
+        dgs_mlps_prof[blockIdx.x * 64 + 62] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));  // HW_ID-ish
+    }
+#endif
+}
+
+// ------------------------------------------------------------------------------------------------
+// backward (dX chain): dZ_i for every layer -> scratch; deterministic
+// ------------------------------------------------------------------------------------------------
+struct BwdArgs {
+    int N;
+    size_t Ns;
+    const bf16x8 *img;
+    const uint32_t *mask;
+    const float *dout;
+    float *dz;
+    int tHd, tL[8], tT2;  // image k-slots
+    int flags;
+};
+
+// relu' bits of the layer input for this wave's 32x32 tile, loaded ahead of the GEMM
+struct MaskPre {
+    uint32_t *mk;
+    const uint32_t *words;  // &mask[32-point tile][mrow0 + n0]
+    int lane;
+    __device__ void operator()() const { *mk = reinterpret_cast<const unsigned short *>(words)[lane]; }
+};
+
+__global__ __launch_bounds__(NTHR) void k_bwd(BwdArgs a) {
+    __shared__ bf16x8 lds[G_BWD * UG];
+    float *lf = reinterpret_cast<float *>(lds);
+    float *stage = lf + G_BH * UG * 4;  // fp32 [32][BM] (H region, before the first dZ)
+    float *part = stage;                // PART slots alias the H region (layer 0 only)
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int w = wave & 7, ct = wave >> 3;  // n-tile, column tile
+    const int p0 = blockIdx.x * BM, pw = p0 + 32 * ct;
+    const Flags F = make_flags(a.flags);
+    const size_t Ns = a.Ns;
+    const uint32_t *mwords = a.mask + (size_t)(blockIdx.x * NT + ct) * F.nmask + w * 32;  // + mask row
+    // dOut -> dz rows Z_G (heads' dW) and the split G image
+    for (int e = tid; e < 32 * BM; e += NTHR) {
+        const int c = e / BM, m = e % BM;
+        const int p = p0 + m;
+        const float v = (p < a.N && c < F.nout) ? a.dout[(size_t)p * F.nout + c] : 0.f;
+        a.dz[(size_t)(Z_G + c) * Ns + p] = v;
+        stage[c * BM + m] = v;
+    }
+    __syncthreads();
+    if (tid < 4 * BM) {
+        const int g = tid / BM, m = tid % BM;
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = stage[(8 * g + j) * BM + m];
+        put_unit8(lds, G_BG + g, m, v);
+    }
+    lds_barrier();
+    f32x16 kt;  // dZ of the layer whose GEMM runs next
+    // heads^T: dH7 = W_h^T dOut (K = 32 from G) -> mask H7 -> dZ7
+    {
+        uint32_t mk;
+        f32x16 c = zero16();
+        gemm<2>(a.img + (size_t)(a.tHd + w * 2) * KSLOT, 0, lds, G_BG, ct, lane, c, MaskPre{&mk, mwords + m_h(7), lane});
+        mask_apply(c, mk);
+        acc_to_lds(c, lds, G_BH + 4 * w, ct, lane);
+        kt = c;
+        lds_barrier();
+    }
+    f32x16 ct_te = zero16();  // dL/dt_emb partial (blender): this wave's K-part of layers 5 and 0
+#pragma unroll 1
+    for (int L = 7; L >= 1; L--) {
+        // dX_L = W_L^T dZ_L; the H-part rows of the padded L5 input are n-tiles F_H/32 + w
+        const int tile0 = (L == 5) ? F_H / 32 : 0;
+        if (L == 5 && F.blender)  // t_emb rows (padded 64..95 = n-tile 2), K split over the n-tile waves
+            gemm<2>(a.img + (size_t)(a.tL[5] + (F_TE / 32) * 16) * KSLOT, 2 * w, lds, G_BH, ct, lane, ct_te);
+        uint32_t mk;
+        f32x16 c = zero16();
+        gemm<16>(a.img + (size_t)(a.tL[L] + (tile0 + w) * 16) * KSLOT, 0, lds, G_BH, ct, lane, c,
+                 MaskPre{&mk, mwords + m_h(L - 1), lane}, Stash{kt, tile_addr(a.dz, Ns, Z_L0 + L * 256, w * 32, pw, lane)});
+        lds_barrier();
+        mask_apply(c, mk);
+        acc_to_lds(c, lds, G_BH + 4 * w, ct, lane);
+        kt = c;
+        lds_barrier();
+    }
+    const Stash dz0{kt, tile_addr(a.dz, Ns, Z_L0, w * 32, pw, lane)};
+    if (!F.blender) {
+        dz0.store_all();
+        return;  // raw t PE has no parameters upstream of it
+    }
+    // layer 0: t_emb rows of W_0^T dZ_0 (K split), dZ_0 stored under it; then sum the K-parts
+    gemm<2>(a.img + (size_t)(a.tL[0] + (F_TE / 32) * 16) * KSLOT, 2 * w, lds, G_BH, ct, lane, ct_te, NoPre(), dz0);
+    lds_barrier();
+    acc_to_part(ct_te, part, w, ct, lane);
+    lds_barrier();
+    if (tid < 4 * BM) {  // dTE (30 real rows) -> dz rows Z_TE (timenet.2's dW) and the split G image
+        const int g = tid / BM, m = tid % BM;
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int row = 8 * g + j;
+            float s = part[row * BM + m];
+#pragma unroll
+            for (int q = 1; q < NPART; q++) s += part[(q * 32 + row) * BM + m];
+            v[j] = s;
+            a.dz[(size_t)(Z_TE + row) * Ns + p0 + m] = s;
+        }
+        put_unit8(lds, G_BG + g, m, v);
+    }
+    lds_barrier();
+    // timenet.2^T: dTH = W_T2^T dTE (K = 32) -> mask TH -> dZ_T1
+    {
+        uint32_t mk;
+        f32x16 c = zero16();
+        gemm<2>(a.img + (size_t)(a.tT2 + w * 2) * KSLOT, 0, lds, G_BG, ct, lane, c, MaskPre{&mk, mwords + M_TH, lane});
+        mask_apply(c, mk);
+        Stash{c, tile_addr(a.dz, Ns, Z_T1, w * 32, pw, lane)}.store_all();
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// dW = dZ X^T over all points (split-N): operands staged fp32 -> split bf16 planes in LDS, 16 points
+// (one bf16 k-step) per chunk, double-buffered; per-workgroup slabs reduced by k_dw_reduce (mlp.hip)
+// ------------------------------------------------------------------------------------------------
+constexpr int PC = 16;                 // points per chunk = one k-step
+constexpr int PITCH = 24;              // bf16 per LDS row: 16 + 8 pad (48 B: conflict-free b128 reads)
+constexpr int PLANE = WT * PITCH;      // bf16 per split plane
+constexpr int OPND = NSPLIT * PLANE;   // bf16 per operand
+constexpr int DW_LDS = 2 * 2 * OPND * 2;  // bytes: 2 buffers x (A, B)
+constexpr int DW_THREADS = 512;
+static_assert(DW_LDS <= 160 * 1024, "dW LDS");
+
+__device__ inline AFrag load_plane_frag(const __bf16 *op, int row, int h) {
+    const __bf16 *p = op + row * PITCH + 8 * h;
+    return AFrag{*reinterpret_cast<const bf16x8 *>(p), *reinterpret_cast<const bf16x8 *>(p + PLANE),
+                 *reinterpret_cast<const bf16x8 *>(p + 2 * PLANE)};
+}
+
+// one float4 (row, 4 points) -> the three planes
+__device__ inline void stage_split(__bf16 *op, int row, int col4, float4 v) {
+    const Split4 s = split4(v.x, v.y, v.z, v.w);
+    bf16x4 *p = reinterpret_cast<bf16x4 *>(op + row * PITCH + 4 * col4);
+    p[0] = s.h;
+    p[PLANE / 4] = s.m;
+    p[2 * PLANE / 4] = s.l;
+}
+
+__device__ inline float4 zsel4(float4 v, bool ok) {
+    return make_float4(ok ? v.x : 0.f, ok ? v.y : 0.f, ok ? v.z : 0.f, ok ? v.w : 0.f);
+}
+
+template <bool NARROW>
+__device__ __forceinline__ void dw_tile(const WJob &J, size_t Ns, const float *__restrict__ dz,
+                                        const float *__restrict__ saved, float *__restrict__ slabs, __bf16 *lds) {
+    const int split = blockIdx.x - J.block0;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wn = wave >> 2, wk = wave & 3;  // wide wave tile: rows [128 wn, +128), cols [64 wk, +64)
+    const int h = lane >> 5, i = lane & 31;
+    const int nch = (int)(Ns / PC);
+    const int per = div_up(nch, J.nsplit);
+    const int c0 = split * per;
+    const int c1 = min(nch, c0 + per);
+    // staging: float4 q = tid + 512 j (j < 2): row = q / 4 (0..255), points 4 (q % 4) .. +3
+    const int srow = tid >> 2, scol = tid & 3;
+    const float *baseA = dz + (size_t)J.zrow * Ns;
+    const float *baseB = saved + (size_t)J.xrow * Ns;
+    const bool okA0 = srow < J.nrows, okA1 = srow + 128 < J.nrows;
+    const bool okB0 = srow < J.krows, okB1 = srow + 128 < J.krows;
+    // 32-bit byte offsets from a uniform base; rows past the extent load row 0 (always valid) and are
+    // zeroed at the LDS store, so the loads stay in flight across the chunk's MFMAs
+    const uint32_t ns = (uint32_t)Ns;
+    const uint32_t uA0 = ((okA0 ? srow : 0) * ns + 4 * scol) * 4, uA1 = ((okA1 ? srow + 128 : 0) * ns + 4 * scol) * 4;
+    const uint32_t uB0 = ((okB0 ? srow : 0) * ns + 4 * scol) * 4, uB1 = ((okB1 ? srow + 128 : 0) * ns + 4 * scol) * 4;
+#define DW_LD(base, u, c) \
+    (*reinterpret_cast<const float4 *>(reinterpret_cast<const char *>(base) + (uint32_t)((u) + (uint32_t)(c) * (PC * 4u))))
+    struct Stage {
+        float4 a0, a1, b0, b1;
+    };
+    float bs0 = 0.f, bs1 = 0.f;  // bias row sums of the staged dZ rows
+    auto gload = [&](Stage &r, int c) {
+        r.a0 = DW_LD(baseA, uA0, c);
+        r.a1 = DW_LD(baseA, uA1, c);
+        r.b0 = DW_LD(baseB, uB0, c);
+        r.b1 = DW_LD(baseB, uB1, c);
+    };
+    auto lstore = [&](const Stage &r, int buf) {
+        __bf16 *A = lds + buf * 2 * OPND;
+        __bf16 *B = A + OPND;
+        const float4 a0 = zsel4(r.a0, okA0), a1 = zsel4(r.a1, okA1);
+        bs0 += (a0.x + a0.y) + (a0.z + a0.w);
+        bs1 += (a1.x + a1.y) + (a1.z + a1.w);
+        stage_split(A, srow, scol, a0);
+        stage_split(A, srow + 128, scol, a1);
+        stage_split(B, srow, scol, zsel4(r.b0, okB0));
+        stage_split(B, srow + 128, scol, zsel4(r.b1, okB1));
+    };
+#undef DW_LD
+    // this wave's active sub-tiles (wave-uniform). wide: rows 128 wn + 32 t, cols 64 wk + 32 u
+    // (acc[t][u]); narrow: rows 32 wave, cols 32 v (acc[v >> 1][v & 1], v < 4)
+    const int nact_r = NARROW ? (32 * wave < J.nrows ? 1 : 0) : min(4, max(0, div_up(J.nrows - 128 * wn, 32)));
+    const int nact_c = NARROW ? min(4, div_up(J.krows, 32)) : min(2, max(0, div_up(J.krows - 64 * wk, 32)));
+    const bool any = nact_r > 0 && nact_c > 0;
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+#pragma unroll
+        for (int u = 0; u < 2; u++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[t][u][r] = 0.f;
+    auto compute = [&](int buf) {
+        const __bf16 *A = lds + buf * 2 * OPND;
+        const __bf16 *B = A + OPND;
+        if (any && NARROW) {
+            const AFrag a0 = load_plane_frag(A, 32 * wave + i, h);
+#pragma unroll
+            for (int v = 0; v < 4; v++) {
+                if (v >= nact_c) continue;
+                const AFrag b = load_plane_frag(B, 32 * v + i, h);
+                mma6_1(a0, b, acc[v >> 1][v & 1]);
+            }
+        } else if (any) {
+            AFrag bb[2];
+#pragma unroll
+            for (int u = 0; u < 2; u++) bb[u] = load_plane_frag(B, 64 * wk + 32 * u + i, h);
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                if (t >= nact_r) continue;
+                const AFrag at = load_plane_frag(A, 128 * wn + 32 * t + i, h);
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    if (u >= nact_c) continue;
+                    mma6_1(at, bb[u], acc[t][u]);
+                }
+            }
+        }
+    };
+    // Pipeline: LDS buffers alternate per chunk; two register stages keep the global loads two chunks
+    // ahead. Barriers wait for LDS only (lds_barrier): a __syncthreads() would also drain the
+    // prefetched global loads (vmcnt 0) every 48 MFMAs.
+    Stage R0, R1;
+    if (c0 < c1) gload(R0, c0);
+    if (c0 + 1 < c1) gload(R1, c0 + 1);
+    if (c0 < c1) lstore(R0, 0);
+    if (c0 + 2 < c1) gload(R0, c0 + 2);
+    lds_barrier();
+    for (int c = c0; c < c1; c += 2) {
+        // buffer 0 holds chunk c, R1 chunk c + 1, R0 chunk c + 2 (in flight)
+        compute(0);
+        if (c + 1 < c1) lstore(R1, 1);
+        if (c + 3 < c1) gload(R1, c + 3);
+        lds_barrier();
+        if (c + 1 >= c1) break;
+        compute(1);
+        if (c + 2 < c1) lstore(R0, 0);
+        if (c + 4 < c1) gload(R0, c + 4);
+        lds_barrier();
+    }
+    float *slab = slabs + (size_t)blockIdx.x * SLAB;
+    // bias row sums: the 4 lanes staging a row hold its partial sums (fixed xor-tree order)
+    bs0 += __shfl_xor(bs0, 1);
+    bs0 += __shfl_xor(bs0, 2);
+    bs1 += __shfl_xor(bs1, 1);
+    bs1 += __shfl_xor(bs1, 2);
+    if (scol == 0) {
+        slab[WT * WT + srow] = bs0;
+        slab[WT * WT + srow + 128] = bs1;
+    }
+    // rows past nrows / cols past krows hold zeros or partial garbage that k_dw_reduce never reads
+    if (NARROW) {
+#pragma unroll
+        for (int v = 0; v < 4; v++) {
+            const int nb = 32 * wave, kb = 32 * v;
+#pragma unroll
+            for (int r = 0; r < 16; r++) slab[(nb + TileAddr::row(r) + 4 * h) * WT + kb + i] = acc[v >> 1][v & 1][r];
+        }
+        return;
+    }
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int nb = 128 * wn + 32 * t, kb = 64 * wk + 32 * u;
+#pragma unroll
+            for (int r = 0; r < 16; r++) slab[(nb + TileAddr::row(r) + 4 * h) * WT + kb + i] = acc[t][u][r];
+        }
+}
+
+__global__ __launch_bounds__(DW_THREADS) void k_dw(WJobs JT, size_t Ns, const float *__restrict__ dz,
+                                                   const float *__restrict__ saved, float *__restrict__ slabs) {
+    extern __shared__ bf16x8 dw_lds[];
+    // job of this workgroup: static-index selects over the kernel-argument table (no scratch copy)
+    WJob J = JT.j[0];
+#pragma unroll
+    for (int q = 1; q < MAXJ; q++)
+        if (q < JT.n && (int)blockIdx.x >= JT.j[q].block0) J = JT.j[q];
+    // the two wave layouts are separate code regions (one loop with a runtime switch spills)
+    if (J.narrow)
+        dw_tile<true>(J, Ns, dz, saved, slabs, reinterpret_cast<__bf16 *>(dw_lds));
+    else
+        dw_tile<false>(J, Ns, dz, saved, slabs, reinterpret_cast<__bf16 *>(dw_lds));
+}
+
+// ------------------------------------------------------------------------------------------------
+// packing plan (host)
+// ------------------------------------------------------------------------------------------------
+struct Img {           // one A-operand image: ntiles x nk k-slots
+    int src;           // parameter index (weight)
+    int transpose;     // 0: A[n][f] = W[n][f]; 1: A[n][f] = W[f][n]
+    int ntiles, nk;
+    int nseg_n, nseg_f;
+    Seg segn[3], segf[3];
+    int slot;          // first k-slot
+};
+struct F32Job {        // fp32 region entry: dst[r * cpad + c] = W[sr][sc] (bias: cpad = 1)
+    int src;
+    int rpad, cpad;
+    int nseg_r, nseg_c;
+    Seg segr[3], segc[3];
+    int off;
+};
+
+struct Plan : Params {
+    Flags F;
+    std::vector<Img> imgs;
+    std::vector<F32Job> f32;
+    int fT1 = -1, fT2 = -1, fL[8], fHd, tHd, tL[8], tT2 = -1;  // k-slots
+    int bT1 = -1, bT2 = -1, bL[8], bHd, wT1 = -1, wT2 = -1;     // fp32 offsets
+    int nslots = 0, nf32 = 0;
+    size_t img_floats() const { return (size_t)nslots * KSLOT * 4; }  // 16-B unit = 4 floats
+    size_t total() const { return img_floats() + nf32; }
+};
+
+Plan make_plan(int flags) {
+    Plan P;
+    P.F = make_flags(flags);
+    const Flags &F = P.F;
+    static_cast<Params &>(P) = make_params(F);
+    auto img = [&](int src, int tr, int ntiles, int nk, int nsn, const Seg *sn, int nsf, const Seg *sf, int slot) {
+        Img j{};
+        j.src = src; j.transpose = tr; j.ntiles = ntiles; j.nk = nk; j.nseg_n = nsn; j.nseg_f = nsf;
+        for (int q = 0; q < nsn; q++) j.segn[q] = sn[q];
+        for (int q = 0; q < nsf; q++) j.segf[q] = sf[q];
+        j.slot = slot;
+        P.imgs.push_back(j);
+    };
+    auto new_img = [&](int src, int tr, int ntiles, int nk, int nsn, const Seg *sn, int nsf, const Seg *sf) {
+        const int slot = P.nslots;
+        img(src, tr, ntiles, nk, nsn, sn, nsf, sf, slot);
+        P.nslots += ntiles * nk;
+        return slot;
+    };
+    auto f32 = [&](int src, int rpad, int cpad, int nsr, const Seg *sr, int nsc, const Seg *sc, int off) {
+        F32Job j{};
+        j.src = src; j.rpad = rpad; j.cpad = cpad; j.nseg_r = nsr; j.nseg_c = nsc;
+        for (int q = 0; q < nsr; q++) j.segr[q] = sr[q];
+        for (int q = 0; q < nsc; q++) j.segc[q] = sc[q];
+        j.off = off;
+        P.f32.push_back(j);
+    };
+    auto new_f32 = [&](int src, int rpad, int cpad, int nsr, const Seg *sr, int nsc, const Seg *sc) {
+        const int off = P.nf32;
+        f32(src, rpad, cpad, nsr, sr, nsc, sc, off);
+        P.nf32 += rpad * cpad;
+        return off;
+    };
+    const Seg full = seg(0, 256, 0), one = seg(0, 1, 0);
+    if (F.blender) {
+        const Seg st = seg(0, F.tin, 0), s30 = seg(0, 30, 0);
+        P.fT1 = new_img(P.pT0w, 0, 8, 1, 1, &full, 1, &st);
+        P.fT2 = new_img(P.pT2w, 0, 1, 16, 1, &s30, 1, &full);
+        P.tT2 = new_img(P.pT2w, 1, 8, 2, 1, &full, 1, &s30);  // A[n = TH feature][f = TE feature]
+        P.bT1 = new_f32(P.pT0b, 256, 1, 1, &full, 1, &one);
+        P.bT2 = new_f32(P.pT2b, 32, 1, 1, &s30, 1, &one);
+        P.wT1 = new_f32(P.pT0w, 256, 16, 1, &full, 1, &st);
+        P.wT2 = new_f32(P.pT2w, 32, 256, 1, &s30, 1, &full);
+    }
+    for (int i = 0; i < 8; i++) {
+        Seg s[3];
+        const int ns = layer_in_segs(F, i, s);
+        const int kp = layer_kpad(i);
+        P.fL[i] = new_img(P.pLw[i], 0, 8, kp / 16, 1, &full, ns, s);
+        P.tL[i] = new_img(P.pLw[i], 1, kp / 32, 16, ns, s, 1, &full);  // rows = padded input features
+        P.bL[i] = new_f32(P.pLb[i], 256, 1, 1, &full, 1, &one);
+    }
+    // heads: rows stacked in output order in one 32-row image each way
+    P.fHd = P.nslots;
+    P.nslots += 16;
+    P.tHd = P.nslots;
+    P.nslots += 16;  // 8 n-tiles x 2 k-steps
+    P.bHd = P.nf32;
+    P.nf32 += 32;
+    int r0 = 0;
+    for (int h = 0; h < P.nheads; h++) {
+        const Seg sr = seg(r0, P.hrows[h], 0);
+        img(P.pHw[h], 0, 1, 16, 1, &sr, 1, &full, P.fHd);
+        img(P.pHw[h], 1, 8, 2, 1, &full, 1, &sr, P.tHd);
+        f32(P.pHb[h], 32, 1, 1, &sr, 1, &one, P.bHd);
+        r0 += P.hrows[h];
+    }
+    P.nf32 = (P.nf32 + 3) & ~3;
+    return P;
+}
+
+// Packing is one gather + split launch over map[i] = (parameter << 22) | element, or -1 for zero
+// padding: i < nslots * 512 are the A-image elements in [k-slot][lane][8] order (each split into
+// three bf16 planes of its k-slot), the rest the fp32 region. The map depends only on the flags
+// (built once on the host, cached on the device).
+constexpr int PACK_MAXP = 32;
+constexpr int PACK_SHIFT = 22;
+struct PackPtrs {
+    const float *p[PACK_MAXP];
+};
+
+__global__ __launch_bounds__(256) void k_pack(const int *__restrict__ map, PackPtrs src, __bf16 *__restrict__ img,
+                                              float *__restrict__ fp, int nimg, int total) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int c = map[i];
+    const float v = c < 0 ? 0.f : src.p[c >> PACK_SHIFT][c & ((1 << PACK_SHIFT) - 1)];
+    if (i < nimg) {
+        const __bf16 hb = (__bf16)v;
+        const float r = v - (float)hb;
+        const __bf16 mb = (__bf16)r;
+        __bf16 *d = img + (size_t)(i >> 9) * 1536 + (i & 511);  // k-slot: 3 planes of 512 bf16
+        d[0] = hb;
+        d[512] = mb;
+        d[1024] = (__bf16)(r - (float)mb);
+    } else {
+        fp[i - nimg] = v;
+    }
+}
+
+static std::vector<int> build_pack_map(const Plan &P) {
+    const size_t nimg = (size_t)P.nslots * 512;
+    std::vector<int> map(nimg + P.nf32, -1);
+    for (const Img &j : P.imgs) {
+        int r, c;
+        param_shape(P.F, P, j.src, r, c);
+        for (int idx = 0; idx < j.ntiles * j.nk * 512; idx++) {
+            const int e = idx & 7, lane = (idx >> 3) & 63, slot = idx >> 9;
+            const int k = slot % j.nk, ntile = slot / j.nk;
+            const int n = ntile * 32 + (lane & 31);
+            const int f = 16 * k + 8 * (lane >> 5) + e;
+            const int sn = seg_lookup(j.segn, j.nseg_n, n);
+            const int sf = seg_lookup(j.segf, j.nseg_f, f);
+            if (sn >= 0 && sf >= 0)
+                map[(size_t)j.slot * 512 + idx] = (j.src << PACK_SHIFT) | (j.transpose ? sf * c + sn : sn * c + sf);
+        }
+    }
+    for (const F32Job &j : P.f32) {
+        int r, c;
+        param_shape(P.F, P, j.src, r, c);
+        for (int rr = 0; rr < j.rpad; rr++)
+            for (int cc = 0; cc < j.cpad; cc++) {
+                const int sr = seg_lookup(j.segr, j.nseg_r, rr), sc = seg_lookup(j.segc, j.nseg_c, cc);
+                if (sr >= 0 && sc >= 0) map[nimg + j.off + rr * j.cpad + cc] = (j.src << PACK_SHIFT) | (c ? sr * c + sc : sr);
+            }
+    }
+    return map;
+}
+
+static std::mutex g_map_mu;
+static std::map<std::pair<int, int>, int *> g_pack_maps;  // (device, flags) -> device map
+
+static int *pack_map_for(const Plan &P, int flags) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(g_map_mu);
+    auto it = g_pack_maps.find({dev, flags});
+    if (it != g_pack_maps.end()) return it->second;
+    std::vector<int> h = build_pack_map(P);
+    int *d = nullptr;
+    if (hipMalloc(&d, h.size() * sizeof(int)) != hipSuccess) return nullptr;
+    if (hipMemcpy(d, h.data(), h.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(d);
+        return nullptr;
+    }
+    g_pack_maps[{dev, flags}] = d;
+    return d;
+}
+
+// dW split plan: one 8-wave workgroup per CU (LDS 144 KiB); per-chunk cost in MFMA tiles + staging
+static WPlan split_wplan(const Flags &F) { return make_wplan(F, 256, 1.5, 4.0); }
+
+static size_t padded_points(int N) { return (size_t)div_up(N, BM) * BM; }
+
+size_t saved_floats(int flags, int N) {
+    const Flags F = make_flags(flags);
+    const size_t Ns = padded_points(N);
+    return (size_t)F.nsaved * Ns + (size_t)F.nmask * (Ns / 32) + TC_FLOATS;
+}
+
+// dW arithmetic: the split-bf16 k_dw above, or (default) the fp32-input MFMA k_dw of mlp.hip on the
+// same [rows][Ns] arrays (DGS_MLP_SPLIT_DW=1 selects the split one)
+static bool split_dw() {
+    static const bool on = [] {
+        const char *e = getenv("DGS_MLP_SPLIT_DW");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
+size_t scratch_floats(int flags, int N) {
+    const Flags F = make_flags(flags);
+    const size_t slabs = std::max((size_t)split_wplan(F).nblocks * SLAB, mlp::dw_fp32_slab_floats(flags));
+    return (size_t)F.nz * padded_points(N) + slabs;
+}
+
+int pack(int flags, const float *const *params, float *packed, hipStream_t stream) {
+    const Plan P = make_plan(flags);
+    if (P.nparams > PACK_MAXP) {
+        set_error("dgs_deform_pack: too many parameters");
+        return DGS_ERR_ARGS;
+    }
+    PackPtrs src{};
+    for (int k = 0; k < P.nparams; k++) {
+        if (!params[k]) {
+            set_error("dgs_deform_pack: null parameter pointer");
+            return DGS_ERR_ARGS;
+        }
+        src.p[k] = params[k];
+    }
+    const int *map = pack_map_for(P, flags);
+    if (!map) {
+        set_error("dgs_deform_pack: could not allocate the pack map");
+        return DGS_ERR_HIP;
+    }
+    const int nimg = P.nslots * 512, total = nimg + P.nf32;
+    hipLaunchKernelGGL(k_pack, dim3(div_up(total, 256)), dim3(256), 0, stream, map, src,
+                       reinterpret_cast<__bf16 *>(packed), packed + P.img_floats(), nimg, total);
+    DGS_LAUNCH_CHECK("k_pack", false, stream);
+    return DGS_OK;
+}
+
+int forward(int flags, int N, const float *xyz, const float *t, const float *packed, float *out, float *saved,
+            hipStream_t stream) {
+    const Plan P = make_plan(flags);
+    FwdArgs a{};
+    a.N = N;
+    a.Ns = padded_points(N);
+    a.xyz = xyz; a.t = t; a.out = out; a.saved = saved;
+    a.img = reinterpret_cast<const bf16x8 *>(packed);
+    a.fp = packed + P.img_floats();
+    a.mask = saved ? reinterpret_cast<uint32_t *>(saved + (size_t)P.F.nsaved * a.Ns) : nullptr;
+    a.fT1 = P.fT1; a.fT2 = P.fT2; a.fHd = P.fHd;
+    a.bT1 = P.bT1; a.bT2 = P.bT2; a.bHd = P.bHd; a.wT1 = P.wT1; a.wT2 = P.wT2;
+    for (int i = 0; i < 8; i++) { a.fL[i] = P.fL[i]; a.bL[i] = P.bL[i]; }
+    a.flags = flags;
+    {
+        ScopedTimer tm("mlp_fwd", stream);
+        if (saved && P.F.blender) {
+            a.tc = saved + (size_t)P.F.nsaved * a.Ns + (size_t)P.F.nmask * (a.Ns / 32);
+            hipLaunchKernelGGL(k_timenet, dim3(1), dim3(256), 0, stream, a);
+        }
+        if (saved)
+            hipLaunchKernelGGL(k_fwd<true>, dim3(div_up(N, BM)), dim3(NTHR), 0, stream, a);
+        else
+            hipLaunchKernelGGL(k_fwd<false>, dim3(div_up(N, BM)), dim3(NTHR), 0, stream, a);
+    }
+    DGS_LAUNCH_CHECK("k_fwd", false, stream);
+    return DGS_OK;
+}
+
+int backward(int flags, int N, const float *packed, const float *saved, const float *dout, float *scratch,
+             float *const *grads, hipStream_t stream) {
+    const Plan P = make_plan(flags);
+    const Flags &F = P.F;
+    const size_t Ns = padded_points(N);
+    float *dz = scratch;
+    float *slabs = scratch + (size_t)F.nz * Ns;
+    BwdArgs b{};
+    b.N = N; b.Ns = Ns; b.dout = dout; b.dz = dz;
+    b.img = reinterpret_cast<const bf16x8 *>(packed);
+    b.mask = reinterpret_cast<const uint32_t *>(saved + (size_t)F.nsaved * Ns);
+    b.tHd = P.tHd; b.tT2 = P.tT2;
+    for (int i = 0; i < 8; i++) b.tL[i] = P.tL[i];
+    b.flags = flags;
+    {
+        ScopedTimer tm("mlp_bwd", stream);
+        hipLaunchKernelGGL(k_bwd, dim3(div_up(N, BM)), dim3(NTHR), 0, stream, b);
+    }
+    DGS_LAUNCH_CHECK("k_bwd", false, stream);
+    if (!split_dw()) return mlp::dw_fp32(F, Ns, dz, saved, slabs, grads, stream);
+    const WPlan W = split_wplan(F);
+    {
+        static bool attr_set = false;  // 144 KiB dynamic LDS
+        if (!attr_set) {
+            DGS_HIP_CHECK(hipFuncSetAttribute((const void *)k_dw, hipFuncAttributeMaxDynamicSharedMemorySize, DW_LDS));
+            attr_set = true;
+        }
+        ScopedTimer tm("mlp_dw", stream);
+        hipLaunchKernelGGL(k_dw, dim3(W.nblocks), dim3(DW_THREADS), DW_LDS, stream, W.jobs, Ns, dz, saved, slabs);
+    }
+    DGS_LAUNCH_CHECK("k_dw", false, stream);
+    return launch_dw_reduce(F, W, slabs, grads, stream);
+}
+
+}  // namespace mlps
+}  // namespace dgs
+
+#ifdef DGS_MLP_PROFILE
+extern "C" void dgs_mlps_set_prof(unsigned long long *p) {
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(dgs::mlps::dgs_mlps_prof), &p, sizeof(p));
+}
+#endif
+
+// ------------------------------------------------------------------------------------------------
+// C ABI (include/dgs.h): the split-bf16 path unless DGS_MLP_EXACT_FP32 is set in the flags
+// ------------------------------------------------------------------------------------------------
+using namespace dgs;
+
+static bool exact_fp32(int flags) { return (flags & DGS_MLP_EXACT_FP32) != 0; }
+static int net_flags(int flags) { return flags & (DGS_MLP_BLENDER | DGS_MLP_6DOF | DGS_MLP_NO_ROTSCALE); }
+
+extern "C" int dgs_deform_outputs(int flags) { return mlpc::make_flags(flags).nout; }
+extern "C" int dgs_deform_num_params(int flags) { return mlpc::make_params(mlpc::make_flags(flags)).nparams; }
+
+extern "C" size_t dgs_deform_packed_floats(int flags) {
+    return exact_fp32(flags) ? mlp::packed_floats(net_flags(flags)) : mlps::make_plan(net_flags(flags)).total();
+}
+
+extern "C" size_t dgs_deform_saved_floats(int flags, int N) {
+    return exact_fp32(flags) ? mlp::saved_floats(net_flags(flags), N) : mlps::saved_floats(net_flags(flags), N);
+}
+
+extern "C" size_t dgs_deform_scratch_floats(int flags, int N) {
+    return exact_fp32(flags) ? mlp::scratch_floats(net_flags(flags), N) : mlps::scratch_floats(net_flags(flags), N);
+}
+
+extern "C" int dgs_deform_pack(int flags, const float *const *params, float *packed, void *stream_) {
+    hipStream_t stream = (hipStream_t)stream_;
+    if (!params || !packed) {
+        set_error("dgs_deform_pack: null argument");
+        return DGS_ERR_ARGS;
+    }
+    return exact_fp32(flags) ? mlp::pack(net_flags(flags), params, packed, stream)
+                             : mlps::pack(net_flags(flags), params, packed, stream);
+}
+
+extern "C" int dgs_deform_forward(int flags, int N, const float *xyz, const float *t, const float *packed, float *out,
+                                  float *saved, void *stream_) {
+    hipStream_t stream = (hipStream_t)stream_;
+    if (N < 0 || (N > 0 && (!xyz || !t || !packed || !out))) {
+        set_error("dgs_deform_forward: null argument");
+        return DGS_ERR_ARGS;
+    }
+    if (N == 0) return DGS_OK;
+    return exact_fp32(flags) ? mlp::forward(net_flags(flags), N, xyz, t, packed, out, saved, stream)
+                             : mlps::forward(net_flags(flags), N, xyz, t, packed, out, saved, stream);
+}
+
+extern "C" int dgs_deform_backward(int flags, int N, const float *packed, const float *saved, const float *dout,
+                                   float *scratch, float *const *grads, void *stream_) {
+    hipStream_t stream = (hipStream_t)stream_;
+    if (N < 0 || (N > 0 && (!packed || !saved || !dout || !scratch || !grads))) {
+        set_error("dgs_deform_backward: null argument");
+        return DGS_ERR_ARGS;
+    }
+    const mlpc::Flags F = mlpc::make_flags(flags);
+    const mlpc::Params P = mlpc::make_params(F);
+    if (N == 0) {
+        for (int k = 0; k < P.nparams; k++) {
+            int r, c;
+            mlpc::param_shape(F, P, k, r, c);
+            DGS_HIP_CHECK(hipMemsetAsync(grads[k], 0, sizeof(float) * r * (c ? c : 1), stream));
+        }
+        return DGS_OK;
+    }
+    return exact_fp32(flags) ? mlp::backward(net_flags(flags), N, packed, saved, dout, scratch, grads, stream)
+                             : mlps::backward(net_flags(flags), N, packed, saved, dout, scratch, grads, stream);
+}

@@ -10,7 +10,8 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load)
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_PKG, "lib", "libdgs_hip.so")
+# DGS_LIB: diagnostic builds only (tools/build_diag.sh); the product path is lib/libdgs_hip.so
+LIB_PATH = os.environ.get("DGS_LIB") or os.path.join(_PKG, "lib", "libdgs_hip.so")
 
 P = ctypes.c_void_p
 I = ctypes.c_int

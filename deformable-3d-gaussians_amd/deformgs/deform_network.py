@@ -8,6 +8,8 @@ split-N dW GEMM. Only the reference's shape is supported (D=8, W=256, multires=1
 raise. Gradients flow to the parameters only — every reference call site detaches x
 (train_baseline.py:115, render*.py) and t never requires grad; asking for d/dx raises.
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -17,6 +19,11 @@ from .rigid import screw_from_raw
 FLAG_BLENDER = 1
 FLAG_6DOF = 2
 FLAG_NO_ROTSCALE = 4
+FLAG_EXACT_FP32 = 8  # v_mfma_f32_32x32x2_f32 kernels instead of the split-bf16 (bf16x6) default
+
+
+def _exact_default():
+    return os.environ.get("DGS_MLP_EXACT_FP32", "0") not in ("", "0")
 
 
 def get_embedder_out_dim(multires, i=1):
@@ -66,7 +73,8 @@ class _FusedDeformMLP(torch.autograd.Function):
 class _DeformBase(nn.Module):
     _rotscale = True
 
-    def __init__(self, D=8, W=256, input_ch=3, output_ch=59, multires=10, is_blender=False, is_6dof=False):
+    def __init__(self, D=8, W=256, input_ch=3, output_ch=59, multires=10, is_blender=False, is_6dof=False,
+                 exact_fp32=None):
         super().__init__()
         if D != 8 or W != 256 or multires != 10:
             raise NotImplementedError("fused deformation MLP supports the reference shape D=8, W=256, multires=10")
@@ -101,6 +109,9 @@ class _DeformBase(nn.Module):
         self.gaussian_scaling = nn.Linear(W, 3)
         self.flags = (FLAG_BLENDER if is_blender else 0) | (FLAG_6DOF if is_6dof else 0) | (
             0 if self._rotscale else FLAG_NO_ROTSCALE)
+        # GEMM arithmetic: fp32 on bf16 MFMA over an exact hi/mid/lo split (default) or fp32-input MFMA;
+        # both are fp32-accurate (include/dgs.h), the flag is not part of the state_dict
+        self.exact_fp32 = _exact_default() if exact_fp32 is None else bool(exact_fp32)
 
     def kernel_params(self):
         """Parameters in the order of the C ABI's table (include/dgs.h)."""
@@ -123,7 +134,8 @@ class _DeformBase(nn.Module):
         _lib.require_cuda(x, t)
         x = x.detach().float().contiguous()
         t = t.detach().float().reshape(-1, 1).expand(x.shape[0], 1).contiguous()
-        return _FusedDeformMLP.apply(self.flags, x, t, *self.kernel_params())
+        flags = self.flags | (FLAG_EXACT_FP32 if self.exact_fp32 else 0)
+        return _FusedDeformMLP.apply(flags, x, t, *self.kernel_params())
 
     def forward(self, x, t):
         out = self.raw(x, t)

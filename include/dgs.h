@@ -98,11 +98,16 @@ void dgs_timing_select(const char *csv);
 double dgs_timing_query(const char *name, int *launches);
 void dgs_timing_reset(void);
 
-/* ---- deformation MLP (utils/time_utils.py:56-201), fused PE + 8x256 MLP on fp32 MFMA ---- */
+/* ---- deformation MLP (utils/time_utils.py:56-201), fused PE + 8x256 MLP ----
+ * Default: fp32 GEMMs on bf16 MFMA over an exact hi/mid/lo operand split (six products per fp32
+ * product, dropped terms < 2^-23 relative: fp32 accuracy). DGS_MLP_EXACT_FP32 selects the
+ * v_mfma_f32_32x32x2_f32 kernels (bit-identical to fp32 fma chains). The flag changes the packed /
+ * saved / scratch layouts: pass the same flags to every call of one forward/backward. */
 enum {
     DGS_MLP_BLENDER = 1,   /* timenet on (t: L=6 -> 256 -> 30); else raw t PE (L=10, 21 ch) */
     DGS_MLP_6DOF = 2,      /* heads branch_w(3), branch_v(3) instead of gaussian_warp(3) */
-    DGS_MLP_NO_ROTSCALE = 4 /* DeformNetwork fork variant: rotation/scaling heads unused */
+    DGS_MLP_NO_ROTSCALE = 4, /* DeformNetwork fork variant: rotation/scaling heads unused */
+    DGS_MLP_EXACT_FP32 = 8 /* fp32-input MFMA path instead of the split-bf16 path */
 };
 
 /* Parameter table: device pointers in state_dict order of DeformNetworkBaseline

@@ -64,3 +64,33 @@ def frac_close(a, b, atol, rtol):
     b = np.asarray(b, np.float64)
     ok = np.abs(a - b) <= atol + rtol * np.abs(b)
     return float(ok.mean())
+
+
+# saved-activation rows of the fused MLP (csrc/mlp_shared.h: S_H0.., S_H4.., S_TH), feature-major [rows][Ns]
+_S_H = [0, 256, 512, 768, 1120, 1376, 1632, 1888]
+_S_TH = 2160
+
+
+def mlp_relu_masks(output, N, blender, exact):
+    """The fused MLP kernel's own relu' masks {layer: bool (N, 256), "th": ...} read back from the
+    activations it saved for backward (autograd ctx of the fused node reached from `output`)."""
+    seen, todo, node = set(), [output.grad_fn], None
+    while todo:
+        fn = todo.pop()
+        if fn is None or fn in seen:
+            continue
+        seen.add(fn)
+        if "FusedDeformMLP" in type(fn).__name__:
+            node = fn
+            break
+        todo.extend(f for f, _ in fn.next_functions)
+    assert node is not None, "fused MLP node not found in the autograd graph"
+    _, saved = node.saved_tensors
+    block = 32 if exact else 64
+    Ns = (N + block - 1) // block * block
+    rows = 2416 if blender else 2144
+    sv = saved[: rows * Ns].view(rows, Ns)[:, :N].cpu().numpy()
+    masks = {i: (sv[r:r + 256] > 0).T for i, r in enumerate(_S_H)}
+    if blender:
+        masks["th"] = (sv[_S_TH:_S_TH + 256] > 0).T
+    return masks

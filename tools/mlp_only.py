@@ -21,7 +21,7 @@ def main():
     torch.manual_seed(0)
     net = DeformNetworkBaseline(is_blender=True).to(dev)
     x = torch.rand(a.n, 3, device=dev) * 2 - 1
-    t = torch.rand(a.n, 1, device=dev)
+    t = torch.full((a.n, 1), 0.3, device=dev)  # one frame time, as in training
     for _ in range(a.iters):
         d_xyz, d_rot, d_s = net(x, t)
         (d_xyz.sum() + d_rot.square().sum() + d_s.abs().sum()).backward()
