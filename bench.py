@@ -25,13 +25,18 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense FP32 matrix peak (spec)
+# split-bf16 GEMMs (csrc/mlp_split.hip): an fp32 product costs six bf16 MFMA products, so their fp32
+# roofline is the dense bf16 MFMA peak (~2.5 PF, MI355X_MICROARCH.md) / 6
+SPLIT_MFMA_PEAK_TFLOPS = 2500.0 / 6
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")  # tools/pmc_traffic.py output
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak (spec)
 
-# algorithmic multiply-accumulates per point of the blender network
-MLP_FWD_MAC = 519936            # every weight once
-MLP_DX_MAC = 484352             # W^T products whose input gradient is needed
-MLP_DW_MAC = 519936             # every weight once
+# algorithmic multiply-accumulates per point of the blender network with one frame time per step
+# (train_baseline.py:107-110): the timenet (13*256 + 256*30 = 11,008 MACs) is evaluated
+# once per launch, and its gradients come from the layer-0/5 bias gradients (DGS_MLP_UNIFORM_T)
+MLP_FWD_MAC = 508928            # every trunk + head weight once
+MLP_DX_MAC = 461312             # W^T products whose input gradient is needed (heads, L7..L1 hidden rows)
+MLP_DW_MAC = 508928             # every trunk + head weight once
 
 
 def parse():
@@ -51,6 +56,16 @@ def parse():
                     help="keep nn.Linear's default init on the deformation heads (the iteration-3000 transient: "
                          "deltas O(0.3) make every Gaussian hundreds of pixels wide)")
     return ap.parse_args()
+
+
+def mfma_peak(name):
+    """Dense MFMA peak (fp32-equivalent TFLOP/s) of the arithmetic kernel class `name` runs on."""
+    exact = os.environ.get("DGS_MLP_EXACT_FP32", "0") not in ("", "0")
+    if name == "mlp_dw" and os.environ.get("DGS_MLP_SPLIT_DW", "0") != "1":
+        return FP32_MFMA_PEAK_TFLOPS, "fp32 MFMA (v_mfma_f32_32x32x2_f32)"
+    if exact:
+        return FP32_MFMA_PEAK_TFLOPS, "fp32 MFMA (v_mfma_f32_32x32x2_f32)"
+    return SPLIT_MFMA_PEAK_TFLOPS, "bf16 MFMA peak / 6 (exact hi/mid/lo split, six products per fp32 product)"
 
 
 def kernel_algorithmic(name, N, P, HW):
@@ -248,8 +263,9 @@ def main():
         avg_s = ms / 1000.0 / n
         if bound == "mfma":
             achieved = amount / avg_s / 1e12
-            roofline = {"bound": "mfma", "kernel": name, "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS,
-                        "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
+            peak, arith = mfma_peak(name)
+            roofline = {"bound": "mfma", "kernel": name, "achieved": achieved, "peak": peak, "peak_basis": arith,
+                        "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
                         "avg_launch_ms": avg_s * 1e3, "launches": n}
         else:
             achieved = amount / avg_s / 1e9

@@ -1231,7 +1231,7 @@ int launch_dw_reduce(const Flags &F, const WPlan &W, const float *slabs, float *
             add(P.pHb[hh], r0, 1, &full, 8, true);
             r0 += P.hrows[hh];
         }
-        if (F.blender) {
+        if (F.blender && !F.uniform_t) {  // uniform t: written by the split path's k_tgrad
             Seg st = seg(0, F.tin, 0);
             add(P.pT0w, 0, 1, &st, 9, false);
             add(P.pT0b, 0, 1, &st, 9, true);

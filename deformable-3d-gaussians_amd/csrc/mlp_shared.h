@@ -30,6 +30,7 @@ constexpr int Z_L0 = 0, Z_G = 2048, Z_TE = 2080, Z_T1 = 2112;
 
 struct Flags {
     bool blender, sixdof, norotscale;
+    bool uniform_t;  // DGS_MLP_UNIFORM_T on a blender network: no per-point timenet backward
     int nout;     // head outputs: 10 or 13
     int tin;      // raw t PE channels: 13 (L=6) or 21 (L=10)
     int nsaved;   // saved rows
@@ -42,6 +43,7 @@ __host__ __device__ inline Flags make_flags(int f) {
     F.blender = f & DGS_MLP_BLENDER;
     F.sixdof = f & DGS_MLP_6DOF;
     F.norotscale = f & DGS_MLP_NO_ROTSCALE;
+    F.uniform_t = F.blender && (f & DGS_MLP_UNIFORM_T);
     F.nout = F.sixdof ? 13 : 10;
     F.tin = F.blender ? 13 : 21;
     F.nsaved = F.blender ? 2416 : 2144;
@@ -177,7 +179,7 @@ inline WPlan make_wplan(const Flags &F, int target, double fixed, double floor_)
             raw[nr++] = Raw{Z_L0 + 256 * i, 256, xrow + kt * WT, kp - kt * WT < WT ? kp - kt * WT : WT, i, kt};
     }
     raw[nr++] = Raw{Z_G, 32, s_h(7), 256, 8, 0};
-    if (F.blender) {
+    if (F.blender && !F.uniform_t) {  // uniform t: timenet gradients from the bias gradients instead
         raw[nr++] = Raw{Z_T1, 256, S_TIN, 16, 9, 0};
         raw[nr++] = Raw{Z_TE, 32, S_TH, 256, 10, 0};
     }

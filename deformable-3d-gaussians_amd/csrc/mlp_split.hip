@@ -356,8 +356,8 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
     DGS_STAMP(0);
     // frame-uniform t: all 64 points of the block carry k_timenet's t0 (every wave checks the same
     // 64 values, so the branch is block-uniform without a barrier)
-    bool uniform_t = false;
-    if (F.blender && a.tc) {
+    bool uniform_t = F.uniform_t && a.tc;  // the caller's guarantee (DGS_MLP_UNIFORM_T), else checked
+    if (F.blender && a.tc && !uniform_t) {
         const float t0 = a.tc[TC_T];
         const int p = p0 + lane;
         const float tv = p < a.N ? a.t[p] : t0;
@@ -433,7 +433,7 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
     lds_barrier();
     DGS_STAMP(1);
     f32x16 kt = zero16();  // previous layer's activations, awaiting their store
-    if (SAVE && uniform_t) {  // TH tile of this wave from k_timenet: relu' bits and the saved rows
+    if (SAVE && uniform_t && !F.uniform_t) {  // TH tile from k_timenet: relu' bits + saved rows (per-point backward)
         const Bias4 th = load_bias(a.tc + TC_TH, w * 32, lane);
         f32x16 c;
 #pragma unroll
@@ -609,7 +609,7 @@ __global__ __launch_bounds__(NTHR) void k_bwd(BwdArgs a) {
     for (int L = 7; L >= 1; L--) {
         // dX_L = W_L^T dZ_L; the H-part rows of the padded L5 input are n-tiles F_H/32 + w
         const int tile0 = (L == 5) ? F_H / 32 : 0;
-        if (L == 5 && F.blender)  // t_emb rows (padded 64..95 = n-tile 2), K split over the n-tile waves
+        if (L == 5 && F.blender && !F.uniform_t)  // t_emb rows (padded 64..95 = n-tile 2), K split over n-tiles
             gemm<2>(a.img + (size_t)(a.tL[5] + (F_TE / 32) * 16) * KSLOT, 2 * w, lds, G_BH, ct, lane, ct_te);
         uint32_t mk;
         f32x16 c = zero16();
@@ -622,9 +622,9 @@ __global__ __launch_bounds__(NTHR) void k_bwd(BwdArgs a) {
         lds_barrier();
     }
     const Stash dz0{kt, tile_addr(a.dz, Ns, Z_L0, w * 32, pw, lane)};
-    if (!F.blender) {
+    if (!F.blender || F.uniform_t) {  // raw t PE: no parameters upstream; uniform t: k_tgrad
         dz0.store_all();
-        return;  // raw t PE has no parameters upstream of it
+        return;
     }
     // layer 0: t_emb rows of W_0^T dZ_0 (K split), dZ_0 stored under it; then sum the K-parts
     gemm<2>(a.img + (size_t)(a.tL[0] + (F_TE / 32) * 16) * KSLOT, 2 * w, lds, G_BH, ct, lane, ct_te, NoPre(), dz0);
@@ -654,6 +654,40 @@ __global__ __launch_bounds__(NTHR) void k_bwd(BwdArgs a) {
         mask_apply(c, mk);
         Stash{c, tile_addr(a.dz, Ns, Z_T1, w * 32, pw, lane)}.store_all();
     }
+}
+
+// Timenet gradients for a frame-uniform t (DGS_MLP_UNIFORM_T). With one TIN / TH for every point,
+// dL/dt_emb summed over points is S = W0[:, TE]^T gb0 + W5[:, TE]^T gb5 (gb = the layer-0 / 5 bias
+// gradients = sums of dZ over points), and then
+//   timenet.2: dW = S TH^T, db = S;   dZ_T1 = relu'(TH) (W_T2^T S);   timenet.0: dW = dZ_T1 TIN^T, db = dZ_T1
+// — the per-point sums of the general path (time_utils.py:74-76 autograd) regrouped; one workgroup.
+struct TGradArgs {
+    const float *fp;
+    int w0te, w5te, wT2;  // fp32 [256][32] t_emb columns of linear.0 / linear.5, [32][256] timenet.2
+    const float *tc;      // k_timenet's TIN / TH
+    const float *gb0, *gb5;
+    float *gT0w, *gT0b, *gT2w, *gT2b;
+    int tin;
+};
+
+__global__ __launch_bounds__(256) void k_tgrad(TGradArgs a) {
+    __shared__ float S[32];
+    const int j = threadIdx.x;
+    if (j < 32) {
+        float s = 0.f;
+        for (int n = 0; n < 256; n++) s = fmaf(a.fp[a.w0te + n * 32 + j], a.gb0[n], s);
+        for (int n = 0; n < 256; n++) s = fmaf(a.fp[a.w5te + n * 32 + j], a.gb5[n], s);
+        S[j] = s;
+    }
+    __syncthreads();
+    const float th = a.tc[TC_TH + j];
+    float d = 0.f;
+    for (int k = 0; k < 30; k++) d = fmaf(a.fp[a.wT2 + k * 256 + j], S[k], d);
+    d = th > 0.f ? d : 0.f;
+    a.gT0b[j] = d;
+    for (int f = 0; f < a.tin; f++) a.gT0w[j * a.tin + f] = d * a.tc[TC_TIN + f];
+    for (int k = 0; k < 30; k++) a.gT2w[k * 256 + j] = S[k] * th;
+    if (j < 30) a.gT2b[j] = S[j];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -864,6 +898,7 @@ struct Plan : Params {
     std::vector<F32Job> f32;
     int fT1 = -1, fT2 = -1, fL[8], fHd, tHd, tL[8], tT2 = -1;  // k-slots
     int bT1 = -1, bT2 = -1, bL[8], bHd, wT1 = -1, wT2 = -1;     // fp32 offsets
+    int w0te = -1, w5te = -1;                                    // fp32 t_emb columns of linear.0 / .5
     int nslots = 0, nf32 = 0;
     size_t img_floats() const { return (size_t)nslots * KSLOT * 4; }  // 16-B unit = 4 floats
     size_t total() const { return img_floats() + nf32; }
@@ -912,6 +947,9 @@ Plan make_plan(int flags) {
         P.bT2 = new_f32(P.pT2b, 32, 1, 1, &s30, 1, &one);
         P.wT1 = new_f32(P.pT0w, 256, 16, 1, &full, 1, &st);
         P.wT2 = new_f32(P.pT2w, 32, 256, 1, &s30, 1, &full);
+        const Seg te0 = seg(0, 30, 63);  // linear.0 / linear.5 columns 63..92 = t_emb (layer_in_segs)
+        P.w0te = new_f32(P.pLw[0], 256, 32, 1, &full, 1, &te0);
+        P.w5te = new_f32(P.pLw[5], 256, 32, 1, &full, 1, &te0);
     }
     for (int i = 0; i < 8; i++) {
         Seg s[3];
@@ -1020,6 +1058,8 @@ static int *pack_map_for(const Plan &P, int flags) {
 
 // dW split plan: one 8-wave workgroup per CU (LDS 144 KiB); per-chunk cost in MFMA tiles + staging
 static WPlan split_wplan(const Flags &F) { return make_wplan(F, 256, 1.5, 4.0); }
+static int dw_split(const Flags &F, size_t Ns, const float *dz, const float *saved, float *slabs, float *const *grads,
+                    hipStream_t stream);
 
 static size_t padded_points(int N) { return (size_t)div_up(N, BM) * BM; }
 
@@ -1119,7 +1159,27 @@ int backward(int flags, int N, const float *packed, const float *saved, const fl
         hipLaunchKernelGGL(k_bwd, dim3(div_up(N, BM)), dim3(NTHR), 0, stream, b);
     }
     DGS_LAUNCH_CHECK("k_bwd", false, stream);
-    if (!split_dw()) return mlp::dw_fp32(F, Ns, dz, saved, slabs, grads, stream);
+    int rc;
+    if (!split_dw()) {
+        rc = mlp::dw_fp32(F, Ns, dz, saved, slabs, grads, stream);
+    } else {
+        rc = dw_split(F, Ns, dz, saved, slabs, grads, stream);
+    }
+    if (rc != DGS_OK || !F.uniform_t) return rc;
+    TGradArgs g{};
+    g.fp = packed + P.img_floats();
+    g.w0te = P.w0te; g.w5te = P.w5te; g.wT2 = P.wT2;
+    g.tc = saved + (size_t)F.nsaved * Ns + (size_t)F.nmask * (Ns / 32);
+    g.gb0 = grads[P.pLb[0]]; g.gb5 = grads[P.pLb[5]];
+    g.gT0w = grads[P.pT0w]; g.gT0b = grads[P.pT0b]; g.gT2w = grads[P.pT2w]; g.gT2b = grads[P.pT2b];
+    g.tin = F.tin;
+    hipLaunchKernelGGL(k_tgrad, dim3(1), dim3(256), 0, stream, g);
+    DGS_LAUNCH_CHECK("k_tgrad", false, stream);
+    return DGS_OK;
+}
+
+static int dw_split(const Flags &F, size_t Ns, const float *dz, const float *saved, float *slabs, float *const *grads,
+                    hipStream_t stream) {
     const WPlan W = split_wplan(F);
     {
         static bool attr_set = false;  // 144 KiB dynamic LDS
@@ -1149,7 +1209,10 @@ extern "C" void dgs_mlps_set_prof(unsigned long long *p) {
 using namespace dgs;
 
 static bool exact_fp32(int flags) { return (flags & DGS_MLP_EXACT_FP32) != 0; }
-static int net_flags(int flags) { return flags & (DGS_MLP_BLENDER | DGS_MLP_6DOF | DGS_MLP_NO_ROTSCALE); }
+static int net_flags(int flags) {
+    return exact_fp32(flags) ? flags & (DGS_MLP_BLENDER | DGS_MLP_6DOF | DGS_MLP_NO_ROTSCALE)
+                             : flags & (DGS_MLP_BLENDER | DGS_MLP_6DOF | DGS_MLP_NO_ROTSCALE | DGS_MLP_UNIFORM_T);
+}
 
 extern "C" int dgs_deform_outputs(int flags) { return mlpc::make_flags(flags).nout; }
 extern "C" int dgs_deform_num_params(int flags) { return mlpc::make_params(mlpc::make_flags(flags)).nparams; }

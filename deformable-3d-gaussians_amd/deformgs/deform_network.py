@@ -20,6 +20,7 @@ FLAG_BLENDER = 1
 FLAG_6DOF = 2
 FLAG_NO_ROTSCALE = 4
 FLAG_EXACT_FP32 = 8  # v_mfma_f32_32x32x2_f32 kernels instead of the split-bf16 (bf16x6) default
+FLAG_UNIFORM_T = 16  # every point carries t[0] (set when t is one value or a stride-0 expand)
 
 
 def _exact_default():
@@ -132,9 +133,14 @@ class _DeformBase(nn.Module):
             raise NotImplementedError("fused deformation MLP does not differentiate w.r.t. its inputs; "
                                       "detach xyz / t as every reference call site does")
         _lib.require_cuda(x, t)
+        N = x.shape[0]
+        # one frame time for every Gaussian (train_baseline.py:107-110: fid.unsqueeze(0).expand(N, -1),
+        # ast_noise likewise expanded from (1, 1)): recognisable without a device read as a single value
+        # or a stride-0 expand; the kernels then form the timenet gradients from the bias gradients
+        uniform = t.numel() == 1 or (t.dim() >= 1 and t.shape[0] == N and t.stride(0) == 0)
         x = x.detach().float().contiguous()
-        t = t.detach().float().reshape(-1, 1).expand(x.shape[0], 1).contiguous()
-        flags = self.flags | (FLAG_EXACT_FP32 if self.exact_fp32 else 0)
+        t = t.detach().float().reshape(-1, 1).expand(N, 1).contiguous()
+        flags = self.flags | (FLAG_EXACT_FP32 if self.exact_fp32 else 0) | (FLAG_UNIFORM_T if uniform else 0)
         return _FusedDeformMLP.apply(flags, x, t, *self.kernel_params())
 
     def forward(self, x, t):

@@ -15,8 +15,14 @@ def forward_backward(gaussians, deform, cam, gt_image, pipe, background, is_6dof
         d_xyz, d_rotation, d_scaling = 0.0, 0.0, 0.0
     else:
         N = gaussians.get_xyz.shape[0]
-        time_input = cam.fid.unsqueeze(0).expand(N, -1)
-        d_xyz, d_rotation, d_scaling = deform.step(gaussians.get_xyz.detach(), time_input + ast_noise)
+        # time_input = fid.unsqueeze(0).expand(N, -1) + ast_noise (train_baseline.py:107-110); the noise
+        # is one value per iteration (randn(1, 1).expand), so it is added before the expand and the
+        # network sees a stride-0 time column (one frame time: DGS_MLP_UNIFORM_T)
+        t = cam.fid.unsqueeze(0)
+        if torch.is_tensor(ast_noise) or ast_noise != 0.0:
+            t = t + (ast_noise.reshape(-1)[:1].reshape(1, 1) if torch.is_tensor(ast_noise) else ast_noise)
+        time_input = t.expand(N, -1)
+        d_xyz, d_rotation, d_scaling = deform.step(gaussians.get_xyz.detach(), time_input)
     pkg = render(cam, gaussians, pipe, background, d_xyz, d_rotation, d_scaling, is_6dof)
     image = pkg["render"]
     # (1-l)*l1_loss(image, gt) + l*(1-ssim(image, gt)) (train_baseline.py:126-127), fused HIP kernels

@@ -107,7 +107,11 @@ enum {
     DGS_MLP_BLENDER = 1,   /* timenet on (t: L=6 -> 256 -> 30); else raw t PE (L=10, 21 ch) */
     DGS_MLP_6DOF = 2,      /* heads branch_w(3), branch_v(3) instead of gaussian_warp(3) */
     DGS_MLP_NO_ROTSCALE = 4, /* DeformNetwork fork variant: rotation/scaling heads unused */
-    DGS_MLP_EXACT_FP32 = 8 /* fp32-input MFMA path instead of the split-bf16 path */
+    DGS_MLP_EXACT_FP32 = 8, /* fp32-input MFMA path instead of the split-bf16 path */
+    DGS_MLP_UNIFORM_T = 16  /* caller guarantees t[i] == t[0] for every point (one frame time, as
+                               train_baseline.py:107-110 feeds it): the timenet gradients are formed
+                               from the layer-0/5 bias gradients instead of per-point sums (split path,
+                               blender only; ignored otherwise) */
 };
 
 /* Parameter table: device pointers in state_dict order of DeformNetworkBaseline

@@ -71,9 +71,11 @@ _S_H = [0, 256, 512, 768, 1120, 1376, 1632, 1888]
 _S_TH = 2160
 
 
-def mlp_relu_masks(output, N, blender, exact):
+def mlp_relu_masks(output, N, blender, exact, th_saved=True):
     """The fused MLP kernel's own relu' masks {layer: bool (N, 256), "th": ...} read back from the
-    activations it saved for backward (autograd ctx of the fused node reached from `output`)."""
+    activations it saved for backward (autograd ctx of the fused node reached from `output`).
+    th_saved=False: the forward ran with DGS_MLP_UNIFORM_T (one-element or stride-0 t), which keeps
+    no per-point TH rows; the oracle then uses its own TH masks."""
     seen, todo, node = set(), [output.grad_fn], None
     while todo:
         fn = todo.pop()
@@ -91,6 +93,6 @@ def mlp_relu_masks(output, N, blender, exact):
     rows = 2416 if blender else 2144
     sv = saved[: rows * Ns].view(rows, Ns)[:, :N].cpu().numpy()
     masks = {i: (sv[r:r + 256] > 0).T for i, r in enumerate(_S_H)}
-    if blender:
+    if blender and th_saved:
         masks["th"] = (sv[_S_TH:_S_TH + 256] > 0).T
     return masks

@@ -92,7 +92,8 @@ def test_mlp_vs_oracle_ragged(name, tmode, N, arith):
     t = _times(rng, N, tmode)
     out, c = mlp_ref.forward(w, x, t, bl, d6)
     d_xyz, d_rot, d_scale = net(torch.from_numpy(x).cuda(), torch.from_numpy(t).cuda())
-    masks = mlp_relu_masks(d_xyz, N, bl, ARITH[arith])  # read before backward frees the saved activations
+    # read before backward frees the saved activations; a one-element t (N = 1) runs DGS_MLP_UNIFORM_T
+    masks = mlp_relu_masks(d_xyz, N, bl, ARITH[arith], th_saved=N > 1 or ARITH[arith])
     for a, b in ((d_xyz, out["d_xyz"]), (d_rot, out["d_rot"]), (d_scale, out["d_scale"])):
         assert np.allclose(a.detach().cpu().numpy(), b, atol=2e-5, rtol=1e-4)
     g = {k: rng.standard_normal(out[k].shape) for k in ("d_xyz", "d_rot", "d_scale")}
@@ -172,3 +173,46 @@ def test_split_accuracy_matches_fp32(name):
         errs[arith] = e
     for k in errs["exact"]:
         assert errs["split"][k] <= 2.0 * errs["exact"][k] + 1e-6, (k, errs["split"][k], errs["exact"][k])
+
+
+def _raw_grads(G, d6, fork):
+    if d6:
+        return {"w_raw": G[:, 0:3], "v_raw": G[:, 3:6], "d_rot": G[:, 6:10], "d_scale": G[:, 10:13]}
+    return {"d_xyz": G[:, 0:3], "d_rot": G[:, 3:7], "d_scale": G[:, 7:10]}
+
+
+@pytest.mark.parametrize("name", ["blender", "6dof", "nonblender", "fork"])
+@pytest.mark.parametrize("N", [63, 4099])
+def test_uniform_t_flag(name, N):
+    """A stride-0 time column (train_baseline.py:107-110) sets DGS_MLP_UNIFORM_T: the backward skips
+    the per-point t_emb GEMMs and k_tgrad forms the timenet gradients from the layer-0/5 bias
+    gradients. Outputs must equal the per-point path's bit for bit; gradients match the oracle
+    (1e-4 of each tensor's max) and the per-point path."""
+    bl, d6, fork = VARIANTS[name]
+    rng = np.random.default_rng(N + 1)
+    x = rng.uniform(-1.3, 1.3, (N, 3)).astype(np.float32)
+    t0 = 0.43
+    xt = torch.from_numpy(x).cuda()
+    G = rng.standard_normal((N, 13 if d6 else 10))
+    if fork:
+        G[:, 3:] = 0.0
+    res = {}
+    for mode in ("expanded", "full"):
+        net, w = _net(name, 31)
+        tt = torch.full((1, 1), t0, device="cuda").expand(N, -1) if mode == "expanded" else \
+            torch.full((N, 1), t0, device="cuda")
+        raw = net.raw(xt, tt)
+        masks = mlp_relu_masks(raw, N, bl, False, th_saved=mode == "full")
+        (raw * torch.from_numpy(G).float().cuda()).sum().backward()
+        res[mode] = (raw.detach().clone(), {k: p.grad.clone() for k, p in net.named_parameters()}, masks)
+    assert torch.equal(res["expanded"][0], res["full"][0])
+    out, c = mlp_ref.forward(w, x, np.full((N, 1), t0, np.float32), bl, d6)
+    ref = mlp_ref.backward(w, c, out, _raw_grads(G, d6, fork), bl, d6, fork, relu_masks=res["expanded"][2])
+    for k, g in res["expanded"][1].items():
+        got = g.cpu().numpy()
+        if k not in ref:
+            assert np.abs(got).max() == 0.0, k
+            continue
+        tol = 1e-4 * max(np.abs(ref[k]).max(), 1e-6) + 1e-6
+        assert np.abs(got - ref[k]).max() <= tol, (k, np.abs(got - ref[k]).max(), tol)
+        assert np.abs(got - res["full"][1][k].cpu().numpy()).max() <= 2 * tol, k
