@@ -10,31 +10,36 @@
 //   hi = bf16(x), mid = bf16(x - hi), lo = x - hi - mid        (round to nearest)
 // (x - hi is exact in fp32 and has at most 16 significant bits, so lo has at most 8: x = hi+mid+lo,
 // |mid| <= 2^-8 |x|, |lo| <= 2^-16 |x|). A product a*b is accumulated as the six bf16 x bf16 products
-// hh + hm + mh + hl + lh + mm, each exact in the fp32 accumulator of v_mfma_f32_32x32x16_bf16; the
-// dropped ml + lm + ll are below 2^-23 |ab| (fp32's own rounding of a product is up to 2^-24 |ab|).
-// The GEMMs therefore keep fp32 accuracy (tests/test_gpu_mlp.py holds them to the same tolerances
-// as the exact-fp32 path) at 16/6 = 2.67x the fp32-MFMA rate (MI355X: bf16 MFMA = 16x f32 MFMA per
-// clock, MI355X_MICROARCH.md). Additions, biases, ReLU, PE and all reductions stay fp32.
+// hh + hm + mh + hl + lh + mm, each exact in the fp32 accumulator of the MFMA; the dropped ml + lm +
+// ll are below 2^-23 |ab| (fp32's own rounding of a product is up to 2^-24 |ab|). An MFMA aligns its
+// products and C to the largest term within a limited window (tools/mfma_round_probe.hip), so the
+// five corrections of each k-step go into a fresh accumulator that is added to the running sum in
+// fp32 (tools/mfma_accum_probe.hip: as accurate as the fp32 fma chain). The GEMMs keep fp32 accuracy
+// (tests/test_gpu_mlp.py holds them to the exact-fp32 path's error) at 16/6 = 2.67x the fp32-MFMA
+// rate (MI355X: bf16 MFMA = 16x f32 MFMA per clock). Biases, ReLU, PE and reductions stay fp32.
 //
-// Layout ("transposed" formulation, Y^T = W X^T: features on MFMA rows, points on MFMA columns):
-//  * One workgroup = 64 points (two 32-point column tiles) x 16 waves (4 per SIMD): wave (w, ct)
-//    owns output rows 32w..32w+31 of every 256-wide layer for column tile ct; the two waves of an
-//    n-tile fetch the same weight fragments (L1-shared when they run close together).
+// Layout ("transposed" formulation, Y^T = W X^T: features on MFMA rows, points on MFMA columns),
+// v_mfma_f32_16x16x32_bf16:
+//  * One workgroup = 64 points x 16 waves (4 per SIMD); wave r owns output rows 16r..16r+15 of every
+//    256-wide layer for all four 16-point column tiles, so each 3 KiB weight fragment (16 rows x 32
+//    features x 3 splits) fetched from L2 feeds 4 x 6 MFMAs.
 //  * Activations live in LDS split into hi/mid/lo bf16 images of 16-byte units (8 features x 1
-//    point), [8-feature group][split][64 points]: the B operand of a k-step (16 features) is one
-//    ds_read_b128 per split and column tile, and an accumulator's rows 8j + 4h + 0..3 are one 8-byte
-//    store per split into the next layer's image. XE | TE | H groups are contiguous, so
-//    cat(x_emb, t_emb) and cat(x_emb, t_emb, h) are plain group ranges (141 KB of LDS: one block per
-//    CU).
+//    point), [8-feature group][split][64 points]: the B operand of a k-step (32 features) is one
+//    ds_read_b128 per split and column tile, and an accumulator's 4 rows are one 8-byte store per
+//    split into the next layer's image. XE | TE | H groups are contiguous, so cat(x_emb, t_emb) and
+//    cat(x_emb, t_emb, h) are plain group ranges (147 KB of LDS: one block per CU).
+//  * Narrow layers (timenet.2, heads, the t_emb rows of the backward) run as full-K 16x16 tiles on a
+//    subset of the waves: no partial sums.
 //  * Weights are packed every call (they change every optimizer step) by one gather + split launch
-//    into A-fragment images [n-tile][k-step][split][64 lanes][8 bf16] (3 KiB per wave k-step).
-//  * Saved activations / dZ stay fp32 feature-major [rows][Ns] (mlp_shared.h row map), the dW
-//    GEMM splits them while staging its LDS tiles; relu' masks are 16-bit lane masks per 32x32 tile
-//    (same layout as the fp32 path). Every reduction is in a fixed order: bitwise deterministic.
+//    into A-fragment images [n-tile][k-step][split][64 lanes][8 bf16].
+//  * Saved activations / dZ stay fp32 feature-major [rows][Ns] (mlp_shared.h row map; the dW GEMM
+//    reads them), written in each layer's epilogue; relu' masks are one u16 per lane and 16-row
+//    tile ([64-point block][row / 16][64 lanes]). Every reduction has a fixed order: bitwise
+//    deterministic.
 #include <hip/hip_runtime.h>
 
-#include <cmath>
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <map>
 #include <mutex>
@@ -49,28 +54,30 @@ namespace mlps {
 using namespace mlpc;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BM = 64;            // points per workgroup
-constexpr int NT = 2;             // 32-point column tiles per workgroup
-constexpr int NWAVE = 16;         // 8 n-tiles x 2 column tiles
+constexpr int NQ = 4;             // 16-point column tiles per workgroup
+constexpr int NWAVE = 16;         // one 16-row n-tile of a 256-wide layer per wave
 constexpr int NTHR = NWAVE * 64;
 constexpr int NSPLIT = 3;         // hi, mid, lo
 constexpr int UG = NSPLIT * BM;   // 16-B units per 8-feature group (all splits, all points)
 constexpr int KSLOT = 3 * 64;     // units per (n-tile, k-step) of an A image: 3 splits x 64 lanes
-// forward LDS groups: XE (64 features) | TE (32) | H (256) | TIN (16)
-constexpr int G_XE = 0, G_TE = 8, G_H = 12, G_TIN = 44, G_FWD = 46;
+constexpr int KG = 4;             // 8-feature groups per k-step (32 features)
+// forward LDS groups: XE (64 features) | TE (32) | H (256) | TIN (16 + 16 zero: one k-step)
+constexpr int G_XE = 0, G_TE = 8, G_H = 12, G_TIN = 44, G_FWD = 48;
 // backward LDS groups: H (dZ, 256) | G (dOut / dTE, 32)
 constexpr int G_BH = 0, G_BG = 32, G_BWD = 36;
 // fp32 staging rows (inside the H region): XE 0..63 | TE 64..95 | TIN 96..111
 constexpr int ST_TE = 64, ST_TIN = 96;
+// relu' mask tiles: [64-point block][row / 16][64 lanes] u16 = 2 * nmask u32 words per block
+constexpr int MR_TH = M_TH / 16;
 
 static_assert(G_TE == G_XE + 8 && G_H == G_TE + 4, "XE|TE|H must be contiguous");
 static_assert(G_FWD * UG * 16 <= 160 * 1024 && G_BWD * UG * 16 <= 160 * 1024, "LDS");
-// PART (8 K-part slots x 32 rows x 64 points fp32) and the fp32 staging alias the H region
-constexpr int NPART = 8;
-static_assert(NPART * 32 * BM * 4 <= 32 * UG * 16, "PART must fit the H region");
+static_assert(112 * BM * 4 <= 32 * UG * 16, "fp32 staging must fit the H region");
 
 // ------------------------------------------------------------------------------------------------
 // exact three-way split
@@ -105,9 +112,10 @@ __device__ inline void put_unit8(bf16x8 *lds, int g, int m, const float (&v)[8])
 }
 
 // ------------------------------------------------------------------------------------------------
-// GEMM pieces: acc[ct] (32 rows of this wave x 32 points of column tile ct) += A . X
+// GEMM pieces. 16x16x32 lane maps (cdna_hip_programming.md §3): lane l (kq = l >> 4, col = l & 15)
+// holds A[row col][k = 8 kq + j] and B[k = 8 kq + j][col col]; C/D element i is row 4 kq + i, col col.
 // ------------------------------------------------------------------------------------------------
-#define MFMA16(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
+#define MF16(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
 
 struct AFrag {  // one operand fragment in its three split parts
     bf16x8 h, m, l;
@@ -115,39 +123,21 @@ struct AFrag {  // one operand fragment in its three split parts
 
 __device__ inline AFrag load_a(const bf16x8 *p) { return AFrag{p[0], p[64], p[128]}; }
 
-// B fragment of column tile ct from the LDS image (p: this lane's unit of split 0, column tile 0)
-__device__ inline AFrag load_b(const bf16x8 *p, int ct) { return AFrag{p[32 * ct], p[BM + 32 * ct], p[2 * BM + 32 * ct]}; }
+// B fragment of column tile q from the LDS image (p: this lane's unit of split 0, column tile 0)
+__device__ inline AFrag load_b(const bf16x8 *p, int q) { return AFrag{p[16 * q], p[BM + 16 * q], p[2 * BM + 16 * q]}; }
 
-// The six split products: hh into `hi`, the five corrections (mm, hl, lh, hm, mh: |.| <= 2^-8 |hh|)
-// into `lo`, summed in fp32 once at the end. An MFMA aligns its 16 products and C to the largest
-// term inside a limited window (tools/mfma_round_probe.hip: C = 1 plus 2^-30 minus 1 gives 0), so
-// corrections added into a running C of the hh magnitude would lose their low bits, with a slight
-// bias that long point sums (dW over 10^4-10^5 points) expose; in their own accumulator they keep
-// them. (Dependent 32x32x16 MFMAs issue back to back at full rate: MI355X_MICROARCH.md.)
-__device__ inline void mma6_2(const AFrag &a, const AFrag &b, f32x16 &hi, f32x16 &lo) {
-    lo = MFMA16(a.m, b.m, lo);
-    lo = MFMA16(a.h, b.l, lo);
-    lo = MFMA16(a.l, b.h, lo);
-    lo = MFMA16(a.h, b.m, lo);
-    lo = MFMA16(a.m, b.h, lo);
-    hi = MFMA16(a.h, b.h, hi);
-}
+__device__ inline f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
-// the six split products into one accumulator, smallest first
-__device__ inline void mma6_1(const AFrag &a, const AFrag &b, f32x16 &c) {
-    c = MFMA16(a.m, b.m, c);
-    c = MFMA16(a.h, b.l, c);
-    c = MFMA16(a.l, b.h, c);
-    c = MFMA16(a.h, b.m, c);
-    c = MFMA16(a.m, b.h, c);
-    c = MFMA16(a.h, b.h, c);
-}
-
-__device__ inline f32x16 zero16() {
-    f32x16 z;
-#pragma unroll
-    for (int i = 0; i < 16; i++) z[i] = 0.f;
-    return z;
+// The six split products of one k-step: hh into the running accumulator, the five corrections
+// (|.| <= 2^-8 |hh|) into a fresh one added in fp32 (see the numerics note above).
+__device__ inline void mma6(const AFrag &a, const AFrag &b, f32x4 &acc) {
+    f32x4 t = MF16(a.m, b.m, zero4());
+    t = MF16(a.h, b.l, t);
+    t = MF16(a.l, b.h, t);
+    t = MF16(a.h, b.m, t);
+    t = MF16(a.m, b.h, t);
+    acc = MF16(a.h, b.h, acc);
+    acc += t;
 }
 
 #ifdef DGS_MLP_PROFILE  // diagnostic build only (tools/mlp_phase.py): per-phase s_memtime stamps
@@ -165,49 +155,26 @@ __device__ unsigned long long *dgs_mlps_prof;
 struct NoPre {
     __device__ void operator()() const {}
 };
-struct NoStash {
-    __device__ void store(int) const {}
-};
 
-// The previous layer's output tile of this wave (16 values per lane), kept in registers and
-// written to a feature-major [rows][Ns] array during the first two k-steps of the next GEMM (8
-// coalesced stores per k-step, issued after that GEMM's prologue loads).
-struct Stash {
-    f32x16 t;
-    TileAddr d;
-    __device__ void store(int k) const {
-#pragma unroll
-        for (int j = 0; j < 8; j++) d.st(8 * k + j, t[8 * k + j]);
-    }
-    __device__ void store_all() const {
-        store(0);
-        store(1);
-    }
-};
-
-// acc += A . X over NK k-steps starting at k-step c0 of this wave's A image (Aw: unit pointer of
-// its n-tile at k-step 0) and of column tile ct of the LDS image at group g0 (k-step c = groups
-// g0 + 2c + h). Fully unrolled; per k-step: the six MFMAs (mma6_2), then the next k-step's B into
-// the same registers and the A fragment RING k-steps ahead (register ring; the A stream comes from
-// L2, 3 KiB per wave k-step), and the stash stores in k-steps 0-1 (sched_barrier keeps that order;
-// the three other waves of the SIMD cover the B reload latency). pre() runs after the A prologue.
-template <int NK, class Pre = NoPre, class St = NoStash>
-__device__ inline void gemm(const bf16x8 *__restrict__ Aw, int c0, const bf16x8 *lds, int g0, int ct, int lane,
-                            f32x16 &acc, Pre pre = Pre(), const St stash = St()) {
+// acc[q] += A . X for the column tiles q0 .. q0 + NQ_ - 1 over NK k-steps of this wave's A image
+// (Aw: unit pointer of its n-tile at k-step 0) and of the LDS image from group g0 (k-step c =
+// groups g0 + 4c + kq). Fully unrolled; per k-step: each column tile's six MFMAs followed by its B
+// fragment for the next k-step into the same registers, then the A fragment RING k-steps ahead
+// (register ring: the A stream comes from L2). sched_barrier keeps that order per k-step; the other
+// three waves of the SIMD cover the B reload latency. pre() runs after the A prologue.
+template <int NK, int NQ_, class Pre = NoPre>
+__device__ inline void gemm(const bf16x8 *__restrict__ Aw, const bf16x8 *lds, int g0, int q0, int lane,
+                            f32x4 (&acc)[NQ_], Pre pre = Pre()) {
     static_assert(NK >= 1, "empty GEMM");
-    const int h = lane >> 5, m = lane & 31;
-    const bf16x8 *Ap = Aw + c0 * KSLOT + lane;
-    const bf16x8 *Bp = lds + (g0 + 2 * c0 + h) * UG + 32 * ct + m;
+    const int kq = lane >> 4, col = lane & 15;
+    const bf16x8 *Ap = Aw + lane;
+    const bf16x8 *Bp = lds + (g0 + kq) * UG + 16 * q0 + col;
 #ifdef DGS_DIAG_A_STATIC  // timing experiment only (wrong results): every k-step re-reads k-step 0's A
     constexpr int AK = 0;
 #else
     constexpr int AK = KSLOT;
 #endif
-#ifdef DGS_DIAG_B_STATIC  // timing experiment only (wrong results): every k-step re-reads k-step 0's B
-    constexpr int BK = 0;
-#else
-    constexpr int BK = 2 * UG;
-#endif
+    constexpr int BK = KG * UG;
     constexpr int RING = 2;
     AFrag ring[RING];
 #pragma unroll
@@ -215,64 +182,99 @@ __device__ inline void gemm(const bf16x8 *__restrict__ Aw, int c0, const bf16x8 
         if (k < NK) ring[k] = load_a(Ap + k * AK);
     pre();
     AFrag b = load_b(Bp, 0);
-    f32x16 lo = zero16();  // the correction products (mma6_2)
 #pragma unroll
     for (int k = 0; k < NK; k++) {
         __builtin_amdgcn_sched_barrier(0);
-        mma6_2(ring[k % RING], b, acc, lo);
-        if (k + 1 < NK) b = load_b(Bp + (k + 1) * BK, 0);  // B of the next k-step into the same registers
+#pragma unroll
+        for (int q = 0; q < NQ_; q++) {
+            // the next tile's B fragment (or the next k-step's first) is in flight during this tile's MFMAs
+            AFrag nb;
+            if (q + 1 < NQ_) nb = load_b(Bp + k * BK, q + 1);
+            else if (k + 1 < NK) nb = load_b(Bp + (k + 1) * BK, 0);
+            mma6(ring[k % RING], b, acc[q]);
+            if (q + 1 < NQ_ || k + 1 < NK) b = nb;
+        }
         if (k + RING < NK) ring[k % RING] = load_a(Ap + (k + RING) * AK);
-        if (k < 2) stash.store(k);
         __builtin_amdgcn_sched_barrier(0);
     }
-#pragma unroll
-    for (int k = NK; k < 2; k++) stash.store(k);
-#pragma unroll
-    for (int i = 0; i < 16; i++) acc[i] += lo[i];
 }
 
-// accumulator tile ct (rows n0.. of this wave) -> split units of groups gbase + j (j < 4)
-__device__ inline void acc_to_lds(const f32x16 &acc, bf16x8 *lds, int gbase, int ct, int lane) {
-    const int h = lane >> 5, m = lane & 31;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const Split4 s = split4(acc[4 * j], acc[4 * j + 1], acc[4 * j + 2], acc[4 * j + 3]);
-        bf16x4 *u = reinterpret_cast<bf16x4 *>(lds + (gbase + j) * UG + 32 * ct + m) + h;
-        u[0] = s.h;
-        u[2 * BM] = s.m;  // bf16x4 units: one 16-B unit = 2 of them
-        u[4 * BM] = s.l;
+// accumulator tile q (rows 16r + 4kq + i of this wave, point 16q + col) -> its 8-byte half of the
+// split units of group 2r + (kq >> 1) (LDS image from group gbase)
+__device__ inline void acc_to_lds(const f32x4 &v, bf16x8 *lds, int gbase, int r, int q, int lane) {
+    const int kq = lane >> 4, col = lane & 15;
+    const Split4 s = split4(v[0], v[1], v[2], v[3]);
+    bf16x4 *u = reinterpret_cast<bf16x4 *>(lds + (gbase + 2 * r + (kq >> 1)) * UG + 16 * q + col) + (kq & 1);
+    u[0] = s.h;
+    u[2 * BM] = s.m;  // bf16x4 units: one 16-B unit = 2 of them
+    u[4 * BM] = s.l;
+}
+
+// A wave's 16-row x 64-point tile of a feature-major [rows][Ns] array through a buffer descriptor
+// whose base is the tile origin (wave-uniform: SGPRs): store (i, q) writes rows 4kq + i of column
+// tile q, one buffer instruction each with the row offset in an SGPR.
+struct Tile16 {
+    __amdgpu_buffer_rsrc_t rsrc;  // base = &dst[row0 * Ns + p0]
+    int voff;                     // (4kq * Ns + col) * 4 bytes
+    int ns4;                      // Ns * 4 bytes
+    __device__ void st(int i, int q, float v) const {
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc, voff + 64 * q, i * ns4, 0);
     }
-}
-
-// PART slot q (fp32 [32 rows][BM points]), column tile ct <- this wave's accumulator tile
-__device__ inline void acc_to_part(const f32x16 &acc, float *part, int q, int ct, int lane) {
-    const int h = lane >> 5, m = lane & 31;
+    template <int NQ_>
+    __device__ void store(const f32x4 (&v)[NQ_], int q0 = 0) const {
 #pragma unroll
-    for (int r = 0; r < 16; r++) part[(q * 32 + TileAddr::row(r) + 4 * h) * BM + 32 * ct + m] = acc[r];
-}
-
-
-// bias of this lane's accumulator rows (n0 + 8j + 4h .. +3, j < 4), loaded ahead of the GEMM
-struct Bias4 {
-    float4 v[4];
+        for (int q = 0; q < NQ_; q++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) st(i, q0 + q, v[q][i]);
+    }
 };
 
-__device__ inline Bias4 load_bias(const float *bias, int n0, int lane) {
-    const int h = lane >> 5;
-    Bias4 b;
-#pragma unroll
-    for (int j = 0; j < 4; j++) b.v[j] = *reinterpret_cast<const float4 *>(bias + n0 + 8 * j + 4 * h);
-    return b;
+__device__ inline Tile16 tile16(const float *dst, size_t Ns, int row0, int p0, int lane) {
+    const float *base = dst + (size_t)row0 * Ns + p0;
+    return Tile16{__builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(base), 0, 0x7fffffff, 0x00020000),
+                  (4 * (lane >> 4) * (int)Ns + (lane & 15)) * 4, (int)Ns * 4};
 }
 
-__device__ inline void bias_relu(f32x16 &acc, const Bias4 &b) {
+// relu' bits of a wave's 16 x 64 tile: bit 4q + i of lane (kq, col) = [row 4kq + i of point 16q + col
+// > 0] (signed clamp of the float bits: -0.0 and +0.0 give 0); the backward's tiles have the same map
+__device__ inline uint32_t relu_bits(const f32x4 (&v)[NQ]) {
+    uint32_t w = 0;
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-        acc[4 * j] = fmaxf(acc[4 * j] + b.v[j].x, 0.f);
-        acc[4 * j + 1] = fmaxf(acc[4 * j + 1] + b.v[j].y, 0.f);
-        acc[4 * j + 2] = fmaxf(acc[4 * j + 2] + b.v[j].z, 0.f);
-        acc[4 * j + 3] = fmaxf(acc[4 * j + 3] + b.v[j].w, 0.f);
+    for (int q = 0; q < NQ; q++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) w |= (uint32_t)min(max(__float_as_int(v[q][i]), 0), 1) << (4 * q + i);
+    return w;
+}
+
+__device__ inline void mask_apply(f32x4 (&v)[NQ], uint32_t bits) {
+#pragma unroll
+    for (int q = 0; q < NQ; q++)
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            v[q][i] = __int_as_float(__float_as_int(v[q][i]) & __builtin_amdgcn_sbfe((int)bits, 4 * q + i, 1));
+}
+
+// this lane's 4 rows (16r + 4kq .. +3) of a padded bias vector
+__device__ inline float4 load_bias4(const float *bias, int r, int lane) {
+    return *reinterpret_cast<const float4 *>(bias + 16 * r + 4 * (lane >> 4));
+}
+
+__device__ inline void bias_relu(f32x4 (&v)[NQ], float4 b, bool relu) {
+#pragma unroll
+    for (int q = 0; q < NQ; q++) {
+        v[q][0] += b.x;
+        v[q][1] += b.y;
+        v[q][2] += b.z;
+        v[q][3] += b.w;
+        if (relu)
+#pragma unroll
+            for (int i = 0; i < 4; i++) v[q][i] = fmaxf(v[q][i], 0.f);
     }
+}
+
+__device__ inline void zero_tiles(f32x4 (&v)[NQ]) {
+#pragma unroll
+    for (int q = 0; q < NQ; q++) v[q] = zero4();
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -286,7 +288,7 @@ struct FwdArgs {
     const float *fp;    // fp32 region: biases, timenet weights
     float *out;
     float *saved;
-    uint32_t *mask;     // relu' bits, [32-point tile][nmask] words (after the saved rows)
+    uint32_t *mask;     // relu' bits, [64-point block][row / 16][64 lanes] u16 (after the saved rows)
     float *tc;          // timenet of t[0] (k_timenet), or nullptr
     int fT1, fT2, fL[8], fHd;      // image k-slots
     int bT1, bT2, bL[8], bHd;      // fp32 offsets
@@ -343,16 +345,17 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
     __shared__ bf16x8 lds[G_FWD * UG];
     float *lf = reinterpret_cast<float *>(lds);
     float *stage = lf + G_H * UG * 4;  // fp32 [112][BM] feature staging (H region, before the trunk)
-    float *part = stage;               // PART slots alias the H region too
     const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform
-    const int w = wave & 7, ct = wave >> 3;                      // n-tile, column tile
+    const int r = __builtin_amdgcn_readfirstlane(tid >> 6);  // n-tile of this wave (provably uniform)
+    const int kq = lane >> 4, col = lane & 15;
     const int p0 = blockIdx.x * BM;
     const Flags F = make_flags(a.flags);
     const size_t Ns = a.Ns;
     const __amdgpu_buffer_rsrc_t mrsrc = __builtin_amdgcn_make_buffer_rsrc(
-        a.mask + (SAVE ? (size_t)(blockIdx.x * NT + ct) * F.nmask : 0), 0, 0x7fffffff, 0x00020000);
-    const int pw = p0 + 32 * ct;  // first point of this wave's column tile
+        a.mask + (SAVE ? (size_t)blockIdx.x * 2 * F.nmask : 0), 0, 0x7fffffff, 0x00020000);
+    auto store_mask = [&](uint32_t w, int mr) {  // mask tile mr (= row / 16)
+        __builtin_amdgcn_raw_buffer_store_b16((unsigned short)w, mrsrc, lane * 2, mr * 128, 0);
+    };
     DGS_STAMP(0);
     // frame-uniform t: all 64 points of the block carry k_timenet's t0 (every wave checks the same
     // 64 values, so the branch is block-uniform without a barrier)
@@ -366,7 +369,7 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
     // ---- positional encodings (utils/time_utils.py:42-54) into fp32 staging: feature 3 band + d,
     // band 0 = x, band 1 + 2i = sin(2^i x), band 2 + 2i = cos(2^i x) ----
     for (int e = tid; e < BM * 3 * 11; e += NTHR) {
-        const int m = e % BM, r = e / BM, d = r % 3, i = r / 3;  // i = 10: identity band
+        const int m = e % BM, rr = e / BM, d = rr % 3, i = rr / 3;  // i = 10: identity band
         const int p = p0 + m;
         const bool ok = p < a.N;
         const float x = ok ? a.xyz[3 * p + d] : 0.f;
@@ -429,54 +432,39 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
             for (int j = 0; j < 8; j++) v[j] = stage[(8 * g + j) * BM + m];
             put_unit8(lds, g < 12 ? g : G_TIN + g - 12, m, v);
         }
+        if (F.blender)  // TIN k-step padding (features 16..31): zero, not stale LDS
+            for (int u = tid; u < 2 * UG; u += NTHR) lds[(G_TIN + 2) * UG + u] = bf16x8{};
     }
     lds_barrier();
     DGS_STAMP(1);
-    f32x16 kt = zero16();  // previous layer's activations, awaiting their store
+    f32x4 c[NQ];
     if (SAVE && uniform_t && !F.uniform_t) {  // TH tile from k_timenet: relu' bits + saved rows (per-point backward)
-        const Bias4 th = load_bias(a.tc + TC_TH, w * 32, lane);
-        f32x16 c;
+        const float4 th = load_bias4(a.tc + TC_TH, r, lane);
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            c[4 * j] = th.v[j].x;
-            c[4 * j + 1] = th.v[j].y;
-            c[4 * j + 2] = th.v[j].z;
-            c[4 * j + 3] = th.v[j].w;
-        }
-        store_mask_bits(c, mrsrc, (M_TH + w * 32) * 4, lane);
-        Stash{c, tile_addr(a.saved, Ns, S_TH, w * 32, pw, lane)}.store_all();
+        for (int q = 0; q < NQ; q++) c[q] = f32x4{th.x, th.y, th.z, th.w};
+        store_mask(relu_bits(c), MR_TH + r);
+        tile16(a.saved, Ns, S_TH + 16 * r, p0, lane).store(c);
     }
     // ---- per-point timenet (blender, t not frame-uniform): Linear(13,256)+ReLU -> H; Linear(256,30) -> TE
     if (F.blender && !uniform_t) {
-        f32x16 c = zero16();
-        const Bias4 tb = load_bias(a.fp + a.bT1, w * 32, lane);
-        gemm<1>(a.img + (size_t)(a.fT1 + w) * KSLOT, 0, lds, G_TIN, ct, lane, c);
-        bias_relu(c, tb);
-        if (SAVE) store_mask_bits(c, mrsrc, (M_TH + w * 32) * 4, lane);
-        acc_to_lds(c, lds, G_H + 4 * w, ct, lane);
-        lds_barrier();
-        f32x16 c2 = zero16();
-        if (SAVE)
-            gemm<2>(a.img + (size_t)a.fT2 * KSLOT, 2 * w, lds, G_H, ct, lane, c2, NoPre(),
-                    Stash{c, tile_addr(a.saved, Ns, S_TH, w * 32, pw, lane)});
-        else
-            gemm<2>(a.img + (size_t)a.fT2 * KSLOT, 2 * w, lds, G_H, ct, lane, c2);
-        lds_barrier();  // every wave finished reading TH
-        acc_to_part(c2, part, w, ct, lane);
-        lds_barrier();
-        for (int u = tid; u < 4 * BM; u += NTHR) {  // TE = sum of the 8 K-parts + bias
-            const int g = u / BM, m = u % BM;
-            float v[8];
+        zero_tiles(c);
+        gemm<1, NQ>(a.img + (size_t)(a.fT1 + r) * KSLOT, lds, G_TIN, 0, lane, c);
+        bias_relu(c, load_bias4(a.fp + a.bT1, r, lane), true);
+        if (SAVE) {
+            store_mask(relu_bits(c), MR_TH + r);
+            tile16(a.saved, Ns, S_TH + 16 * r, p0, lane).store(c);
+        }
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const int row = 8 * g + j;
-                float s = part[row * BM + m];
-#pragma unroll
-                for (int q = 1; q < NPART; q++) s += part[(q * 32 + row) * BM + m];
-                v[j] = s + a.fp[a.bT2 + row];
-                if (SAVE) a.saved[(size_t)(S_TE + row) * Ns + p0 + m] = v[j];
-            }
-            put_unit8(lds, G_TE + g, m, v);
+        for (int q = 0; q < NQ; q++) acc_to_lds(c[q], lds, G_H, r, q, lane);
+        lds_barrier();
+        if (r < 8) {  // TE tile (n-tile r >> 2 of 2, column tile r & 3), full K on one wave
+            const int nt = r >> 2, q = r & 3;
+            f32x4 c1[1] = {zero4()};
+            gemm<8, 1>(a.img + (size_t)(a.fT2 + nt * 8) * KSLOT, lds, G_H, q, lane, c1);
+            const float4 b = load_bias4(a.fp + a.bT2, nt, lane);
+            c1[0] += f32x4{b.x, b.y, b.z, b.w};
+            if (SAVE) tile16(a.saved, Ns, S_TE + 16 * nt, p0, lane).store(c1, q);
+            acc_to_lds(c1[0], lds, G_TE, nt, q, lane);  // TE groups: not read by the T2 GEMM
         }
         lds_barrier();
     }
@@ -484,60 +472,42 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
 #pragma unroll 1
     for (int L = 0; L < 8; L++) {
         const int g0 = (L == 0 || L == 5) ? G_XE : G_H;
-        const int nk = layer_kpad(L) / 16;
-        f32x16 c = zero16();
-        const bf16x8 *Aw = a.img + (size_t)(a.fL[L] + w * nk) * KSLOT;
-        if (L == 0) {
-            gemm<6>(Aw, 0, lds, g0, ct, lane, c);
-        } else {
-            const Stash st{kt, tile_addr(a.saved, Ns, s_h(L - 1), w * 32, pw, lane)};
-            if (L == 5) {
-                if (SAVE) gemm<22>(Aw, 0, lds, g0, ct, lane, c, NoPre(), st);
-                else gemm<22>(Aw, 0, lds, g0, ct, lane, c);
-            } else {
-                if (SAVE) gemm<16>(Aw, 0, lds, g0, ct, lane, c, NoPre(), st);
-                else gemm<16>(Aw, 0, lds, g0, ct, lane, c);
-            }
-        }
+        const int nk = layer_kpad(L) / 32;
+        zero_tiles(c);
+        const bf16x8 *Aw = a.img + (size_t)(a.fL[L] + r * nk) * KSLOT;
+        if (L == 0) gemm<3, NQ>(Aw, lds, g0, 0, lane, c);
+        else if (L == 5) gemm<11, NQ>(Aw, lds, g0, 0, lane, c);
+        else gemm<8, NQ>(Aw, lds, g0, 0, lane, c);
         DGS_STAMP(4 + 2 * L);
-        const Bias4 bv = load_bias(a.fp + a.bL[L], w * 32, lane);  // in flight across the barrier
+        const float4 bv = load_bias4(a.fp + a.bL[L], r, lane);  // in flight across the barrier
         lds_barrier();  // all waves finished reading H before it is overwritten
-#ifndef DGS_DIAG_NO_EPI  // timing experiment only (wrong results): no bias/relu/mask/split epilogue
-        bias_relu(c, bv);
-        if (SAVE) store_mask_bits(c, mrsrc, (m_h(L) + w * 32) * 4, lane);
-        acc_to_lds(c, lds, G_H + 4 * w, ct, lane);
-#endif
+        bias_relu(c, bv, true);
+        if (SAVE) {
+            store_mask(relu_bits(c), 16 * L + r);
+            tile16(a.saved, Ns, s_h(L) + 16 * r, p0, lane).store(c);
+        }
+#pragma unroll
+        for (int q = 0; q < NQ; q++) acc_to_lds(c[q], lds, G_H, r, q, lane);
         lds_barrier();
         DGS_STAMP(5 + 2 * L);
-        kt = c;
     }
-    // ---- heads (no activation): [warp | branch_w, branch_v], rotation, scaling; K split over waves ----
-    {
-        f32x16 c = zero16();
-        if (SAVE)
-            gemm<2>(a.img + (size_t)a.fHd * KSLOT, 2 * w, lds, G_H, ct, lane, c, NoPre(),
-                    Stash{kt, tile_addr(a.saved, Ns, s_h(7), w * 32, pw, lane)});
-        else
-            gemm<2>(a.img + (size_t)a.fHd * KSLOT, 2 * w, lds, G_H, ct, lane, c);
-        lds_barrier();
-        acc_to_part(c, part, w, ct, lane);
-        lds_barrier();
-    }
-    DGS_STAMP(20);
-    for (int e = tid; e < F.nout * BM; e += NTHR) {
-        const int cc = e % F.nout, m = e / F.nout;
-        const int p = p0 + m;
-        float s = part[cc * BM + m];
+    // ---- heads (no activation): [warp | branch_w, branch_v], rotation, scaling: 16 rows (nout <= 13),
+    // one column tile per wave on waves 0-3 ----
+    if (r < NQ) {
+        f32x4 c1[1] = {zero4()};
+        gemm<8, 1>(a.img + (size_t)a.fHd * KSLOT, lds, G_H, r, lane, c1);
+        const float4 b = load_bias4(a.fp + a.bHd, 0, lane);
+        c1[0] += f32x4{b.x, b.y, b.z, b.w};
+        const int p = p0 + 16 * r + col;
 #pragma unroll
-        for (int q = 1; q < NPART; q++) s += part[(q * 32 + cc) * BM + m];
-        if (p < a.N) a.out[(size_t)p * F.nout + cc] = s + a.fp[a.bHd + cc];
+        for (int i = 0; i < 4; i++)
+            if (p < a.N && 4 * kq + i < F.nout) a.out[(size_t)p * F.nout + 4 * kq + i] = c1[0][i];
     }
     DGS_STAMP(21);
 #ifdef DGS_MLP_PROFILE
-    if (threadIdx.x == 0) {  // shader-clock rate: s_memtime vs the 100 MHz s_memrealtime
+    if (threadIdx.x == 0) {
         dgs_mlps_prof[blockIdx.x * 64 + 60] = __builtin_amdgcn_s_memrealtime();
         dgs_mlps_prof[blockIdx.x * 64 + 61] = __builtin_amdgcn_s_memtime();
-        dgs_mlps_prof[blockIdx.x * 64 + 62] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));  // HW_ID-ish
     }
 #endif
 }
@@ -556,26 +526,28 @@ struct BwdArgs {
     int flags;
 };
 
-// relu' bits of the layer input for this wave's 32x32 tile, loaded ahead of the GEMM
+// relu' bits of the layer input for this wave's 16 x 64 tile, loaded ahead of the GEMM
 struct MaskPre {
     uint32_t *mk;
-    const uint32_t *words;  // &mask[32-point tile][mrow0 + n0]
+    const unsigned short *tile;  // &mask[block][mr][0]
     int lane;
-    __device__ void operator()() const { *mk = reinterpret_cast<const unsigned short *>(words)[lane]; }
+    __device__ void operator()() const { *mk = tile[lane]; }
 };
 
+// TE_ROWS: per-point dL/dt_emb (blender, t not frame-uniform); the other instantiation carries no
+// t_emb registers or code (raw t PE has no parameters upstream; uniform t: k_tgrad)
+template <bool TE_ROWS>
 __global__ __launch_bounds__(NTHR) void k_bwd(BwdArgs a) {
     __shared__ bf16x8 lds[G_BWD * UG];
     float *lf = reinterpret_cast<float *>(lds);
     float *stage = lf + G_BH * UG * 4;  // fp32 [32][BM] (H region, before the first dZ)
-    float *part = stage;                // PART slots alias the H region (layer 0 only)
     const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int w = wave & 7, ct = wave >> 3;  // n-tile, column tile
-    const int p0 = blockIdx.x * BM, pw = p0 + 32 * ct;
+    const int r = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int p0 = blockIdx.x * BM;
     const Flags F = make_flags(a.flags);
     const size_t Ns = a.Ns;
-    const uint32_t *mwords = a.mask + (size_t)(blockIdx.x * NT + ct) * F.nmask + w * 32;  // + mask row
+    const unsigned short *mtiles = reinterpret_cast<const unsigned short *>(a.mask + (size_t)blockIdx.x * 2 * F.nmask);
+    auto mask_tile = [&](int mr) { return mtiles + (size_t)mr * 64; };
     // dOut -> dz rows Z_G (heads' dW) and the split G image
     for (int e = tid; e < 32 * BM; e += NTHR) {
         const int c = e / BM, m = e % BM;
@@ -593,66 +565,53 @@ __global__ __launch_bounds__(NTHR) void k_bwd(BwdArgs a) {
         put_unit8(lds, G_BG + g, m, v);
     }
     lds_barrier();
-    f32x16 kt;  // dZ of the layer whose GEMM runs next
+    f32x4 c[NQ];
     // heads^T: dH7 = W_h^T dOut (K = 32 from G) -> mask H7 -> dZ7
     {
         uint32_t mk;
-        f32x16 c = zero16();
-        gemm<2>(a.img + (size_t)(a.tHd + w * 2) * KSLOT, 0, lds, G_BG, ct, lane, c, MaskPre{&mk, mwords + m_h(7), lane});
+        zero_tiles(c);
+        gemm<1, NQ>(a.img + (size_t)(a.tHd + r) * KSLOT, lds, G_BG, 0, lane, c, MaskPre{&mk, mask_tile(16 * 7 + r), lane});
         mask_apply(c, mk);
-        acc_to_lds(c, lds, G_BH + 4 * w, ct, lane);
-        kt = c;
+        tile16(a.dz, Ns, Z_L0 + 7 * 256 + 16 * r, p0, lane).store(c);
+#pragma unroll
+        for (int q = 0; q < NQ; q++) acc_to_lds(c[q], lds, G_BH, r, q, lane);
         lds_barrier();
     }
-    f32x16 ct_te = zero16();  // dL/dt_emb partial (blender): this wave's K-part of layers 5 and 0
+    f32x4 te5[1] = {zero4()};  // t_emb tile of layer 5's dX (waves 0-7, TE_ROWS)
 #pragma unroll 1
     for (int L = 7; L >= 1; L--) {
-        // dX_L = W_L^T dZ_L; the H-part rows of the padded L5 input are n-tiles F_H/32 + w
-        const int tile0 = (L == 5) ? F_H / 32 : 0;
-        if (L == 5 && F.blender && !F.uniform_t)  // t_emb rows (padded 64..95 = n-tile 2), K split over n-tiles
-            gemm<2>(a.img + (size_t)(a.tL[5] + (F_TE / 32) * 16) * KSLOT, 2 * w, lds, G_BH, ct, lane, ct_te);
+        // dX_L = W_L^T dZ_L; the H-part rows of the padded L5 input are n-tiles F_H / 16 + r
+        if (TE_ROWS && L == 5 && r < 8)  // t_emb rows (padded 64..95 = n-tiles 4, 5) x column tile r & 3
+            gemm<8, 1>(a.img + (size_t)(a.tL[5] + (F_TE / 16 + (r >> 2)) * 8) * KSLOT, lds, G_BH, r & 3, lane, te5);
+        const int tile0 = (L == 5) ? F_H / 16 : 0;
         uint32_t mk;
-        f32x16 c = zero16();
-        gemm<16>(a.img + (size_t)(a.tL[L] + (tile0 + w) * 16) * KSLOT, 0, lds, G_BH, ct, lane, c,
-                 MaskPre{&mk, mwords + m_h(L - 1), lane}, Stash{kt, tile_addr(a.dz, Ns, Z_L0 + L * 256, w * 32, pw, lane)});
+        zero_tiles(c);
+        gemm<8, NQ>(a.img + (size_t)(a.tL[L] + (tile0 + r) * 8) * KSLOT, lds, G_BH, 0, lane, c,
+                    MaskPre{&mk, mask_tile(16 * (L - 1) + r), lane});
         lds_barrier();
         mask_apply(c, mk);
-        acc_to_lds(c, lds, G_BH + 4 * w, ct, lane);
-        kt = c;
+        tile16(a.dz, Ns, Z_L0 + (L - 1) * 256 + 16 * r, p0, lane).store(c);
+#pragma unroll
+        for (int q = 0; q < NQ; q++) acc_to_lds(c[q], lds, G_BH, r, q, lane);
         lds_barrier();
     }
-    const Stash dz0{kt, tile_addr(a.dz, Ns, Z_L0, w * 32, pw, lane)};
-    if (!F.blender || F.uniform_t) {  // raw t PE: no parameters upstream; uniform t: k_tgrad
-        dz0.store_all();
-        return;
-    }
-    // layer 0: t_emb rows of W_0^T dZ_0 (K split), dZ_0 stored under it; then sum the K-parts
-    gemm<2>(a.img + (size_t)(a.tL[0] + (F_TE / 32) * 16) * KSLOT, 2 * w, lds, G_BH, ct, lane, ct_te, NoPre(), dz0);
-    lds_barrier();
-    acc_to_part(ct_te, part, w, ct, lane);
-    lds_barrier();
-    if (tid < 4 * BM) {  // dTE (30 real rows) -> dz rows Z_TE (timenet.2's dW) and the split G image
-        const int g = tid / BM, m = tid % BM;
-        float v[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const int row = 8 * g + j;
-            float s = part[row * BM + m];
-#pragma unroll
-            for (int q = 1; q < NPART; q++) s += part[(q * 32 + row) * BM + m];
-            v[j] = s;
-            a.dz[(size_t)(Z_TE + row) * Ns + p0 + m] = s;
-        }
-        put_unit8(lds, G_BG + g, m, v);
+    if (!TE_ROWS) return;
+    // layer 0's t_emb rows added to layer 5's: dTE tile (n-tile r >> 2, column tile r & 3) -> dz rows
+    // Z_TE (timenet.2's dW) and the split G image (dOut's, no longer read)
+    if (r < 8) {
+        const int nt = r >> 2, q = r & 3;
+        gemm<8, 1>(a.img + (size_t)(a.tL[0] + (F_TE / 16 + nt) * 8) * KSLOT, lds, G_BH, q, lane, te5);
+        tile16(a.dz, Ns, Z_TE + 16 * nt, p0, lane).store(te5, q);
+        acc_to_lds(te5[0], lds, G_BG, nt, q, lane);
     }
     lds_barrier();
     // timenet.2^T: dTH = W_T2^T dTE (K = 32) -> mask TH -> dZ_T1
     {
         uint32_t mk;
-        f32x16 c = zero16();
-        gemm<2>(a.img + (size_t)(a.tT2 + w * 2) * KSLOT, 0, lds, G_BG, ct, lane, c, MaskPre{&mk, mwords + M_TH, lane});
+        zero_tiles(c);
+        gemm<1, NQ>(a.img + (size_t)(a.tT2 + r) * KSLOT, lds, G_BG, 0, lane, c, MaskPre{&mk, mask_tile(MR_TH + r), lane});
         mask_apply(c, mk);
-        Stash{c, tile_addr(a.dz, Ns, Z_T1, w * 32, pw, lane)}.store_all();
+        tile16(a.dz, Ns, Z_T1 + 16 * r, p0, lane).store(c);
     }
 }
 
@@ -701,6 +660,18 @@ constexpr int OPND = NSPLIT * PLANE;   // bf16 per operand
 constexpr int DW_LDS = 2 * 2 * OPND * 2;  // bytes: 2 buffers x (A, B)
 constexpr int DW_THREADS = 512;
 static_assert(DW_LDS <= 160 * 1024, "dW LDS");
+
+#define MFMA32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
+
+// the six split products into one 32x32 accumulator, smallest first
+__device__ inline void mma6_1(const AFrag &a, const AFrag &b, f32x16 &c) {
+    c = MFMA32(a.m, b.m, c);
+    c = MFMA32(a.h, b.l, c);
+    c = MFMA32(a.l, b.h, c);
+    c = MFMA32(a.h, b.m, c);
+    c = MFMA32(a.m, b.h, c);
+    c = MFMA32(a.h, b.h, c);
+}
 
 __device__ inline AFrag load_plane_frag(const __bf16 *op, int row, int h) {
     const __bf16 *p = op + row * PITCH + 8 * h;
@@ -940,9 +911,9 @@ Plan make_plan(int flags) {
     const Seg full = seg(0, 256, 0), one = seg(0, 1, 0);
     if (F.blender) {
         const Seg st = seg(0, F.tin, 0), s30 = seg(0, 30, 0);
-        P.fT1 = new_img(P.pT0w, 0, 8, 1, 1, &full, 1, &st);
-        P.fT2 = new_img(P.pT2w, 0, 1, 16, 1, &s30, 1, &full);
-        P.tT2 = new_img(P.pT2w, 1, 8, 2, 1, &full, 1, &s30);  // A[n = TH feature][f = TE feature]
+        P.fT1 = new_img(P.pT0w, 0, 16, 1, 1, &full, 1, &st);   // K = TIN (13) padded to one k-step
+        P.fT2 = new_img(P.pT2w, 0, 2, 8, 1, &s30, 1, &full);
+        P.tT2 = new_img(P.pT2w, 1, 16, 1, 1, &full, 1, &s30);  // A[n = TH feature][f = TE feature]
         P.bT1 = new_f32(P.pT0b, 256, 1, 1, &full, 1, &one);
         P.bT2 = new_f32(P.pT2b, 32, 1, 1, &s30, 1, &one);
         P.wT1 = new_f32(P.pT0w, 256, 16, 1, &full, 1, &st);
@@ -955,22 +926,22 @@ Plan make_plan(int flags) {
         Seg s[3];
         const int ns = layer_in_segs(F, i, s);
         const int kp = layer_kpad(i);
-        P.fL[i] = new_img(P.pLw[i], 0, 8, kp / 16, 1, &full, ns, s);
-        P.tL[i] = new_img(P.pLw[i], 1, kp / 32, 16, ns, s, 1, &full);  // rows = padded input features
+        P.fL[i] = new_img(P.pLw[i], 0, 16, kp / 32, 1, &full, ns, s);
+        P.tL[i] = new_img(P.pLw[i], 1, kp / 16, 8, ns, s, 1, &full);  // rows = padded input features
         P.bL[i] = new_f32(P.pLb[i], 256, 1, 1, &full, 1, &one);
     }
-    // heads: rows stacked in output order in one 32-row image each way
+    // heads: rows stacked in output order (nout <= 13) in one 16-row image each way
     P.fHd = P.nslots;
-    P.nslots += 16;
+    P.nslots += 8;   // 1 n-tile x 8 k-steps
     P.tHd = P.nslots;
-    P.nslots += 16;  // 8 n-tiles x 2 k-steps
+    P.nslots += 16;  // 16 n-tiles x 1 k-step (K = head rows padded to 32)
     P.bHd = P.nf32;
     P.nf32 += 32;
     int r0 = 0;
     for (int h = 0; h < P.nheads; h++) {
         const Seg sr = seg(r0, P.hrows[h], 0);
-        img(P.pHw[h], 0, 1, 16, 1, &sr, 1, &full, P.fHd);
-        img(P.pHw[h], 1, 8, 2, 1, &full, 1, &sr, P.tHd);
+        img(P.pHw[h], 0, 1, 8, 1, &sr, 1, &full, P.fHd);
+        img(P.pHw[h], 1, 16, 1, 1, &full, 1, &sr, P.tHd);
         f32(P.pHb[h], 32, 1, 1, &sr, 1, &one, P.bHd);
         r0 += P.hrows[h];
     }
@@ -1016,8 +987,8 @@ static std::vector<int> build_pack_map(const Plan &P) {
         for (int idx = 0; idx < j.ntiles * j.nk * 512; idx++) {
             const int e = idx & 7, lane = (idx >> 3) & 63, slot = idx >> 9;
             const int k = slot % j.nk, ntile = slot / j.nk;
-            const int n = ntile * 32 + (lane & 31);
-            const int f = 16 * k + 8 * (lane >> 5) + e;
+            const int n = ntile * 16 + (lane & 15);  // v_mfma_f32_16x16x32_bf16 A map
+            const int f = 32 * k + 8 * (lane >> 4) + e;
             const int sn = seg_lookup(j.segn, j.nseg_n, n);
             const int sf = seg_lookup(j.segf, j.nseg_f, f);
             if (sn >= 0 && sf >= 0)
@@ -1156,7 +1127,10 @@ int backward(int flags, int N, const float *packed, const float *saved, const fl
     b.flags = flags;
     {
         ScopedTimer tm("mlp_bwd", stream);
-        hipLaunchKernelGGL(k_bwd, dim3(div_up(N, BM)), dim3(NTHR), 0, stream, b);
+        if (F.blender && !F.uniform_t)
+            hipLaunchKernelGGL(k_bwd<true>, dim3(div_up(N, BM)), dim3(NTHR), 0, stream, b);
+        else
+            hipLaunchKernelGGL(k_bwd<false>, dim3(div_up(N, BM)), dim3(NTHR), 0, stream, b);
     }
     DGS_LAUNCH_CHECK("k_bwd", false, stream);
     int rc;
