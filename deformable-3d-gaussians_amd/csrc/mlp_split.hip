@@ -630,13 +630,24 @@ struct TGradArgs {
 };
 
 __global__ __launch_bounds__(256) void k_tgrad(TGradArgs a) {
-    __shared__ float S[32];
+    __shared__ float S[32], gb[512];
     const int j = threadIdx.x;
-    if (j < 32) {
+    gb[j] = a.gb0[j];
+    gb[256 + j] = a.gb5[j];
+    __syncthreads();
+    {  // S[k]: 8 lanes per k, each over 64 of the 512 (n, layer) terms, then a fixed xor tree
+        const int k = j >> 3, part = j & 7;
         float s = 0.f;
-        for (int n = 0; n < 256; n++) s = fmaf(a.fp[a.w0te + n * 32 + j], a.gb0[n], s);
-        for (int n = 0; n < 256; n++) s = fmaf(a.fp[a.w5te + n * 32 + j], a.gb5[n], s);
-        S[j] = s;
+#pragma unroll 8
+        for (int i = 0; i < 64; i++) {
+            const int n = part * 64 + i;  // n < 256: linear.0, else linear.5
+            const float w = n < 256 ? a.fp[a.w0te + n * 32 + k] : a.fp[a.w5te + (n - 256) * 32 + k];
+            s = fmaf(w, gb[n], s);
+        }
+        s += __shfl_xor(s, 1);
+        s += __shfl_xor(s, 2);
+        s += __shfl_xor(s, 4);
+        if (part == 0) S[k] = s;
     }
     __syncthreads();
     const float th = a.tc[TC_TH + j];

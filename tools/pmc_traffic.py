@@ -14,8 +14,9 @@ import os
 import sys
 from collections import defaultdict
 
-CLASSES = {  # bench.py kernel class -> substring of the device symbol
-    "mlp_fwd": "k_mlp_fwd", "mlp_bwd": "k_mlp_bwd", "mlp_dw": "mlp4k_dw", "mlp_dw_reduce": "k_dw_reduce",
+CLASSES = {  # bench.py kernel class -> substring(s) of the device symbol (split-bf16 | exact-fp32 MLP)
+    "mlp_fwd": ("mlps::k_fwd", "k_mlp_fwd"), "mlp_bwd": ("mlps::k_bwd", "k_mlp_bwd"),
+    "mlp_dw": ("mlp::k_dw(", "mlps::k_dw(", "mlp4k_dw"), "mlp_dw_reduce": "k_dw_reduce",
     "preprocess_fwd": "k_preprocess(", "duplicate": "k_duplicate", "ranges": "k_ranges",
     "blend_fwd": "k_blend_fwd", "blend_bwd": "k_blend_bwd", "preprocess_bwd": "k_preprocess_bwd",
     "ssim_fwd": "k_ssim_fwd", "ssim_bwd": "k_ssim_bwd", "adam": "k_adam", "inputs_fwd": "k_inputs_fwd",
@@ -38,9 +39,12 @@ def main():
     write = load(os.path.join(root, "pmc_WRITE_SIZE", "run_counter_collection.csv"), "WRITE_SIZE")
     out = {}
     for cls, sub in CLASSES.items():
-        # mangled names: match on the readable part rocprofv3 prints
-        fk = [k for k in fetch if sub.replace("mlp4k_dw", "k_dw(") in k and ("k_dw_reduce" not in k or cls == "mlp_dw_reduce")]
-        wk = [k for k in write if sub.replace("mlp4k_dw", "k_dw(") in k and ("k_dw_reduce" not in k or cls == "mlp_dw_reduce")]
+        subs = sub if isinstance(sub, tuple) else (sub,)
+
+        def match(k):  # the readable part of the symbol rocprofv3 prints
+            return any(x in k for x in subs) and ("k_dw_reduce" not in k or cls == "mlp_dw_reduce")
+        fk = [k for k in fetch if match(k)]
+        wk = [k for k in write if match(k)]
         if not fk or not wk:
             continue
         fv = [v for k in fk for v in fetch[k]]
