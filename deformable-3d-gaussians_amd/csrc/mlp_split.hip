@@ -129,15 +129,15 @@ __device__ inline AFrag load_b(const bf16x8 *p, int q) { return AFrag{p[16 * q],
 __device__ inline f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
 // The six split products of one k-step: hh into the running accumulator, the five corrections
-// (|.| <= 2^-8 |hh|) into a fresh one added in fp32 (see the numerics note above).
-__device__ inline void mma6(const AFrag &a, const AFrag &b, f32x4 &acc) {
-    f32x4 t = MF16(a.m, b.m, zero4());
-    t = MF16(a.h, b.l, t);
-    t = MF16(a.l, b.h, t);
-    t = MF16(a.h, b.m, t);
-    t = MF16(a.m, b.h, t);
+// (|.| <= 2^-8 |hh|) into their own accumulator, added in fp32 once per GEMM (see the numerics note:
+// at 2^-8 of the sum's magnitude the corrections lose nothing in their own C)
+__device__ inline void mma6(const AFrag &a, const AFrag &b, f32x4 &acc, f32x4 &lo) {
+    lo = MF16(a.m, b.m, lo);
+    lo = MF16(a.h, b.l, lo);
+    lo = MF16(a.l, b.h, lo);
+    lo = MF16(a.h, b.m, lo);
+    lo = MF16(a.m, b.h, lo);
     acc = MF16(a.h, b.h, acc);
-    acc += t;
 }
 
 #ifdef DGS_MLP_PROFILE  // diagnostic build only (tools/mlp_phase.py): per-phase s_memtime stamps
@@ -182,6 +182,9 @@ __device__ inline void gemm(const bf16x8 *__restrict__ Aw, const bf16x8 *lds, in
         if (k < NK) ring[k] = load_a(Ap + k * AK);
     pre();
     AFrag b = load_b(Bp, 0);
+    f32x4 lo[NQ_];
+#pragma unroll
+    for (int q = 0; q < NQ_; q++) lo[q] = zero4();
 #pragma unroll
     for (int k = 0; k < NK; k++) {
         __builtin_amdgcn_sched_barrier(0);
@@ -191,12 +194,14 @@ __device__ inline void gemm(const bf16x8 *__restrict__ Aw, const bf16x8 *lds, in
             AFrag nb;
             if (q + 1 < NQ_) nb = load_b(Bp + k * BK, q + 1);
             else if (k + 1 < NK) nb = load_b(Bp + (k + 1) * BK, 0);
-            mma6(ring[k % RING], b, acc[q]);
+            mma6(ring[k % RING], b, acc[q], lo[q]);
             if (q + 1 < NQ_ || k + 1 < NK) b = nb;
         }
         if (k + RING < NK) ring[k % RING] = load_a(Ap + (k + RING) * AK);
         __builtin_amdgcn_sched_barrier(0);
     }
+#pragma unroll
+    for (int q = 0; q < NQ_; q++) acc[q] += lo[q];
 }
 
 // accumulator tile q (rows 16r + 4kq + i of this wave, point 16q + col) -> its 8-byte half of the
@@ -349,6 +354,9 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
     const int r = __builtin_amdgcn_readfirstlane(tid >> 6);  // n-tile of this wave (provably uniform)
     const int kq = lane >> 4, col = lane & 15;
     const int p0 = blockIdx.x * BM;
+#ifdef DGS_DIAG_PRIO  // experiment: static priority for the second-dispatched half (MI355X_MICROARCH.md)
+    if (r >= 8) __builtin_amdgcn_s_setprio(1);
+#endif
     const Flags F = make_flags(a.flags);
     const size_t Ns = a.Ns;
     const __amdgpu_buffer_rsrc_t mrsrc = __builtin_amdgcn_make_buffer_rsrc(
@@ -481,6 +489,7 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
         DGS_STAMP(4 + 2 * L);
         const float4 bv = load_bias4(a.fp + a.bL[L], r, lane);  // in flight across the barrier
         lds_barrier();  // all waves finished reading H before it is overwritten
+#ifndef DGS_DIAG_NO_EPI  // timing experiment only (wrong results): no bias/relu/mask/split/store epilogue
         bias_relu(c, bv, true);
         if (SAVE) {
             store_mask(relu_bits(c), 16 * L + r);
@@ -488,6 +497,7 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
         }
 #pragma unroll
         for (int q = 0; q < NQ; q++) acc_to_lds(c[q], lds, G_H, r, q, lane);
+#endif
         lds_barrier();
         DGS_STAMP(5 + 2 * L);
     }

@@ -27,7 +27,7 @@ def main():
         torch.manual_seed(0)
         net = DeformNetworkBaseline(is_blender=True, exact_fp32=exact).to(dev)
         x = torch.rand(a.n, 3, device=dev) * 2.6 - 1.3
-        t = torch.full((a.n, 1), 0.3, device=dev)
+        t = torch.full((1, 1), 0.3, device=dev).expand(a.n, -1)  # one frame time (training path)
         for it in range(a.iters + 2):
             if it == 2:
                 torch.cuda.synchronize()
