@@ -866,6 +866,189 @@ __global__ __launch_bounds__(DW_THREADS) void k_dw(WJobs JT, size_t Ns, const fl
 }
 
 // ------------------------------------------------------------------------------------------------
+// dW = dZ X^T on split bf16 with LDS-DMA staging (k_dwg). The fp32 dZ / X rows stream global ->
+// LDS through global_load_lds_dwordx4 (no VGPR staging, no staging VALU, no lock-step store
+// phase): 32 points (two 16-point k-steps) per chunk, two buffers, ONE barrier per chunk, the next
+// chunk's DMA in flight during this chunk's MFMAs. Each wave splits its fp32 fragments in registers
+// right before its MFMAs. Same job plan, slab layout and k_dw_reduce as the fp32 k_dw.
+//   Numerics: each k-step's six split products go into a fresh accumulator T (C = 0) added to the
+// running sum in fp32 (RNE): tools/mfma_accum_probe.hip measured this as more accurate than the fp32
+// fma chain at K = 4096 (one running C loses the low bits of the small terms with a bias).
+//   LDS image per operand and buffer: 16-B units (4 points of one row) [s][rb][q][i]: k-step s (2),
+//   32-row block rb (8), point quad q (4), row i (32). One DMA wave-instruction fills the 1 KiB of
+//   (s, rb, q pair) lane-linearly (lane l -> q = 2 qp + (l >> 5), i = l & 31); a 32x32x16 fragment
+//   (lane (i, h): row i, points 8h..8h+7) is two conflict-free ds_read_b128 (units q = 2h, 2h + 1).
+// ------------------------------------------------------------------------------------------------
+constexpr int GPC = 32;                 // points per chunk
+constexpr int G_OPND = 2 * 8 * 4 * 32;  // 16-B units per operand and buffer
+constexpr int G_BUF = 2 * G_OPND;       // units per buffer (dZ, X)
+constexpr int G_LDS = 2 * G_BUF * 16;   // bytes (128 KiB)
+static_assert(G_LDS <= 160 * 1024, "dWg LDS");
+
+__device__ __forceinline__ constexpr int g_unit(int s, int rb, int q, int i) { return ((s * 8 + rb) * 4 + q) * 32 + i; }
+
+// 8 fp32 (one row, points 8h .. 8h + 7) -> the hi / mid / lo bf16 fragments
+__device__ __forceinline__ AFrag split8(const float4 &a, const float4 &b) {
+    const Split4 x = split4(a.x, a.y, a.z, a.w);
+    const Split4 y = split4(b.x, b.y, b.z, b.w);
+    return AFrag{__builtin_shufflevector(x.h, y.h, 0, 1, 2, 3, 4, 5, 6, 7),
+                 __builtin_shufflevector(x.m, y.m, 0, 1, 2, 3, 4, 5, 6, 7),
+                 __builtin_shufflevector(x.l, y.l, 0, 1, 2, 3, 4, 5, 6, 7)};
+}
+
+__device__ __forceinline__ float sum8(const float4 &a, const float4 &b) {
+    return ((a.x + a.y) + (a.z + a.w)) + ((b.x + b.y) + (b.z + b.w));
+}
+
+// one k-step's six split products into a fresh T, then acc += T in fp32
+__device__ __forceinline__ void mma6_fresh(const AFrag &a, const AFrag &b, f32x16 &acc) {
+    f32x16 t = MFMA32(a.m, b.m, (f32x16)(0.f));
+    t = MFMA32(a.h, b.l, t);
+    t = MFMA32(a.l, b.h, t);
+    t = MFMA32(a.h, b.m, t);
+    t = MFMA32(a.m, b.h, t);
+    t = MFMA32(a.h, b.h, t);
+    acc += t;
+}
+
+typedef __attribute__((address_space(1))) void *gptr_t;
+typedef __attribute__((address_space(3))) void *lptr_t;
+
+template <bool NARROW>
+__device__ __forceinline__ void dwg_tile(const WJob &J, size_t Ns, const float *__restrict__ dz,
+                                         const float *__restrict__ saved, float *__restrict__ slabs, float4 *lds) {
+    const int split = blockIdx.x - J.block0;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wn = wave >> 2, wk = wave & 3;
+    const int h = lane >> 5, i = lane & 31;
+    const int nch = (int)(Ns / GPC);
+    const int per = div_up(nch, J.nsplit);
+    const int c0 = split * per;
+    const int c1 = min(nch, c0 + per);
+    // this wave's 8 DMA instructions per chunk: d = 8 wave + j -> operand d >> 5 (waves 0-3 dZ,
+    // 4-7 X), k-step, row block and quad pair of the 1 KiB they fill (all wave-uniform but the lane
+    // offset). Row blocks past the job's extent are not loaded; the rows of a partial block past it
+    // are in bounds (every job's rows rounded up to 32 lie inside saved / dZ, mlp_shared.h row maps)
+    // and only feed outputs k_dw_reduce never reads.
+    const int op = wave >> 2;
+    const float *obase = op ? saved + (size_t)J.xrow * Ns : dz + (size_t)J.zrow * Ns;
+    const int ext = op ? J.krows : J.nrows;
+    // buffer form: lane offset in one VGPR, row-block offset in an SGPR, chunk base in the
+    // descriptor (the host keeps 256 rows x Ns x 4 B below 2^31)
+    const uint32_t lane_off = (uint32_t)((i * Ns + 4 * h) * 4);
+    auto issue = [&](int c, int buf) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float *>(obase + (size_t)c * GPC), 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int e = (8 * wave + j) & 31;
+            const int s = e >> 4, rb = (e >> 1) & 7, qp = e & 1;
+            if (rb * 32 < ext)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rs, (lptr_t)(lds + buf * G_BUF + op * G_OPND + g_unit(s, rb, 2 * qp, 0)), 16, lane_off,
+                    (uint32_t)((rb * 32 * Ns + s * 16 + 8 * qp) * 4), 0, 0);
+        }
+    };
+    const int nact_r = NARROW ? (32 * wave < J.nrows ? 1 : 0) : min(4, max(0, div_up(J.nrows - 128 * wn, 32)));
+    const int nact_c = NARROW ? min(4, div_up(J.krows, 32)) : min(2, max(0, div_up(J.krows - 64 * wk, 32)));
+    const bool any = nact_r > 0 && nact_c > 0;
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+#pragma unroll
+        for (int u = 0; u < 2; u++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[t][u][r] = 0.f;
+    float bs[4] = {0.f, 0.f, 0.f, 0.f};  // bias row sums of this lane's dZ rows (fixed order)
+    const bool bias_wave = NARROW || wk == 0;
+    if (c0 < c1) issue(c0, 0);
+    for (int c = c0; c < c1; c++) {
+        const int buf = (c - c0) & 1;
+        // this wave's DMAs of chunk c have landed; after the barrier everyone's have, and every wave
+        // is done reading the other buffer (chunk c - 1), which the next DMAs overwrite
+        __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) expcnt(7) lgkmcnt(0)
+        __builtin_amdgcn_s_barrier();
+        if (c + 1 < c1) issue(c + 1, buf ^ 1);
+        if (!any) continue;
+        const float4 *A = lds + buf * G_BUF;
+        const float4 *B = A + G_OPND;
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            if (NARROW) {
+                const float4 a0 = A[g_unit(s, wave, 2 * h, i)], a1 = A[g_unit(s, wave, 2 * h + 1, i)];
+                bs[0] += sum8(a0, a1);
+                const AFrag at = split8(a0, a1);
+#pragma unroll
+                for (int v = 0; v < 4; v++) {
+                    if (v >= nact_c) continue;
+                    const AFrag b = split8(B[g_unit(s, v, 2 * h, i)], B[g_unit(s, v, 2 * h + 1, i)]);
+                    mma6_fresh(at, b, acc[v >> 1][v & 1]);
+                }
+            } else {
+                AFrag bb[2];
+#pragma unroll
+                for (int u = 0; u < 2; u++)
+                    if (u < nact_c) bb[u] = split8(B[g_unit(s, 2 * wk + u, 2 * h, i)], B[g_unit(s, 2 * wk + u, 2 * h + 1, i)]);
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    if (t >= nact_r) continue;
+                    const float4 a0 = A[g_unit(s, 4 * wn + t, 2 * h, i)], a1 = A[g_unit(s, 4 * wn + t, 2 * h + 1, i)];
+                    if (bias_wave) bs[t] += sum8(a0, a1);
+                    const AFrag at = split8(a0, a1);
+#pragma unroll
+                    for (int u = 0; u < 2; u++) {
+                        if (u >= nact_c) continue;
+                        mma6_fresh(at, bb[u], acc[t][u]);
+                    }
+                }
+            }
+        }
+    }
+    float *slab = slabs + (size_t)blockIdx.x * SLAB;
+    // rows past nrows / cols past krows hold garbage that k_dw_reduce never reads
+    if (NARROW) {
+        const float v0 = bs[0] + __shfl_xor(bs[0], 32);
+        if (h == 0) slab[WT * WT + 32 * wave + i] = v0;
+#pragma unroll
+        for (int v = 0; v < 4; v++) {
+            const int nb = 32 * wave, kb = 32 * v;
+#pragma unroll
+            for (int r = 0; r < 16; r++) slab[(nb + TileAddr::row(r) + 4 * h) * WT + kb + i] = acc[v >> 1][v & 1][r];
+        }
+        return;
+    }
+    if (bias_wave) {
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const float v = bs[t] + __shfl_xor(bs[t], 32);
+            if (h == 0) slab[WT * WT + 128 * wn + 32 * t + i] = v;
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int nb = 128 * wn + 32 * t, kb = 64 * wk + 32 * u;
+#pragma unroll
+            for (int r = 0; r < 16; r++) slab[(nb + TileAddr::row(r) + 4 * h) * WT + kb + i] = acc[t][u][r];
+        }
+}
+
+__global__ __launch_bounds__(DW_THREADS) void k_dwg(WJobs JT, size_t Ns, const float *__restrict__ dz,
+                                                    const float *__restrict__ saved, float *__restrict__ slabs) {
+    extern __shared__ float4 dwg_lds[];
+    WJob J = JT.j[0];
+#pragma unroll
+    for (int q = 1; q < MAXJ; q++)
+        if (q < JT.n && (int)blockIdx.x >= JT.j[q].block0) J = JT.j[q];
+    if (J.narrow)
+        dwg_tile<true>(J, Ns, dz, saved, slabs, dwg_lds);
+    else
+        dwg_tile<false>(J, Ns, dz, saved, slabs, dwg_lds);
+}
+
+// ------------------------------------------------------------------------------------------------
 // packing plan (host)
 // ------------------------------------------------------------------------------------------------
 struct Img {           // one A-operand image: ntiles x nk k-slots
@@ -1061,15 +1244,17 @@ size_t saved_floats(int flags, int N) {
     return (size_t)F.nsaved * Ns + (size_t)F.nmask * (Ns / 32) + TC_FLOATS;
 }
 
-// dW arithmetic: the split-bf16 k_dw above, or (default) the fp32-input MFMA k_dw of mlp.hip on the
-// same [rows][Ns] arrays (DGS_MLP_SPLIT_DW=1 selects the split one)
-static bool split_dw() {
-    static const bool on = [] {
+// dW arithmetic (DGS_MLP_SPLIT_DW): 2 = the split-bf16 k_dwg above (LDS-DMA staged), 1 = the split-bf16
+// k_dw (VGPR staged), 0 = the fp32-input MFMA k_dw of mlp.hip, all on the same [rows][Ns] arrays
+static int dw_mode() {
+    static const int m = [] {
         const char *e = getenv("DGS_MLP_SPLIT_DW");
-        return e && e[0] == '1';
+        return (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 0;
     }();
-    return on;
+    return m;
 }
+static int dw_glds(const Flags &F, size_t Ns, const float *dz, const float *saved, float *slabs, float *const *grads,
+                   hipStream_t stream);
 
 size_t scratch_floats(int flags, int N) {
     const Flags F = make_flags(flags);
@@ -1155,11 +1340,12 @@ int backward(int flags, int N, const float *packed, const float *saved, const fl
     }
     DGS_LAUNCH_CHECK("k_bwd", false, stream);
     int rc;
-    if (!split_dw()) {
+    if (dw_mode() == 0)
         rc = mlp::dw_fp32(F, Ns, dz, saved, slabs, grads, stream);
-    } else {
+    else if (dw_mode() == 1)
         rc = dw_split(F, Ns, dz, saved, slabs, grads, stream);
-    }
+    else
+        rc = dw_glds(F, Ns, dz, saved, slabs, grads, stream);
     if (rc != DGS_OK || !F.uniform_t) return rc;
     TGradArgs g{};
     g.fp = packed + P.img_floats();
@@ -1186,6 +1372,24 @@ static int dw_split(const Flags &F, size_t Ns, const float *dz, const float *sav
         hipLaunchKernelGGL(k_dw, dim3(W.nblocks), dim3(DW_THREADS), DW_LDS, stream, W.jobs, Ns, dz, saved, slabs);
     }
     DGS_LAUNCH_CHECK("k_dw", false, stream);
+    return launch_dw_reduce(F, W, slabs, grads, stream);
+}
+
+static int dw_glds(const Flags &F, size_t Ns, const float *dz, const float *saved, float *slabs, float *const *grads,
+                   hipStream_t stream) {
+    if ((size_t)WT * Ns * 4 >= 0x7fffffffull)  // buffer offsets of a 256-row tile must fit 31 bits
+        return mlp::dw_fp32(F, Ns, dz, saved, slabs, grads, stream);
+    const WPlan W = split_wplan(F);
+    {
+        static bool attr_set = false;  // 128 KiB dynamic LDS
+        if (!attr_set) {
+            DGS_HIP_CHECK(hipFuncSetAttribute((const void *)k_dwg, hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS));
+            attr_set = true;
+        }
+        ScopedTimer tm("mlp_dw", stream);
+        hipLaunchKernelGGL(k_dwg, dim3(W.nblocks), dim3(DW_THREADS), G_LDS, stream, W.jobs, Ns, dz, saved, slabs);
+    }
+    DGS_LAUNCH_CHECK("k_dwg", false, stream);
     return launch_dw_reduce(F, W, slabs, grads, stream);
 }
 
