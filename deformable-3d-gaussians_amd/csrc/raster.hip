@@ -141,8 +141,14 @@ template <class KT>
 __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t *__restrict__ order,
                                                    const float2 *__restrict__ xy, const int *__restrict__ radii,
                                                    const uint32_t *__restrict__ offsets, int gx, int gy,
-                                                   KT *__restrict__ keys, uint32_t *__restrict__ vals, uint32_t cap) {
+                                                   KT *__restrict__ keys, uint32_t *__restrict__ vals, uint32_t cap,
+                                                   uint2 *__restrict__ ranges, int T) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    // folded fills (no separate memsets): empty tile ranges, and all-ones keys over the
+    // speculative capacity past the pair count so the radix sort leaves the padding at the end
+    const int nthreads = gridDim.x * blockDim.x;
+    for (int t = j; t < T; t += nthreads) ranges[t] = make_uint2(0u, 0u);
+    for (uint32_t k = offsets[P - 1] + (uint32_t)j; k < cap; k += (uint32_t)nthreads) keys[k] = (KT)~(KT)0;
     if (j >= P) return;
     const uint32_t g = order[j];
     const int r = radii[g];
@@ -807,9 +813,8 @@ static int bin_tiles(dgs_raster_ctx *c, int cap, int P, int device, hipStream_t 
     uint32_t *v0 = (uint32_t *)(b + o_v0), *v1 = (uint32_t *)(b + o_v1);
     {
         ScopedTimer tm("duplicate", stream);
-        DGS_HIP_CHECK(hipMemsetAsync(k0, 0xff, sizeof(KT) * cap, stream));
         hipLaunchKernelGGL(k_duplicate<KT>, dim3(div_up(P, 256)), dim3(256), 0, stream, P, c->order, c->xy, c->radii,
-                           c->offsets, c->gx, c->gy, k0, v0, (uint32_t)cap);
+                           c->offsets, c->gx, c->gy, k0, v0, (uint32_t)cap, c->ranges, c->gx * c->gy);
     }
     DGS_LAUNCH_CHECK("k_duplicate", dbg, stream);
     hipcub::DoubleBuffer<KT> kbuf(k0, k1);
@@ -831,13 +836,13 @@ static int bin_tiles(dgs_raster_ctx *c, int cap, int P, int device, hipStream_t 
 static int bin_and_blend(dgs_raster_ctx *c, int cap, int P, int device, hipStream_t stream, bool dbg, float *out_color,
                          float *out_depth) {
     const int T = c->gx * c->gy;
-    DGS_HIP_CHECK(hipMemsetAsync(c->ranges, 0, 8ull * T, stream));
-    if (cap > 0) {
+    if (cap > 0) {  // k_duplicate clears c->ranges
         // 16-bit tile keys up to 65535 tiles (4080 x 4080 pixels), 32-bit beyond
         const int rc = T < 65535 ? bin_tiles<uint16_t>(c, cap, P, device, stream, dbg)
                                  : bin_tiles<uint32_t>(c, cap, P, device, stream, dbg);
         if (rc) return rc;
     } else {
+        DGS_HIP_CHECK(hipMemsetAsync(c->ranges, 0, 8ull * T, stream));
         c->vals = nullptr;
     }
     {
