@@ -94,14 +94,11 @@ def _fused_ok(pc):
 def render(viewpoint_camera, pc, pipe, bg_color, d_xyz, d_rotation, d_scaling, is_6dof=False,
            scaling_modifier=1.0, override_color=None, direct_compute=False):
     dev = pc.get_xyz.device
-    screenspace_points = torch.zeros_like(pc.get_xyz, dtype=pc.get_xyz.dtype, requires_grad=True, device=dev) + 0
-    screenspace_points_densify = torch.zeros_like(pc.get_xyz, dtype=pc.get_xyz.dtype, requires_grad=True,
-                                                  device=dev) + 0
-    try:
-        screenspace_points.retain_grad()
-        screenspace_points_densify.retain_grad()
-    except Exception:
-        pass
+    # gaussian_renderer/__init__.py:41-47 builds these as zeros + 0 with retain_grad; the rasterizer never
+    # reads their values (only .grad is delivered), so uninitialised leaf tensors serve: their .grad is
+    # populated directly and no fill / add kernels run per render
+    screenspace_points = torch.empty_like(pc.get_xyz, device=dev).requires_grad_(True)
+    screenspace_points_densify = torch.empty_like(pc.get_xyz, device=dev).requires_grad_(True)
     tanfovx = math.tan(viewpoint_camera.FoVx * 0.5)
     tanfovy = math.tan(viewpoint_camera.FoVy * 0.5)
     raster_settings = GaussianRasterizationSettings(
