@@ -5,6 +5,7 @@
 #include <set>
 #include <mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "dgs_common.h"
@@ -50,6 +51,19 @@ void drain_locked() {
 }  // namespace
 
 void set_error(const std::string &msg) { g_err = msg; }
+
+int ensure_dynamic_lds(const void *kernel, int bytes) {
+    static std::mutex mu;
+    static std::set<std::tuple<const void *, int, int>> done;  // (kernel, device, bytes)
+    int device = 0;
+    DGS_HIP_CHECK(hipGetDevice(&device));
+    std::lock_guard<std::mutex> lk(mu);
+    auto key = std::make_tuple(kernel, device, bytes);
+    if (done.count(key)) return DGS_OK;
+    DGS_HIP_CHECK(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+    done.insert(key);
+    return DGS_OK;
+}
 
 ScopedTimer::ScopedTimer(const char *n, hipStream_t s) : name(n), stream(s), ev0(nullptr) {
     if (!g_timing) return;

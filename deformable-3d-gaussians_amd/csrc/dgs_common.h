@@ -30,6 +30,11 @@ void set_error(const std::string &msg);
         }                                                                                    \
     } while (0)
 
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) applies to the current device: set it once per
+// (kernel, device) under a lock, so a process driving several GPUs, or several host threads, never
+// launches a kernel on a device where the attribute is missing.
+int ensure_dynamic_lds(const void *kernel, int bytes);
+
 // Kernel timing (bench.py roofline): events recorded around selected launches on their stream.
 struct ScopedTimer {
     const char *name;

@@ -1182,12 +1182,9 @@ int dw_fp32(const Flags &F, size_t Ns, const float *dz, const float *saved, floa
             hipStream_t stream) {
     WPlan W = fp32_wplan(F);
     {
-        static bool attr_set = false;  // 147 KiB dynamic LDS
         const size_t lds_bytes = sizeof(float) * 2 * 2 * WT * LDA;
-        if (!attr_set) {
-            DGS_HIP_CHECK(hipFuncSetAttribute((const void *)k_dw, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes));
-            attr_set = true;
-        }
+        // 147 KiB dynamic LDS: the attribute is per device, set once per (kernel, device)
+        if (int rc = ensure_dynamic_lds((const void *)k_dw, (int)lds_bytes)) return rc;
         ScopedTimer tm("mlp_dw", stream);
         hipLaunchKernelGGL(k_dw, dim3(W.nblocks), dim3(DW_THREADS), lds_bytes, stream, W.jobs, Ns, dz, saved, slabs);
     }

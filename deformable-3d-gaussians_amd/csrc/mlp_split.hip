@@ -1363,11 +1363,8 @@ static int dw_split(const Flags &F, size_t Ns, const float *dz, const float *sav
                     hipStream_t stream) {
     const WPlan W = split_wplan(F);
     {
-        static bool attr_set = false;  // 144 KiB dynamic LDS
-        if (!attr_set) {
-            DGS_HIP_CHECK(hipFuncSetAttribute((const void *)k_dw, hipFuncAttributeMaxDynamicSharedMemorySize, DW_LDS));
-            attr_set = true;
-        }
+        // 144 KiB dynamic LDS: the attribute is per device, set once per (kernel, device)
+        if (int rc = ensure_dynamic_lds((const void *)k_dw, DW_LDS)) return rc;
         ScopedTimer tm("mlp_dw", stream);
         hipLaunchKernelGGL(k_dw, dim3(W.nblocks), dim3(DW_THREADS), DW_LDS, stream, W.jobs, Ns, dz, saved, slabs);
     }
@@ -1381,11 +1378,8 @@ static int dw_glds(const Flags &F, size_t Ns, const float *dz, const float *save
         return mlp::dw_fp32(F, Ns, dz, saved, slabs, grads, stream);
     const WPlan W = split_wplan(F);
     {
-        static bool attr_set = false;  // 128 KiB dynamic LDS
-        if (!attr_set) {
-            DGS_HIP_CHECK(hipFuncSetAttribute((const void *)k_dwg, hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS));
-            attr_set = true;
-        }
+        // 128 KiB dynamic LDS: the attribute is per device, set once per (kernel, device)
+        if (int rc = ensure_dynamic_lds((const void *)k_dwg, G_LDS)) return rc;
         ScopedTimer tm("mlp_dw", stream);
         hipLaunchKernelGGL(k_dwg, dim3(W.nblocks), dim3(DW_THREADS), G_LDS, stream, W.jobs, Ns, dz, saved, slabs);
     }

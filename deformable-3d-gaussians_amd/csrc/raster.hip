@@ -167,12 +167,15 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t *__rest
         }
 }
 
-// L (the pair count) is read on the device: the grid covers the speculative capacity
+// L (the pair count) is read on the device and clipped to the launched capacity: an overflowing
+// speculative launch (count > cap) then covers exactly the cap sorted pairs it wrote, never the
+// padding or stale slots past them, and every range stays inside [0, cap); the host redoes the
+// whole binning at the exact size afterwards.
 template <class KT>
-__global__ __launch_bounds__(256) void k_ranges(const uint32_t *__restrict__ count, const KT *__restrict__ keys,
-                                                uint2 *__restrict__ ranges) {
+__global__ __launch_bounds__(256) void k_ranges(const uint32_t *__restrict__ count, uint32_t cap,
+                                                const KT *__restrict__ keys, uint2 *__restrict__ ranges) {
     int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    const int L = (int)*count;
+    const int L = (int)min(*count, cap);
     if (idx >= L) return;
     uint32_t t = (uint32_t)keys[idx];
     if (idx == 0) {
@@ -716,6 +719,7 @@ int class_upper(int cls) {
 // re-runs binning with a grown capacity (results are always exact).
 std::mutex g_cap_mu;
 std::map<int, int> g_pair_cap;
+long long g_redos = 0;  // overflowing speculative launches redone at the exact size (debug counter)
 
 int grown_cap(long long nr) {
     long long c = nr + nr / 8 + 65536;
@@ -827,7 +831,7 @@ static int bin_tiles(dgs_raster_ctx *c, int cap, int P, int device, hipStream_t 
     {
         ScopedTimer tm("ranges", stream);
         hipLaunchKernelGGL(k_ranges<KT>, dim3(div_up(cap, 256)), dim3(256), 0, stream, c->offsets + (P - 1),
-                           kbuf.Current(), c->ranges);
+                           (uint32_t)cap, kbuf.Current(), c->ranges);
     }
     DGS_LAUNCH_CHECK("k_ranges", dbg, stream);
     return DGS_OK;
@@ -968,6 +972,10 @@ extern "C" int dgs_raster_forward(const dgs_raster_settings *s, int P, int M, co
             DGS_HIP_CHECK(hipEventSynchronize(c->count_ev));
             nr = (int)*c->h_total;
             if (nr > cap) {  // overflow: redo binning + blend at the exact size
+                {
+                    std::lock_guard<std::mutex> lk(g_cap_mu);
+                    g_redos++;
+                }
                 if (int rc = bin_and_blend(c, nr, P, device, stream, dbg, out_color, out_depth)) return rc;
             }
         }
@@ -1042,6 +1050,16 @@ extern "C" void dgs_raster_ctx_free(dgs_raster_ctx *c) {
         if (c->h_total) (void)hipHostFree(c->h_total);
         delete c;
     }
+}
+
+extern "C" void dgs_debug_set_pair_cap(int device, int cap) {
+    std::lock_guard<std::mutex> lk(g_cap_mu);
+    g_pair_cap[device] = cap < 0 ? 0 : cap;
+}
+
+extern "C" long long dgs_debug_binning_redos(void) {
+    std::lock_guard<std::mutex> lk(g_cap_mu);
+    return g_redos;
 }
 
 extern "C" int dgs_mark_visible(int P, const float *means3D, const float *viewmatrix, const float *projmatrix,

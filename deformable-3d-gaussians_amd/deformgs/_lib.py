@@ -43,6 +43,8 @@ _SIGS = {
     "dgs_raster_backward": ([P] * 12 + [P], I),
     "dgs_raster_ctx_free": ([P], None),
     "dgs_mark_visible": ([I, P, P, P, P, P], I),
+    "dgs_debug_set_pair_cap": ([I, I], None),
+    "dgs_debug_binning_redos": ([], ctypes.c_longlong),
     "dgs_timing_enable": ([I], None),
     "dgs_timing_query": ([ctypes.c_char_p, ctypes.POINTER(I)], ctypes.c_double),
     "dgs_timing_reset": ([], None),

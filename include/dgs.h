@@ -90,6 +90,14 @@ void dgs_raster_ctx_free(dgs_raster_ctx *ctx);
 int dgs_mark_visible(int P, const float *means3D, const float *viewmatrix, const float *projmatrix,
                      uint8_t *visible, void *stream);
 
+/* ---- binning debug hooks (tests only) ----
+ * The forward launches tile binning for a learned per-device pair capacity before it knows the
+ * pair count (speculative binning) and redoes binning at the exact size when the count is larger.
+ * dgs_debug_set_pair_cap overrides that capacity for `device` (0 = none: the next forward runs
+ * synchronously); dgs_debug_binning_redos counts the redone (overflowing) launches so far. */
+void dgs_debug_set_pair_cap(int device, int cap);
+long long dgs_debug_binning_redos(void);
+
 /* ---- timing hooks (bench.py): per-kernel-class HIP event accumulation on the launch stream ---- */
 void dgs_timing_enable(int on);
 /* Restrict timing to the comma-separated kernel classes in `csv` (host string; NULL or "" = all). */

@@ -166,3 +166,64 @@ def test_speculative_binning_matches_exact():
     o, _ = oracle_run(big, rs_b)
     c, r, d = _forward_only(big, rs_b, debug=False)
     assert np.abs(c - o.color).mean() <= 1e-5
+
+
+def test_speculative_overflow_redo_is_exact():
+    """Force the overflow path: the per-device pair capacity is overridden with a small value that
+    is not a multiple of 256 (so the ranges/sort grids overhang it), and with a capacity left over
+    from a much larger frame (stale keys past the new pairs). Every forced overflow must be redone
+    (debug counter) and equal the synchronous exact path bit for bit."""
+    from deformgs import _lib
+    lib = _lib.load()
+    dev = torch.cuda.current_device()
+    big, rs_b, _ = scene(4000, 200, 160, seed=4, cam_index=2, scale_boost=1.5)  # ~45k pairs
+    small, rs_s, _ = scene(1500, 96, 80, seed=3, cam_index=1, scale_boost=0.8)  # ~3.7k pairs
+    ref_big = _forward_only(big, rs_b, debug=True)
+    ref_small = _forward_only(small, rs_s, debug=True)
+    nr_small = _num_rendered(small, rs_s)
+    assert nr_small > 2000, "the small scene must have enough pairs to overflow the capacities below"
+    for cap in (1, 255, 1000 + 37, 5 * 256 + 129):
+        for inputs, ref in ((big, ref_big), (small, ref_small)):
+            lib.dgs_debug_set_pair_cap(dev, cap)
+            before = lib.dgs_debug_binning_redos()
+            out = _forward_only(inputs, rs_b if inputs is big else rs_s, debug=False)
+            redone = lib.dgs_debug_binning_redos() - before
+            torch.cuda.synchronize()
+            for x, y in zip(out, ref):
+                np.testing.assert_array_equal(x, y)
+            assert redone == 1, f"cap={cap}: expected one overflow redo, saw {redone}"
+    # a capacity far above the count (tail padded with all-ones keys), after the big frame
+    lib.dgs_debug_set_pair_cap(dev, 3_000_000 + 77)
+    out = _forward_only(small, rs_s, debug=False)
+    for x, y in zip(out, ref_small):
+        np.testing.assert_array_equal(x, y)
+    # and the backward after an overflowing forward matches the exact path's backward
+    lib.dgs_debug_set_pair_cap(dev, 999)
+    g1 = _grads_of(big, rs_b, debug=False)
+    g2 = _grads_of(big, rs_b, debug=True)
+    for k in g1:
+        np.testing.assert_allclose(g1[k], g2[k], rtol=1e-4, atol=1e-6 * max(1.0, np.abs(g2[k]).max()))
+
+
+def _num_rendered(inputs, rs):
+    from diff_gaussian_rasterization import GaussianRasterizer
+    t = {k: v.cuda().requires_grad_(True) for k, v in inputs.items()}
+    N = t["means3D"].shape[0]
+    color, _, _ = GaussianRasterizer(settings_for_gpu(rs))(
+        means3D=t["means3D"], means2D=torch.zeros((N, 3), device="cuda"), shs=t["shs"],
+        opacities=t["opacities"], scales=t["scales"], rotations=t["rotations"])
+    return int(color.grad_fn.num_rendered)
+
+
+def _grads_of(inputs, rs, debug):
+    from diff_gaussian_rasterization import GaussianRasterizer
+    st = settings_for_gpu(rs)._replace(debug=debug)
+    t = {k: v.cuda().requires_grad_(True) for k, v in inputs.items()}
+    N = t["means3D"].shape[0]
+    color, radii, depth = GaussianRasterizer(st)(
+        means3D=t["means3D"], means2D=torch.zeros((N, 3), device="cuda"),
+        means2D_densify=torch.zeros((N, 3), device="cuda"), shs=t["shs"], opacities=t["opacities"],
+        scales=t["scales"], rotations=t["rotations"])
+    w = torch.linspace(-1, 1, color.numel(), device="cuda").reshape(color.shape)
+    (color * w).sum().backward()
+    return {k: v.grad.cpu().numpy() for k, v in t.items()}
