@@ -61,7 +61,7 @@ def parse():
 def mfma_peak(name):
     """Dense MFMA peak (fp32-equivalent TFLOP/s) of the arithmetic kernel class `name` runs on."""
     exact = os.environ.get("DGS_MLP_EXACT_FP32", "0") not in ("", "0")
-    if name == "mlp_dw" and os.environ.get("DGS_MLP_SPLIT_DW", "0") not in ("1", "2"):
+    if name == "mlp_dw" and os.environ.get("DGS_MLP_SPLIT_DW", "3") == "0":
         return FP32_MFMA_PEAK_TFLOPS, "fp32 MFMA (v_mfma_f32_32x32x2_f32)"
     if exact:
         return FP32_MFMA_PEAK_TFLOPS, "fp32 MFMA (v_mfma_f32_32x32x2_f32)"

@@ -43,6 +43,7 @@
 #include <cstdlib>
 #include <map>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 #include "dgs_common.h"
@@ -86,18 +87,31 @@ struct Split4 {
     bf16x4 h, m, l;
 };
 
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// RNE of two floats into one packed bf16 pair (one v_cvt_pk_bf16_f32)
+__device__ __forceinline__ uint32_t cvt2(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
+}
+
+// the exact split of two values, pairwise: 3 v_cvt_pk_bf16_f32 + 4 unpacks (the bf16 -> f32 of
+// a packed pair is a shift / mask) + 4 subtractions
+__device__ __forceinline__ void split2(float a, float b, uint32_t &h, uint32_t &m, uint32_t &l) {
+    h = cvt2(a, b);
+    const float ra = a - __uint_as_float(h << 16), rb = b - __uint_as_float(h & 0xffff0000u);
+    m = cvt2(ra, rb);
+    l = cvt2(ra - __uint_as_float(m << 16), rb - __uint_as_float(m & 0xffff0000u));
+}
+
 __device__ inline Split4 split4(float a, float b, float c, float d) {
+    uint32_t h0, m0, l0, h1, m1, l1;
+    split2(a, b, h0, m0, l0);
+    split2(c, d, h1, m1, l1);
     Split4 s;
-    const float x[4] = {a, b, c, d};
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const __bf16 hb = (__bf16)x[j];
-        const float r = x[j] - (float)hb;
-        const __bf16 mb = (__bf16)r;
-        s.h[j] = hb;
-        s.m[j] = mb;
-        s.l[j] = (__bf16)(r - (float)mb);
-    }
+    s.h = __builtin_bit_cast(bf16x4, make_uint2(h0, h1));
+    s.m = __builtin_bit_cast(bf16x4, make_uint2(m0, m1));
+    s.l = __builtin_bit_cast(bf16x4, make_uint2(l0, l1));
     return s;
 }
 
@@ -889,11 +903,14 @@ __device__ __forceinline__ constexpr int g_unit(int s, int rb, int q, int i) { r
 
 // 8 fp32 (one row, points 8h .. 8h + 7) -> the hi / mid / lo bf16 fragments
 __device__ __forceinline__ AFrag split8(const float4 &a, const float4 &b) {
-    const Split4 x = split4(a.x, a.y, a.z, a.w);
-    const Split4 y = split4(b.x, b.y, b.z, b.w);
-    return AFrag{__builtin_shufflevector(x.h, y.h, 0, 1, 2, 3, 4, 5, 6, 7),
-                 __builtin_shufflevector(x.m, y.m, 0, 1, 2, 3, 4, 5, 6, 7),
-                 __builtin_shufflevector(x.l, y.l, 0, 1, 2, 3, 4, 5, 6, 7)};
+    uint32_t h[4], m[4], l[4];
+    split2(a.x, a.y, h[0], m[0], l[0]);
+    split2(a.z, a.w, h[1], m[1], l[1]);
+    split2(b.x, b.y, h[2], m[2], l[2]);
+    split2(b.z, b.w, h[3], m[3], l[3]);
+    return AFrag{__builtin_bit_cast(bf16x8, make_uint4(h[0], h[1], h[2], h[3])),
+                 __builtin_bit_cast(bf16x8, make_uint4(m[0], m[1], m[2], m[3])),
+                 __builtin_bit_cast(bf16x8, make_uint4(l[0], l[1], l[2], l[3]))};
 }
 
 __device__ __forceinline__ float sum8(const float4 &a, const float4 &b) {
@@ -1046,6 +1063,210 @@ __global__ __launch_bounds__(DW_THREADS) void k_dwg(WJobs JT, size_t Ns, const f
         dwg_tile<true>(J, Ns, dz, saved, slabs, dwg_lds);
     else
         dwg_tile<false>(J, Ns, dz, saved, slabs, dwg_lds);
+}
+
+// ------------------------------------------------------------------------------------------------
+// dW = dZ X^T on split bf16 (k_dws, the default dW). Per job tile (<= 256 dZ rows x 256 X rows) and
+// 32-point chunk, each wave owns 32 rows of ONE operand ("private": loaded, split and kept as MFMA
+// fragments in its own registers) against all rows of the other ("shared": staged by the whole
+// workgroup, split once, through LDS):
+//   COL (krows = 256 jobs): private = X rows 32 w..+31 (B fragments), shared = dZ rows (A, NS tiles)
+//   ROW (krows <= 96 jobs): private = dZ rows 32 w..+31 (A fragments), shared = X rows (B, NS tiles)
+// so every fp32 value is split exactly once per workgroup and only the shared operand makes the LDS
+// round trip (k_dwg split each fragment in every wave reading it; k_dw split once but through LDS
+// for both operands). Per chunk: split the private registers -> fragments | MFMAs on LDS buffer c & 1
+// with the next chunk's shared split (3 ds_write_b64 per float4) and loads interleaved | ONE barrier.
+//   LDS: split planes in fragment order, unit (16 B) [split][k-step][32-row block][lane = 32 h + i]
+//   (row i, points 8h..8h+7): a fragment is one conflict-free ds_read_b128 per split; 2 x 48 KiB.
+//   Numerics: each tile's twelve products of a chunk (two k-steps x six, the corrections first) go
+//   into a fresh accumulator T, added to the running sum in fp32 (tools/mfma_accum_probe.hip: a
+//   long running MFMA C loses the low bits of small terms with a bias).
+// Same job plan, slab layout and k_dw_reduce as the fp32 k_dw.
+// ------------------------------------------------------------------------------------------------
+constexpr int S_UNITS = NSPLIT * 2 * 8 * 64;  // 16-B units per chunk buffer
+constexpr int S_LDS = 2 * S_UNITS * 16;       // bytes (96 KiB)
+static_assert(S_LDS <= 160 * 1024, "dWs LDS");
+
+__device__ __forceinline__ constexpr int s_unit(int p, int ks, int rb, int l) { return ((p * 2 + ks) * 8 + rb) * 64 + l; }
+
+__device__ __forceinline__ AFrag s_frag(const bf16x8 *L, int ks, int rb, int lane) {
+    return AFrag{L[s_unit(0, ks, rb, lane)], L[s_unit(1, ks, rb, lane)], L[s_unit(2, ks, rb, lane)]};
+}
+
+// one tile's products of a 32-point chunk (fragments of k-steps 0 / 1) into a fresh accumulator:
+// the ten corrections first, then the two hh products
+__device__ __forceinline__ f32x16 mma12(const AFrag &a0, const AFrag &b0, const AFrag &a1, const AFrag &b1) {
+    f32x16 t = MFMA32(a0.m, b0.m, (f32x16)(0.f));
+    t = MFMA32(a0.h, b0.l, t);
+    t = MFMA32(a0.l, b0.h, t);
+    t = MFMA32(a1.m, b1.m, t);
+    t = MFMA32(a1.h, b1.l, t);
+    t = MFMA32(a1.l, b1.h, t);
+    t = MFMA32(a0.h, b0.m, t);
+    t = MFMA32(a0.m, b0.h, t);
+    t = MFMA32(a1.h, b1.m, t);
+    t = MFMA32(a1.m, b1.h, t);
+    t = MFMA32(a0.h, b0.h, t);
+    return MFMA32(a1.h, b1.h, t);
+}
+
+// acc += t (this file is built with -fno-slp-vectorize: no v_pk_add_f32 beside the MFMAs)
+__device__ __forceinline__ void add16(f32x16 &acc, const f32x16 &t) {
+#pragma unroll
+    for (int r = 0; r < 16; r++) acc[r] += t[r];
+}
+
+template <bool COL, int NS>
+__device__ __forceinline__ void dws_run(const WJob &J, size_t Ns, const float *__restrict__ dz,
+                                        const float *__restrict__ saved, float *__restrict__ slabs, bf16x8 *lds) {
+    constexpr int SROWS = 32 * NS;                   // shared rows staged per chunk
+    constexpr int NSF = (SROWS * 8 + 511) / 512;     // staged float4 per thread per chunk
+    const int split = blockIdx.x - J.block0;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int h = lane >> 5, i = lane & 31;
+    const int nch = (int)(Ns / 32);
+    const int per = div_up(nch, J.nsplit);
+    const int c0 = split * per;
+    const int c1 = min(nch, c0 + per);
+    // operands through buffer descriptors whose record count ends at the job's extent: rows past
+    // it read as zero (32-bit offsets: the host keeps 256 rows x Ns x 4 B below 2^31)
+    const float *zb = dz + (size_t)J.zrow * Ns, *xb = saved + (size_t)J.xrow * Ns;
+    const __amdgpu_buffer_rsrc_t rsS = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(COL ? zb : xb), 0, (int)((COL ? J.nrows : J.krows) * Ns * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsP = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(COL ? xb : zb), 0, (int)((COL ? J.krows : J.nrows) * Ns * 4), 0x00020000);
+    const bool pact = 32 * wave < (COL ? J.krows : J.nrows);  // this wave has private rows (uniform)
+    // private: lane (i, h) holds row 32 w + i, points 8 h .. + 7 of each k-step (fragment layout)
+    const int pvoff = ((32 * wave + i) * (int)Ns + 8 * h) * 4;
+    float4 pr[4];  // [k-step][half]
+    auto pload = [&](int c) {
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            pr[q] = __builtin_bit_cast(float4,
+                                       __builtin_amdgcn_raw_buffer_load_b128(rsP, pvoff, c * 128 + (q >> 1) * 64 + (q & 1) * 16, 0));
+    };
+    // shared staging: slot g = tid + 512 f -> row g >> 3, points 4 (g & 7) .. + 3 of the chunk
+    float4 st[NSF];
+    auto sload = [&](int c) {
+#pragma unroll
+        for (int f = 0; f < NSF; f++) {
+            const int g = tid + 512 * f;
+            if (SROWS * 8 % 512 == 0 || g < SROWS * 8)
+                st[f] = __builtin_bit_cast(
+                    float4, __builtin_amdgcn_raw_buffer_load_b128(rsS, ((g >> 3) * (int)Ns + 4 * (g & 7)) * 4, c * 128, 0));
+        }
+    };
+    float bsum[NSF] = {};  // COL: bias row sums of the staged dZ rows; ROW: bsum[0] of the private row
+    char *lb = reinterpret_cast<char *>(lds);
+    // `live`: the staged chunk is a real one (the last chunk re-splits a stale copy into the buffer
+    // nobody reads again; it must not count in the bias sums)
+    auto sput = [&](int f, int buf, bool live) {
+        const int g = tid + 512 * f;
+        if (!(SROWS * 8 % 512 == 0 || g < SROWS * 8)) return;
+        const float4 v = st[f];
+        if (COL) bsum[f] += live ? (v.x + v.y) + (v.z + v.w) : 0.f;
+        const Split4 s = split4(v.x, v.y, v.z, v.w);
+        const int row = g >> 3, q = g & 7;
+        char *p = lb + buf * (S_UNITS * 16) +
+                  s_unit(0, q >> 2, row >> 5, 32 * ((q >> 1) & 1) + (row & 31)) * 16 + 8 * (q & 1);
+        *reinterpret_cast<bf16x4 *>(p) = s.h;
+        *reinterpret_cast<bf16x4 *>(p + 2 * 8 * 64 * 16) = s.m;
+        *reinterpret_cast<bf16x4 *>(p + 2 * 2 * 8 * 64 * 16) = s.l;
+    };
+    f32x16 acc[NS];
+#pragma unroll
+    for (int s = 0; s < NS; s++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) acc[s][r] = 0.f;
+    if (c0 < c1) {
+        sload(c0);
+        pload(c0);
+#pragma unroll
+        for (int f = 0; f < NSF; f++) sput(f, 0, true);
+        sload(min(c0 + 1, c1 - 1));
+    }
+    lds_barrier();
+    // shared float4 f of the next chunk is split after tile put_at(f) of this one (within the first
+    // half of the tiles), then the loads of the chunk after are issued
+    constexpr int NH = (NS + 1) / 2;
+    auto put_at = [](int f) { return (f * NH) / NSF; };
+    auto chunk = [&](int c, auto BUFC) {
+        constexpr int buf = decltype(BUFC)::value;
+        const bf16x8 *L = lds + buf * S_UNITS;
+        const bool more = c + 1 < c1;
+        if (pact) {
+            // private fragments of this chunk, then the private loads of the next (in flight for
+            // the whole chunk)
+            AFrag pf0 = split8(pr[0], pr[1]), pf1 = split8(pr[2], pr[3]);
+            if (!COL) bsum[0] += sum8(pr[0], pr[1]) + sum8(pr[2], pr[3]);
+            pload(min(c + 1, c1 - 1));
+#pragma unroll
+            for (int s = 0; s < NS; s++) {
+                const AFrag s0 = s_frag(L, 0, s, lane), s1 = s_frag(L, 1, s, lane);
+                add16(acc[s], COL ? mma12(s0, pf0, s1, pf1) : mma12(pf0, s0, pf1, s1));
+#pragma unroll
+                for (int f = 0; f < NSF; f++)
+                    if (put_at(f) == s) sput(f, buf ^ 1, more);
+                if (s == put_at(NSF - 1)) sload(min(c + 2, c1 - 1));
+            }
+        } else {
+            pload(min(c + 1, c1 - 1));  // (keeps the waves' vmcnt streams alike; reads row 0 + OOB zeros)
+#pragma unroll
+            for (int f = 0; f < NSF; f++) sput(f, buf ^ 1, more);
+            sload(min(c + 2, c1 - 1));
+        }
+        lds_barrier();
+    };
+    for (int c = c0; c < c1; c += 2) {
+        chunk(c, std::integral_constant<int, 0>{});
+        if (c + 1 < c1) chunk(c + 1, std::integral_constant<int, 1>{});
+    }
+    float *slab = slabs + (size_t)blockIdx.x * SLAB;
+    if (COL) {
+        // bias row sums: the 8 lanes staging a row hold its partial sums (fixed xor-tree order)
+#pragma unroll
+        for (int f = 0; f < NSF; f++) {
+            float v = bsum[f];
+            v += __shfl_xor(v, 1);
+            v += __shfl_xor(v, 2);
+            v += __shfl_xor(v, 4);
+            const int g = tid + 512 * f;
+            if ((g & 7) == 0 && g < SROWS * 8) slab[WT * WT + (g >> 3)] = v;
+        }
+    } else if (pact) {
+        const float v = bsum[0] + __shfl_xor(bsum[0], 32);
+        if (h == 0) slab[WT * WT + 32 * wave + i] = v;
+    }
+    if (!pact) return;
+    // rows past nrows / cols past krows hold zeros that k_dw_reduce never reads
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+        const int nb = COL ? 32 * s : 32 * wave, kb = COL ? 32 * wave : 32 * s;
+#pragma unroll
+        for (int r = 0; r < 16; r++) slab[(nb + TileAddr::row(r) + 4 * h) * WT + kb + i] = acc[s][r];
+    }
+}
+
+__global__ __launch_bounds__(DW_THREADS) void k_dws(WJobs JT, size_t Ns, const float *__restrict__ dz,
+                                                    const float *__restrict__ saved, float *__restrict__ slabs) {
+    extern __shared__ bf16x8 dws_lds[];
+    WJob J = JT.j[0];
+#pragma unroll
+    for (int q = 1; q < MAXJ; q++)
+        if (q < JT.n && (int)blockIdx.x >= JT.j[q].block0) J = JT.j[q];
+    // job shapes (host-checked in dw_split_once): krows = 256 with nrows 256 or 32 -> COL; nrows =
+    // 256 with krows 96 or 16 -> ROW
+    if (J.krows == 256) {
+        if (J.nrows == 256)
+            dws_run<true, 8>(J, Ns, dz, saved, slabs, dws_lds);
+        else
+            dws_run<true, 1>(J, Ns, dz, saved, slabs, dws_lds);
+    } else if (J.krows > 32) {
+        dws_run<false, 3>(J, Ns, dz, saved, slabs, dws_lds);
+    } else {
+        dws_run<false, 1>(J, Ns, dz, saved, slabs, dws_lds);
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1244,17 +1465,21 @@ size_t saved_floats(int flags, int N) {
     return (size_t)F.nsaved * Ns + (size_t)F.nmask * (Ns / 32) + TC_FLOATS;
 }
 
-// dW arithmetic (DGS_MLP_SPLIT_DW): 2 = the split-bf16 k_dwg above (LDS-DMA staged), 1 = the split-bf16
-// k_dw (VGPR staged), 0 = the fp32-input MFMA k_dw of mlp.hip, all on the same [rows][Ns] arrays
+// dW arithmetic (DGS_MLP_SPLIT_DW): 3 (default) = the split-bf16 k_dws (private / shared operands,
+// every value split once), 2 = the split-bf16 k_dwg (LDS-DMA staged, per-wave splits), 1 = the
+// split-bf16 k_dw (VGPR staged, split phase), 0 = the fp32-input MFMA k_dw of mlp.hip, all on the
+// same [rows][Ns] arrays
 static int dw_mode() {
     static const int m = [] {
         const char *e = getenv("DGS_MLP_SPLIT_DW");
-        return (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 0;
+        return (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 3;
     }();
     return m;
 }
 static int dw_glds(const Flags &F, size_t Ns, const float *dz, const float *saved, float *slabs, float *const *grads,
                    hipStream_t stream);
+static int dw_split_once(const Flags &F, size_t Ns, const float *dz, const float *saved, float *slabs,
+                         float *const *grads, hipStream_t stream);
 
 size_t scratch_floats(int flags, int N) {
     const Flags F = make_flags(flags);
@@ -1344,8 +1569,10 @@ int backward(int flags, int N, const float *packed, const float *saved, const fl
         rc = mlp::dw_fp32(F, Ns, dz, saved, slabs, grads, stream);
     else if (dw_mode() == 1)
         rc = dw_split(F, Ns, dz, saved, slabs, grads, stream);
-    else
+    else if (dw_mode() == 2)
         rc = dw_glds(F, Ns, dz, saved, slabs, grads, stream);
+    else
+        rc = dw_split_once(F, Ns, dz, saved, slabs, grads, stream);
     if (rc != DGS_OK || !F.uniform_t) return rc;
     TGradArgs g{};
     g.fp = packed + P.img_floats();
@@ -1369,6 +1596,29 @@ static int dw_split(const Flags &F, size_t Ns, const float *dz, const float *sav
         hipLaunchKernelGGL(k_dw, dim3(W.nblocks), dim3(DW_THREADS), DW_LDS, stream, W.jobs, Ns, dz, saved, slabs);
     }
     DGS_LAUNCH_CHECK("k_dw", false, stream);
+    return launch_dw_reduce(F, W, slabs, grads, stream);
+}
+
+static int dw_split_once(const Flags &F, size_t Ns, const float *dz, const float *saved, float *slabs,
+                         float *const *grads, hipStream_t stream) {
+    if ((size_t)WT * Ns * 4 >= 0x7fffffffull)  // 32-bit byte offsets of a 256-row operand
+        return mlp::dw_fp32(F, Ns, dz, saved, slabs, grads, stream);
+    const WPlan W = split_wplan(F);
+    for (int q = 0; q < W.jobs.n; q++) {  // the shapes k_dws instantiates
+        const WJob &j = W.jobs.j[q];
+        const bool ok = (j.krows == 256 && (j.nrows == 256 || j.nrows == 32)) ||
+                        (j.nrows == 256 && (j.krows == 96 || j.krows == 16));
+        if (!ok) {
+            set_error("dgs_deform_backward: dW job shape outside k_dws's instantiations");
+            return DGS_ERR_ARGS;
+        }
+    }
+    {
+        if (int rc = ensure_dynamic_lds((const void *)k_dws, S_LDS)) return rc;
+        ScopedTimer tm("mlp_dw", stream);
+        hipLaunchKernelGGL(k_dws, dim3(W.nblocks), dim3(DW_THREADS), S_LDS, stream, W.jobs, Ns, dz, saved, slabs);
+    }
+    DGS_LAUNCH_CHECK("k_dws", false, stream);
     return launch_dw_reduce(F, W, slabs, grads, stream);
 }
 
