@@ -1078,43 +1078,41 @@ __global__ __launch_bounds__(DW_THREADS) void k_dwg(WJobs JT, size_t Ns, const f
 // with the next chunk's shared split (3 ds_write_b64 per float4) and loads interleaved | ONE barrier.
 //   LDS: split planes in fragment order, unit (16 B) [split][k-step][32-row block][lane = 32 h + i]
 //   (row i, points 8h..8h+7): a fragment is one conflict-free ds_read_b128 per split; 2 x 48 KiB.
-//   Numerics: each tile's twelve products of a chunk (two k-steps x six, the corrections first) go
+//   Numerics: each tile's twelve products of a chunk (per k-step the five corrections, then hh) go
 //   into a fresh accumulator T, added to the running sum in fp32 (tools/mfma_accum_probe.hip: a
-//   long running MFMA C loses the low bits of small terms with a bias).
+//   long running MFMA C loses the low bits of small terms with a bias; within one chunk's T that
+//   loss stays below fp32's own rounding of T).
 // Same job plan, slab layout and k_dw_reduce as the fp32 k_dw.
 // ------------------------------------------------------------------------------------------------
 constexpr int S_UNITS = NSPLIT * 2 * 8 * 64;  // 16-B units per chunk buffer
 constexpr int S_LDS = 2 * S_UNITS * 16;       // bytes (96 KiB)
 static_assert(S_LDS <= 160 * 1024, "dWs LDS");
 
-__device__ __forceinline__ constexpr int s_unit(int p, int ks, int rb, int l) { return ((p * 2 + ks) * 8 + rb) * 64 + l; }
+// unit of (split p, k-step ks, row block rb, point half hh, row i): each 32-unit half is rotated
+// by 4 ks + 2 hh, so the row-major staging stores (8 lanes per row: all (ks, hh, 8-byte half)
+// combinations of 2 rows per 16-lane group) hit 32 distinct banks; a fragment read stays one
+// conflict-free 1 KiB ds_read_b128
+__device__ __forceinline__ constexpr int s_unit(int p, int ks, int rb, int hh, int i) {
+    return ((p * 2 + ks) * 8 + rb) * 64 + 32 * hh + ((i + 4 * ks + 2 * hh) & 31);
+}
 
 __device__ __forceinline__ AFrag s_frag(const bf16x8 *L, int ks, int rb, int lane) {
-    return AFrag{L[s_unit(0, ks, rb, lane)], L[s_unit(1, ks, rb, lane)], L[s_unit(2, ks, rb, lane)]};
+    const int hh = lane >> 5, i = lane & 31;
+    return AFrag{L[s_unit(0, ks, rb, hh, i)], L[s_unit(1, ks, rb, hh, i)], L[s_unit(2, ks, rb, hh, i)]};
 }
 
-// one tile's products of a 32-point chunk (fragments of k-steps 0 / 1) into a fresh accumulator:
-// the ten corrections first, then the two hh products
-__device__ __forceinline__ f32x16 mma12(const AFrag &a0, const AFrag &b0, const AFrag &a1, const AFrag &b1) {
-    f32x16 t = MFMA32(a0.m, b0.m, (f32x16)(0.f));
-    t = MFMA32(a0.h, b0.l, t);
-    t = MFMA32(a0.l, b0.h, t);
-    t = MFMA32(a1.m, b1.m, t);
-    t = MFMA32(a1.h, b1.l, t);
-    t = MFMA32(a1.l, b1.h, t);
-    t = MFMA32(a0.h, b0.m, t);
-    t = MFMA32(a0.m, b0.h, t);
-    t = MFMA32(a1.h, b1.m, t);
-    t = MFMA32(a1.m, b1.h, t);
-    t = MFMA32(a0.h, b0.h, t);
-    return MFMA32(a1.h, b1.h, t);
+// one k-step's six products into t (the five corrections first)
+__device__ __forceinline__ f32x16 mma6_into(const AFrag &a, const AFrag &b, f32x16 t) {
+    t = MFMA32(a.m, b.m, t);
+    t = MFMA32(a.h, b.l, t);
+    t = MFMA32(a.l, b.h, t);
+    t = MFMA32(a.h, b.m, t);
+    t = MFMA32(a.m, b.h, t);
+    return MFMA32(a.h, b.h, t);
 }
 
-// acc += t (this file is built with -fno-slp-vectorize: no v_pk_add_f32 beside the MFMAs)
-__device__ __forceinline__ void add16(f32x16 &acc, const f32x16 &t) {
-#pragma unroll
-    for (int r = 0; r < 16; r++) acc[r] += t[r];
-}
+// acc += t (v_pk_add_f32 or v_add_f32: measured alike here)
+__device__ __forceinline__ void add16(f32x16 &acc, const f32x16 &t) { acc += t; }
 
 template <bool COL, int NS>
 __device__ __forceinline__ void dws_run(const WJob &J, size_t Ns, const float *__restrict__ dz,
@@ -1140,21 +1138,33 @@ __device__ __forceinline__ void dws_run(const WJob &J, size_t Ns, const float *_
     // private: lane (i, h) holds row 32 w + i, points 8 h .. + 7 of each k-step (fragment layout)
     const int pvoff = ((32 * wave + i) * (int)Ns + 8 * h) * 4;
     float4 pr[4];  // [k-step][half]
+#ifdef DGS_DWS_L2  // timing experiment only (wrong results): every chunk re-reads chunks 0 / 1 (cache-resident)
+#define DWS_C(c) ((c) & 1)
+#else
+#define DWS_C(c) (c)
+#endif
     auto pload = [&](int c) {
 #pragma unroll
         for (int q = 0; q < 4; q++)
             pr[q] = __builtin_bit_cast(float4,
-                                       __builtin_amdgcn_raw_buffer_load_b128(rsP, pvoff, c * 128 + (q >> 1) * 64 + (q & 1) * 16, 0));
+                                       __builtin_amdgcn_raw_buffer_load_b128(rsP, pvoff, DWS_C(c) * 128 + (q >> 1) * 64 + (q & 1) * 16, 0));
     };
-    // shared staging: slot g = tid + 512 f -> row g >> 3, points 4 (g & 7) .. + 3 of the chunk
+    // shared staging: slot g = tid + 512 f -> row g >> 3, points 4 (g & 7) .. + 3 of the chunk (8
+    // lanes read a row's 128 B)
     float4 st[NSF];
+    auto sslot = [&](int f, int &row, int &q) {
+        const int g = tid + 512 * f;
+        row = g >> 3;
+        q = g & 7;
+        return SROWS * 8 % 512 == 0 || g < SROWS * 8;
+    };
     auto sload = [&](int c) {
 #pragma unroll
         for (int f = 0; f < NSF; f++) {
-            const int g = tid + 512 * f;
-            if (SROWS * 8 % 512 == 0 || g < SROWS * 8)
+            int row, q;
+            if (sslot(f, row, q))
                 st[f] = __builtin_bit_cast(
-                    float4, __builtin_amdgcn_raw_buffer_load_b128(rsS, ((g >> 3) * (int)Ns + 4 * (g & 7)) * 4, c * 128, 0));
+                    float4, __builtin_amdgcn_raw_buffer_load_b128(rsS, (row * (int)Ns + 4 * q) * 4, DWS_C(c) * 128, 0));
         }
     };
     float bsum[NSF] = {};  // COL: bias row sums of the staged dZ rows; ROW: bsum[0] of the private row
@@ -1162,14 +1172,13 @@ __device__ __forceinline__ void dws_run(const WJob &J, size_t Ns, const float *_
     // `live`: the staged chunk is a real one (the last chunk re-splits a stale copy into the buffer
     // nobody reads again; it must not count in the bias sums)
     auto sput = [&](int f, int buf, bool live) {
-        const int g = tid + 512 * f;
-        if (!(SROWS * 8 % 512 == 0 || g < SROWS * 8)) return;
+        int row, q;
+        if (!sslot(f, row, q)) return;
         const float4 v = st[f];
         if (COL) bsum[f] += live ? (v.x + v.y) + (v.z + v.w) : 0.f;
         const Split4 s = split4(v.x, v.y, v.z, v.w);
-        const int row = g >> 3, q = g & 7;
         char *p = lb + buf * (S_UNITS * 16) +
-                  s_unit(0, q >> 2, row >> 5, 32 * ((q >> 1) & 1) + (row & 31)) * 16 + 8 * (q & 1);
+                  s_unit(0, q >> 2, row >> 5, (q >> 1) & 1, row & 31) * 16 + 8 * (q & 1);
         *reinterpret_cast<bf16x4 *>(p) = s.h;
         *reinterpret_cast<bf16x4 *>(p + 2 * 8 * 64 * 16) = s.m;
         *reinterpret_cast<bf16x4 *>(p + 2 * 2 * 8 * 64 * 16) = s.l;
@@ -1203,8 +1212,11 @@ __device__ __forceinline__ void dws_run(const WJob &J, size_t Ns, const float *_
             pload(min(c + 1, c1 - 1));
 #pragma unroll
             for (int s = 0; s < NS; s++) {
-                const AFrag s0 = s_frag(L, 0, s, lane), s1 = s_frag(L, 1, s, lane);
-                add16(acc[s], COL ? mma12(s0, pf0, s1, pf1) : mma12(pf0, s0, pf1, s1));
+                // the tile's two k-steps into a fresh accumulator, one shared fragment live at a time
+                const AFrag s0 = s_frag(L, 0, s, lane);
+                f32x16 T = COL ? mma6_into(s0, pf0, (f32x16)(0.f)) : mma6_into(pf0, s0, (f32x16)(0.f));
+                const AFrag s1 = s_frag(L, 1, s, lane);
+                add16(acc[s], COL ? mma6_into(s1, pf1, T) : mma6_into(pf1, s1, T));
 #pragma unroll
                 for (int f = 0; f < NSF; f++)
                     if (put_at(f) == s) sput(f, buf ^ 1, more);
@@ -1225,14 +1237,15 @@ __device__ __forceinline__ void dws_run(const WJob &J, size_t Ns, const float *_
     float *slab = slabs + (size_t)blockIdx.x * SLAB;
     if (COL) {
         // bias row sums: the 8 lanes staging a row hold its partial sums (fixed xor-tree order)
+        // bias row sums: the 8 lanes staging a row hold its partial sums (fixed xor-tree order)
 #pragma unroll
         for (int f = 0; f < NSF; f++) {
             float v = bsum[f];
             v += __shfl_xor(v, 1);
             v += __shfl_xor(v, 2);
             v += __shfl_xor(v, 4);
-            const int g = tid + 512 * f;
-            if ((g & 7) == 0 && g < SROWS * 8) slab[WT * WT + (g >> 3)] = v;
+            int row, q;
+            if (sslot(f, row, q) && q == 0) slab[WT * WT + row] = v;
         }
     } else if (pact) {
         const float v = bsum[0] + __shfl_xor(bsum[0], 32);
