@@ -43,9 +43,12 @@ __global__ __launch_bounds__(256) void k_preprocess(
     const float *proj, const float *campos, int W, int H, float tanx, float tany, float fx, float fy,
     int gx, int gy, int *__restrict__ radii, float2 *__restrict__ xy, float4 *__restrict__ conic_o,
     float4 *__restrict__ rgbd, uint32_t *__restrict__ tiles, uint8_t *__restrict__ clamped,
-    uint32_t *__restrict__ dkey, uint32_t *__restrict__ gid) {
+    uint32_t *__restrict__ dkey, uint32_t *__restrict__ gid, float4 *__restrict__ acc) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P) return;
+    // zero this Gaussian's backward accumulator row (the blend backward adds into it): no memset
+    // launch in the backward
+    acc[3 * i] = acc[3 * i + 1] = acc[3 * i + 2] = make_float4(0.f, 0.f, 0.f, 0.f);
     Cam cam;
     load_cam(cam, view, proj, campos);
     radii[i] = 0;
@@ -936,13 +939,16 @@ extern "C" int dgs_raster_forward(const dgs_raster_settings *s, int P, int M, co
 
     const float fx = c->W / (2.f * s->tanfovx), fy = c->H / (2.f * s->tanfovy);
     int nr = 0;
+    // backward accumulators [P][12] (zeroed by k_preprocess)
+    if (P > 0)
+        if (int rc = c->acc.ensure(4ull * ACC_STRIDE * P)) return rc;
     if (P > 0) {
         {
             ScopedTimer tm("preprocess_fwd", stream);
             hipLaunchKernelGGL(k_preprocess, dim3(div_up(P, 256)), dim3(256), 0, stream, P, s->sh_degree, M, means3D, scales,
                                s->scale_modifier, rotations, cov3D_precomp, opacities, shs, colors_precomp, s->viewmatrix,
                                s->projmatrix, s->campos, c->W, c->H, s->tanfovx, s->tanfovy, fx, fy, c->gx, c->gy, out_radii,
-                               c->xy, c->conic_o, c->rgbd, c->tiles, c->clamped, c->dkey, c->gid);
+                               c->xy, c->conic_o, c->rgbd, c->tiles, c->clamped, c->dkey, c->gid, (float4 *)c->acc.p);
         }
         DGS_LAUNCH_CHECK("k_preprocess", dbg, stream);
         {
@@ -1013,9 +1019,7 @@ extern "C" int dgs_raster_backward(dgs_raster_ctx *c, const float *dL_dcolor, co
     if (P == 0) return DGS_OK;
     const bool dbg = c->s.debug != 0;
     const int T = c->gx * c->gy;
-    if (int rc = c->acc.ensure(4ull * ACC_STRIDE * P)) return rc;
-    float *acc = (float *)c->acc.p;
-    DGS_HIP_CHECK(hipMemsetAsync(acc, 0, 4ull * ACC_STRIDE * P, stream));
+    float *acc = (float *)c->acc.p;  // [P][12], zeroed by the forward's k_preprocess
     if (c->num_rendered > 0) {
         ScopedTimer tm("blend_bwd", stream);
         hipLaunchKernelGGL(k_blend_bwd, dim3(T), dim3(TILE_PIX), 0, stream, c->ranges, c->vals, c->W, c->H, c->gx, c->s.bg,

@@ -78,7 +78,9 @@ class Camera:
         self.data_device = dev
         self.fid = torch.tensor([fid], dtype=torch.float32, device=dev)
         self.original_image = None if image is None else image.clamp(0.0, 1.0).to(dev)
-        self.world_view_transform = torch.tensor(getWorld2View2(R, T, trans, scale)).transpose(0, 1).to(dev)
+        # stored contiguous (same values as the reference's transposed view): the rasterizer takes it as
+        # a raw 4x4 row-major pointer, so a strided view would cost a copy kernel per render
+        self.world_view_transform = torch.tensor(getWorld2View2(R, T, trans, scale)).transpose(0, 1).contiguous().to(dev)
         self.projection_matrix = getProjectionMatrix(self.znear, self.zfar, FoVx, FoVy).transpose(0, 1).to(dev)
         self.full_proj_transform = self.world_view_transform.unsqueeze(0).bmm(
             self.projection_matrix.unsqueeze(0)).squeeze(0)

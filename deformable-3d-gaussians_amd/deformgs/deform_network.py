@@ -139,9 +139,16 @@ class _DeformBase(nn.Module):
         # or a stride-0 expand; the kernels then form the timenet gradients from the bias gradients
         uniform = t.numel() == 1 or (t.dim() >= 1 and t.shape[0] == N and t.stride(0) == 0)
         x = x.detach().float().contiguous()
-        t = t.detach().float().reshape(-1, 1).expand(N, 1).contiguous()
+        params = self.kernel_params()
+        saves = torch.is_grad_enabled() and any(p.requires_grad for p in params)
+        if uniform and saves and self.is_blender and not self.exact_fp32 and t.dtype == torch.float32:
+            # a training forward of the split path of a blender network (timenet) with one frame time
+            # reads t[0] only (k_timenet): pass the (stride-0) column as is, no per-step copy kernel
+            t = t.detach()
+        else:
+            t = t.detach().float().reshape(-1, 1).expand(N, 1).contiguous()
         flags = self.flags | (FLAG_EXACT_FP32 if self.exact_fp32 else 0) | (FLAG_UNIFORM_T if uniform else 0)
-        return _FusedDeformMLP.apply(flags, x, t, *self.kernel_params())
+        return _FusedDeformMLP.apply(flags, x, t, *params)
 
     def forward(self, x, t):
         out = self.raw(x, t)

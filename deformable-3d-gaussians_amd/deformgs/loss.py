@@ -75,6 +75,7 @@ class _FusedL1SSIM(torch.autograd.Function):
                                            _lib.ptr(scratch), _lib.stream_ptr(img.device)), "l1_ssim_forward")
         ctx.save_for_backward(img, gt, scratch)
         ctx.lam = float(lambda_dssim)
+        ctx.set_materialize_grads(False)  # l1 / ssim are not differentiable: no zero-fill kernels
         loss, l1, s = out[0], out[1], out[2]
         ctx.mark_non_differentiable(l1, s)
         return loss, l1, s
@@ -83,6 +84,8 @@ class _FusedL1SSIM(torch.autograd.Function):
     def backward(ctx, dloss, dl1, dssim):
         from . import _lib
         img, gt, scratch = ctx.saved_tensors
+        if dloss is None:
+            return None, None, None
         C, H, W = img.shape[-3:]
         grad = torch.empty_like(img)
         dl = dloss.float().contiguous()

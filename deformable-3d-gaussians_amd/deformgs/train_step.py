@@ -27,8 +27,19 @@ def forward_backward(gaussians, deform, cam, gt_image, pipe, background, is_6dof
     image = pkg["render"]
     # (1-l)*l1_loss(image, gt) + l*(1-ssim(image, gt)) (train_baseline.py:126-127), fused HIP kernels
     loss, Ll1, _ = l1_ssim_loss(image, gt_image, lambda_dssim)
-    loss.backward()
+    loss.backward(_unit(loss))
     return loss, pkg
+
+
+_UNITS = {}
+
+
+def _unit(loss):
+    """d loss / d loss = 1, cached per device (loss.backward() would fill a new ones tensor)."""
+    u = _UNITS.get(loss.device)
+    if u is None or u.dtype != loss.dtype:
+        u = _UNITS[loss.device] = torch.ones((), dtype=loss.dtype, device=loss.device)
+    return u
 
 
 def optimizer_step(gaussians, deform, iteration):

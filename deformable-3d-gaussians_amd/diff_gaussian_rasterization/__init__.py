@@ -126,6 +126,7 @@ class _RasterizeGaussians(torch.autograd.Function):
                                     handle, nr, _lib.stream_ptr(dev))
         _lib.check(rc, "rasterize_gaussians")
         ctx.raster = _Ctx(handle)
+        ctx.raster_hw = (H, W)
         ctx.keep = keep
         ctx.num_rendered = nr.value
         ctx.M = M
@@ -134,6 +135,8 @@ class _RasterizeGaussians(torch.autograd.Function):
                       None if rotations is None else rotations.shape)
         ctx.save_for_backward(means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp, radii)
         ctx.mark_non_differentiable(radii)
+        # an unused depth output (every training loss here) arrives as None: no zero-fill kernel
+        ctx.set_materialize_grads(False)
         return color, radii, depth
 
     @staticmethod
@@ -153,6 +156,8 @@ class _RasterizeGaussians(torch.autograd.Function):
         d_shs = e(*shs.shape) if has_sh else None
         d_scales = e(P, 3) if not has_cov else None
         d_rots = e(P, 4) if not has_cov else None
+        if grad_color is None:
+            grad_color = torch.zeros((3, ctx.raster_hw[0], ctx.raster_hw[1]), dtype=torch.float32, device=dev)
         gc = _f32(grad_color)
         gd = _f32(grad_depth) if grad_depth is not None else None
         rc = lib.dgs_raster_backward(ctx.raster.handle, _lib.ptr(gc), _lib.ptr(gd), _lib.ptr(d_means3D),
