@@ -24,11 +24,13 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <tuple>
 #include <vector>
 
+#include "radix.h"
 #include "raster_kernels.h"
 
 namespace dgs {
@@ -697,6 +699,15 @@ std::vector<dgs_raster_ctx *> g_pool;
 
 size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 
+// DGS_HIPCUB_SORT=1: hipcub::DeviceRadixSort for the depth and tile sorts instead of radix.hip
+bool hipcub_sort() {
+    static const bool v = [] {
+        const char *e = getenv("DGS_HIPCUB_SORT");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
 // hipcub temp-storage sizes, cached per (device, size class): the size queries cost tens of us of
 // host time each inside the num_rendered sync window. Sizes are queried for the class's upper end
 // (temp storage grows monotonically with the item count).
@@ -810,8 +821,9 @@ template <class KT>
 static int bin_tiles(dgs_raster_ctx *c, int cap, int P, int device, hipStream_t stream, bool dbg) {
     const int T = c->gx * c->gy;
     const int end_bit = bits_for((uint32_t)T);
+    const bool cub = hipcub_sort();
     size_t sort_tmp = 0;
-    DGS_HIP_CHECK(sort_tmp_bytes<KT>(device, cap, end_bit, stream, sort_tmp));
+    if (cub) DGS_HIP_CHECK(sort_tmp_bytes<KT>(device, cap, end_bit, stream, sort_tmp));
     size_t o_k0 = 0, o_k1 = align_up(sizeof(KT) * cap), o_v0 = align_up(o_k1 + sizeof(KT) * cap),
            o_v1 = align_up(o_v0 + 4ull * cap), o_t = align_up(o_v1 + 4ull * cap);
     if (int rc = c->bin.ensure(o_t + sort_tmp + 256)) return rc;
@@ -824,17 +836,26 @@ static int bin_tiles(dgs_raster_ctx *c, int cap, int P, int device, hipStream_t 
                            c->offsets, c->gx, c->gy, k0, v0, (uint32_t)cap, c->ranges, c->gx * c->gy);
     }
     DGS_LAUNCH_CHECK("k_duplicate", dbg, stream);
-    hipcub::DoubleBuffer<KT> kbuf(k0, k1);
-    hipcub::DoubleBuffer<uint32_t> vbuf(v0, v1);
+    KT *ksorted = k0;
     {
         ScopedTimer tm("sort", stream);
-        DGS_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(b + o_t, sort_tmp, kbuf, vbuf, cap, 0, end_bit, stream));
+        if (cub) {
+            hipcub::DoubleBuffer<KT> kbuf(k0, k1);
+            hipcub::DoubleBuffer<uint32_t> vbuf(v0, v1);
+            DGS_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(b + o_t, sort_tmp, kbuf, vbuf, cap, 0, end_bit, stream));
+            c->vals = vbuf.Current();
+            ksorted = kbuf.Current();
+        } else {
+            int alt = 0;
+            if (int rc = radix::sort_pairs<KT>(k0, k1, v0, v1, cap, end_bit, stream, &alt)) return rc;
+            c->vals = alt ? v1 : v0;
+            ksorted = alt ? k1 : k0;
+        }
     }
-    c->vals = vbuf.Current();
     {
         ScopedTimer tm("ranges", stream);
         hipLaunchKernelGGL(k_ranges<KT>, dim3(div_up(cap, 256)), dim3(256), 0, stream, c->offsets + (P - 1),
-                           (uint32_t)cap, kbuf.Current(), c->ranges);
+                           (uint32_t)cap, ksorted, c->ranges);
     }
     DGS_LAUNCH_CHECK("k_ranges", dbg, stream);
     return DGS_OK;
@@ -954,13 +975,23 @@ extern "C" int dgs_raster_forward(const dgs_raster_settings *s, int P, int M, co
         {
             // Gaussians by depth (stable on the index), then the pair offsets in that order
             ScopedTimer tm("depth_sort", stream);
-            hipcub::DoubleBuffer<uint32_t> kb(c->dkey, c->dkey_alt), vb(c->gid, c->order);
-            DGS_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(g + off_st, dsort_tmp, kb, vb, P, 0, 32, stream));
-            c->order = vb.Current();  // either buffer, per the pass count
-            hipLaunchKernelGGL(k_gather_tiles, dim3(div_up(P, 256)), dim3(256), 0, stream, P, c->order, c->tiles,
-                               c->tiles_sorted);
+            if (hipcub_sort()) {
+                hipcub::DoubleBuffer<uint32_t> kb(c->dkey, c->dkey_alt), vb(c->gid, c->order);
+                DGS_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(g + off_st, dsort_tmp, kb, vb, P, 0, 32, stream));
+                c->order = vb.Current();  // either buffer, per the pass count
+                hipLaunchKernelGGL(k_gather_tiles, dim3(div_up(P, 256)), dim3(256), 0, stream, P, c->order, c->tiles,
+                                   c->tiles_sorted);
+            } else {
+                // the last pass also gathers tiles[order[j]] (the scan input) into tiles_sorted
+                int alt = 0;
+                uint32_t *gid = c->gid, *ord = c->order;
+                if (int rc = radix::sort_pairs<uint32_t>(c->dkey, c->dkey_alt, gid, ord, P, 32, stream, &alt, c->tiles,
+                                                         c->tiles_sorted))
+                    return rc;
+                c->order = alt ? ord : gid;
+            }
         }
-        DGS_LAUNCH_CHECK("k_gather_tiles", dbg, stream);
+        DGS_LAUNCH_CHECK("depth_sort", dbg, stream);
         DGS_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(g + off_st, scan_tmp, c->tiles_sorted, c->offsets, P, stream));
         if (!c->h_total) DGS_HIP_CHECK(hipHostMalloc((void **)&c->h_total, sizeof(uint32_t), hipHostMallocDefault));
         if (!c->count_ev) DGS_HIP_CHECK(hipEventCreateWithFlags(&c->count_ev, hipEventDisableTiming));
