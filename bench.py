@@ -68,8 +68,13 @@ def mfma_peak(name):
     return SPLIT_MFMA_PEAK_TFLOPS, "bf16 MFMA peak / 6 (exact hi/mid/lo split, six products per fp32 product)"
 
 
-def kernel_algorithmic(name, N, P, HW):
-    """(amount, unit, bound) per launch for the roofline of a kernel class."""
+def kernel_algorithmic(name, N, P, HW, cap=None, T=None):
+    """(amount, unit, bound) per launch for the roofline of a kernel class. P = pairs,
+    cap = the launched pair capacity of the sort-path kernels (>= P; their loops cover cap items),
+    T = tiles."""
+    cap = max(cap or P, P)
+    T = T or 1
+    NB = -(-N // 256)
     if name == "mlp_fwd":
         return 2.0 * MLP_FWD_MAC * N, "flop", "mfma"
     if name == "mlp_bwd":
@@ -84,14 +89,24 @@ def kernel_algorithmic(name, N, P, HW):
         return 44.0 * P + 24.0 * HW, "byte", "hbm"
     if name == "blend_bwd":
         return 44.0 * P + 24.0 * HW + 48.0 * N, "byte", "hbm"
-    if name == "sort":
-        return 24.0 * P, "byte", "hbm"       # 2 passes x (read + write) x (2-B key + 4-B id)
     if name == "depth_sort":
         return 64.0 * N, "byte", "hbm"       # 4 passes x (read + write) x (4-B key + 4-B id)
+    # rect binning (default): count matrix NB x T u32, no keys
+    if name == "count":
+        return 16.0 * N + 4.0 * NB * T, "byte", "hbm"      # order, xy, radii in; count matrix out
+    if name == "scan":
+        return 8.0 * NB * T + 4.0 * T, "byte", "hbm"       # count matrix in + offsets out; tile totals
+    if name == "starts":
+        return 16.0 * T, "byte", "hbm"                      # totals in; starts + ranges out
+    if name == "place":
+        return 16.0 * N + 4.0 * NB * T + 4.0 * T + 4.0 * P, "byte", "hbm"  # + pair ids out
+    # sort binning (DGS_BINNING=sort): loops cover the launched capacity
+    if name == "sort":
+        return 24.0 * cap, "byte", "hbm"     # 2 passes x (read + write) x (2-B key + 4-B id)
     if name == "duplicate":
-        return 20.0 * N + 12.0 * P, "byte", "hbm"
+        return 20.0 * N + 12.0 * cap, "byte", "hbm"  # + all-ones key fill of the tail
     if name == "ranges":
-        return 8.0 * P, "byte", "hbm"
+        return 8.0 * cap, "byte", "hbm"
     if name == "ssim_fwd":
         return 3 * HW * (4 + 4 + 12), "byte", "hbm"
     if name == "ssim_bwd":
@@ -99,8 +114,8 @@ def kernel_algorithmic(name, N, P, HW):
     return None
 
 
-KERNEL_CLASSES = ["mlp_fwd", "mlp_bwd", "mlp_dw", "mlp_dw_reduce", "preprocess_fwd", "depth_sort", "duplicate", "sort",
-                  "ranges",
+KERNEL_CLASSES = ["mlp_fwd", "mlp_bwd", "mlp_dw", "mlp_dw_reduce", "preprocess_fwd", "depth_sort", "count", "scan",
+                  "starts", "place", "duplicate", "sort", "ranges",
                   "blend_fwd", "blend_bwd", "preprocess_bwd", "ssim_fwd", "ssim_bwd"]
 
 
@@ -242,6 +257,8 @@ def main():
     pk = render(cams[0], gaussians, pipe, bg, d[0], d[1], d[2])
     P_pairs = int(pk["render"].grad_fn.num_rendered) if hasattr(pk["render"].grad_fn, "num_rendered") else 0
     del pk
+    pair_cap = int(lib.dgs_debug_pair_cap(local))  # the speculative capacity the sort-path loops cover
+    n_tiles = -(-R // 16) * -(-R // 16)
 
     kernels = {}
     for name in KERNEL_CLASSES:
@@ -252,7 +269,7 @@ def main():
     HW = R * R
     best = None
     for name, (ms, n) in kernels.items():
-        info = kernel_algorithmic(name, N, P_pairs, HW)
+        info = kernel_algorithmic(name, N, P_pairs, HW, cap=pair_cap, T=n_tiles)
         if info is None:
             continue
         if best is None or ms > best[1]:
@@ -291,6 +308,7 @@ def main():
         "config": {"workload": f"synth-100k: {N} Gaussians, {R}x{R}, blender DeformNetworkBaseline, SH3"
                    + (" (raw-init heads)" if args.raw_init else " (heads at 1/100 init: steady-state deltas)"),
                    "global_batch": world, "includes_adam": not args.no_adam, "pairs_per_render": P_pairs,
+                   "pair_capacity": pair_cap,
                    "parallelism": f"dp{world} (frame-parallel, RCCL grad all-reduce)"},
         "roofline": roofline,
         "kernels_ms_per_step": {k: v[0] / args.steps for k, v in kernels.items()},

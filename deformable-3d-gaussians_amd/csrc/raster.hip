@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <map>
+#include <atomic>
 #include <mutex>
 #include <tuple>
 #include <vector>
@@ -170,6 +171,162 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t *__rest
             }
             off++;
         }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Rect binning (the default for images up to RECT_MAX_TILES tiles): the (tile, Gaussian) pairs are
+// placed directly at their position in the tile-sorted order instead of being emitted and radix-
+// sorted. The Gaussians are already in depth order (stable on the index), and Gaussian j covers the
+// tile rectangle of its 3-sigma radius, so the position of pair (j, t) in the stable tile sort is
+//   tile_start[t] + #{j' < j : t in rect(j')}
+// counted hierarchically over blocks of 256 depth-ordered Gaussians: k_rect_count (per block and
+// tile), k_rect_colscan (exclusive down each tile's column of blocks, tile totals, pair count),
+// k_rect_starts (tile starts = scan of the totals; the ranges), k_rect_place (per wave and tile in
+// LDS, then the lanes below in the wave). Same order as the sort, bit for bit; no keys.
+// ------------------------------------------------------------------------------------------------
+constexpr int RECT_MAX_TILES = 12288;     // LDS of the count/place kernels: 4 B per tile (<= 64 KiB)
+constexpr long long RECT_MAX_CELLS = 1 << 24;  // blocks x tiles of the count matrix
+
+__device__ inline bool gauss_rect(uint32_t g, const float2 *xy, const int *radii, int gx, int gy, int4 &rc) {
+    const int r = radii[g];
+    if (r <= 0) return false;
+    const float2 c = xy[g];
+    tile_rect(c.x, c.y, r, gx, gy, rc.x, rc.y, rc.z, rc.w);
+    return rc.x < rc.z && rc.y < rc.w;
+}
+
+__global__ __launch_bounds__(256) void k_rect_count(int P, const uint32_t *__restrict__ order, const float2 *__restrict__ xy,
+                                                    const int *__restrict__ radii, int gx, int gy,
+                                                    uint32_t *__restrict__ cnt, uint32_t *__restrict__ total) {
+    extern __shared__ uint32_t h[];  // [T]
+    const int T = gx * gy;
+    for (int t = threadIdx.x; t < T; t += 256) h[t] = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *total = 0;  // k_rect_colscan adds into it
+    __syncthreads();
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    int4 rc;
+    if (j < P && gauss_rect(order[j], xy, radii, gx, gy, rc))
+        for (int y = rc.y; y < rc.w; y++)
+            for (int x = rc.x; x < rc.z; x++) atomicAdd(&h[y * gx + x], 1u);
+    __syncthreads();
+    uint32_t *row = cnt + (size_t)blockIdx.x * T;
+    for (int t = threadIdx.x; t < T; t += 256) row[t] = h[t];
+}
+
+// the column of block counts of 64 tiles per workgroup -> exclusive offsets (in place), the tile
+// totals and the pair count: 16 waves take 32 rows each per 512-row chunk (loads all in flight),
+// cross-wave prefix in LDS, carry between chunks
+__global__ __launch_bounds__(1024) void k_rect_colscan(int nb, int T, uint32_t *__restrict__ cnt, uint32_t *__restrict__ tot,
+                                                       uint32_t *__restrict__ total) {
+    __shared__ uint32_t part[16][64];
+    __shared__ uint32_t carry[64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int t = blockIdx.x * 64 + lane;
+    const bool ok = t < T;
+    if (w == 0) carry[lane] = 0;
+    for (int b0 = 0; b0 < nb; b0 += 512) {
+        const int r0 = b0 + 32 * w;
+        uint32_t v[32], sum = 0;
+#pragma unroll
+        for (int k = 0; k < 32; k++) {
+            v[k] = (ok && r0 + k < nb) ? cnt[(size_t)(r0 + k) * T + t] : 0u;
+            sum += v[k];
+        }
+        part[w][lane] = sum;
+        __syncthreads();
+        uint32_t run = carry[lane];
+        for (int k = 0; k < w; k++) run += part[k][lane];
+#pragma unroll
+        for (int k = 0; k < 32; k++) {
+            if (ok && r0 + k < nb) cnt[(size_t)(r0 + k) * T + t] = run;
+            run += v[k];
+        }
+        __syncthreads();  // carry and part read by every wave
+        if (w == 15) carry[lane] = run;
+        __syncthreads();
+    }
+    if (w == 0) {
+        const uint32_t c = carry[lane];
+        if (ok) tot[t] = c;
+        uint32_t s = c;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) s += (uint32_t)__shfl_xor((int)s, o);
+        if (lane == 0) atomicAdd(total, s);
+    }
+}
+
+// tile starts = exclusive scan of the tile totals; ranges clipped to the launched pair capacity
+__global__ __launch_bounds__(1024) void k_rect_starts(int T, const uint32_t *__restrict__ tot, uint32_t cap,
+                                                      uint32_t *__restrict__ tile_start, uint2 *__restrict__ ranges) {
+    __shared__ uint32_t wsum[16];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int per = div_up(T, 1024);
+    const int t0 = tid * per;
+    uint32_t local = 0;
+    for (int k = 0; k < per; k++)
+        if (t0 + k < T) local += tot[t0 + k];
+    uint32_t x = local;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    uint32_t run = x - local;
+    for (int k = 0; k < w; k++) run += wsum[k];
+    for (int k = 0; k < per; k++) {
+        const int t = t0 + k;
+        if (t >= T) break;
+        const uint32_t c = tot[t];
+        tile_start[t] = run;
+        ranges[t] = make_uint2(min(run, cap), min(run + c, cap));
+        run += c;
+    }
+}
+
+__host__ __device__ inline size_t rect_place_lds(int gx, int gy) {
+    return 4ull * ((gx * gy + 1) & ~1) + 4ull * 8ull * (gx + gy);
+}
+
+__global__ __launch_bounds__(256) void k_rect_place(int P, const uint32_t *__restrict__ order, const float2 *__restrict__ xy,
+                                                    const int *__restrict__ radii, int gx, int gy,
+                                                    const uint32_t *__restrict__ cnt, const uint32_t *__restrict__ tile_start,
+                                                    uint32_t cap, uint32_t *__restrict__ vals) {
+    extern __shared__ uint32_t lds[];
+    const int T = gx * gy, G = gx + gy;
+    // per tile, the four waves' counts packed one byte each (a wave adds at most 64 per tile)
+    uint32_t *wc = lds;  // [T]
+    // per wave, the lanes whose rectangle spans tile column x ([x]) / tile row y ([gx + y])
+    unsigned long long *span = reinterpret_cast<unsigned long long *>(lds + ((T + 1) & ~1));  // [4][G]
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (int t = tid; t < T; t += 256) wc[t] = 0;
+    for (int t = tid; t < 4 * G; t += 256) span[t] = 0ull;
+    const int j = blockIdx.x * 256 + tid;
+    const uint32_t g = j < P ? order[j] : 0u;
+    int4 rc = make_int4(0, 0, 0, 0);
+    if (j < P && !gauss_rect(g, xy, radii, gx, gy, rc)) rc = make_int4(0, 0, 0, 0);
+    __syncthreads();
+    unsigned long long *ws = span + w * G;
+    const unsigned long long me = 1ull << lane;
+    for (int x = rc.x; x < rc.z; x++) atomicOr(&ws[x], me);
+    for (int y = rc.y; y < rc.w; y++) {
+        atomicOr(&ws[gx + y], me);
+        for (int x = rc.x; x < rc.z; x++) atomicAdd(&wc[y * gx + x], 1u << (8 * w));
+    }
+    __syncthreads();
+    const uint32_t *crow = cnt + (size_t)blockIdx.x * T;
+    for (int y = rc.y; y < rc.w; y++) {
+        const unsigned long long rows = ws[gx + y] & (me - 1ull);  // lanes below spanning row y
+        for (int x = rc.x; x < rc.z; x++) {
+            const int t = y * gx + x;
+            const uint32_t rank = (uint32_t)__popcll(rows & ws[x]);
+            // waves below: byte w-1 of the packed inclusive sums (partial sums <= 192, no carries)
+            const uint32_t below = w ? ((wc[t] * 0x01010101u) >> (8 * (w - 1))) & 0xffu : 0u;
+            const uint32_t pos = tile_start[t] + crow[t] + below + rank;
+            if (pos < cap) vals[pos] = g;
+        }
+    }
 }
 
 // L (the pair count) is read on the device and clipped to the launched capacity: an overflowing
@@ -674,7 +831,7 @@ struct dgs_raster_ctx {
     int P = 0, M = 0, H = 0, W = 0, gx = 0, gy = 0, num_rendered = 0;
     const float *means3D = nullptr, *shs = nullptr, *colors = nullptr, *opac = nullptr, *scales = nullptr,
                 *rots = nullptr, *cov = nullptr;
-    DevBuf geom, bin, img, acc, tmp;
+    DevBuf geom, bin, img, acc, tmp, rect;
     // carved views
     float2 *xy = nullptr;
     float4 *conic_o = nullptr, *rgbd = nullptr;
@@ -682,6 +839,8 @@ struct dgs_raster_ctx {
     uint32_t *dkey = nullptr, *dkey_alt = nullptr, *gid = nullptr, *order = nullptr, *tiles_sorted = nullptr;
     uint8_t *clamped = nullptr;
     uint32_t *vals = nullptr;
+    bool rect_mode = false;  // rect binning (k_rect_*) instead of duplicate + tile sort
+    uint32_t *rect_cnt = nullptr, *rect_tot = nullptr, *rect_start = nullptr, *rect_total = nullptr;
     uint2 *ranges = nullptr;
     float *final_T = nullptr;
     uint32_t *n_contrib = nullptr;
@@ -706,6 +865,27 @@ bool hipcub_sort() {
         return e && e[0] == '1';
     }();
     return v;
+}
+
+// Binning mode: 0 = rect binning up to RECT_MAX_TILES tiles and RECT_MAX_CELLS count-matrix cells
+// (the default), 1 = duplicate + tile-key radix sort + ranges for every image. Initialized from
+// DGS_BINNING=sort (or DGS_HIPCUB_SORT=1); dgs_debug_set_binning switches it at run time.
+std::atomic<int> g_binning{-1};
+
+int binning_mode() {
+    int m = g_binning.load();
+    if (m < 0) {
+        const char *e = getenv("DGS_BINNING");
+        m = ((e && strcmp(e, "sort") == 0) || hipcub_sort()) ? 1 : 0;
+        g_binning.store(m);
+    }
+    return m;
+}
+
+bool rect_binning(int gx, int gy, int P) {
+    const int T = gx * gy;
+    return binning_mode() == 0 && T <= RECT_MAX_TILES && rect_place_lds(gx, gy) <= 65536 &&
+           (long long)div_up(P, 256) * T <= RECT_MAX_CELLS;
 }
 
 // hipcub temp-storage sizes, cached per (device, size class): the size queries cost tens of us of
@@ -864,7 +1044,23 @@ static int bin_tiles(dgs_raster_ctx *c, int cap, int P, int device, hipStream_t 
 static int bin_and_blend(dgs_raster_ctx *c, int cap, int P, int device, hipStream_t stream, bool dbg, float *out_color,
                          float *out_depth) {
     const int T = c->gx * c->gy;
-    if (cap > 0) {  // k_duplicate clears c->ranges
+    if (c->rect_mode) {
+        if (int rc = c->bin.ensure(4ull * std::max(cap, 1) + 256)) return rc;
+        c->vals = (uint32_t *)c->bin.p;
+        const int nb = div_up(P, 256);
+        {
+            ScopedTimer tm("starts", stream);
+            hipLaunchKernelGGL(k_rect_starts, dim3(1), dim3(1024), 0, stream, T, c->rect_tot, (uint32_t)cap, c->rect_start,
+                               c->ranges);
+        }
+        DGS_LAUNCH_CHECK("k_rect_starts", dbg, stream);
+        if (cap > 0) {
+            ScopedTimer tm("place", stream);
+            hipLaunchKernelGGL(k_rect_place, dim3(nb), dim3(256), rect_place_lds(c->gx, c->gy), stream, P, c->order, c->xy, c->radii,
+                               c->gx, c->gy, c->rect_cnt, c->rect_start, (uint32_t)cap, c->vals);
+        }
+        DGS_LAUNCH_CHECK("k_rect_place", dbg, stream);
+    } else if (cap > 0) {  // k_duplicate clears c->ranges
         // 16-bit tile keys up to 65535 tiles (4080 x 4080 pixels), 32-bit beyond
         const int rc = T < 65535 ? bin_tiles<uint16_t>(c, cap, P, device, stream, dbg)
                                  : bin_tiles<uint32_t>(c, cap, P, device, stream, dbg);
@@ -957,6 +1153,17 @@ extern "C" int dgs_raster_forward(const dgs_raster_settings *s, int P, int M, co
     c->ranges = (uint2 *)(im + off_r);
     c->final_T = (float *)(im + off_T);
     c->n_contrib = (uint32_t *)(im + off_n);
+    c->rect_mode = P > 0 && rect_binning(c->gx, c->gy, P);
+    if (c->rect_mode) {  // count matrix [blocks][tiles], tile totals, tile starts, pair count
+        const size_t nb = div_up(P, 256);
+        size_t o_cnt = 0, o_tot = align_up(4ull * nb * T), o_st = align_up(o_tot + 4ull * T), o_n = align_up(o_st + 4ull * T);
+        if (int rc = c->rect.ensure(o_n + 256)) return rc;
+        char *r = (char *)c->rect.p;
+        c->rect_cnt = (uint32_t *)(r + o_cnt);
+        c->rect_tot = (uint32_t *)(r + o_tot);
+        c->rect_start = (uint32_t *)(r + o_st);
+        c->rect_total = (uint32_t *)(r + o_n);
+    }
 
     const float fx = c->W / (2.f * s->tanfovx), fy = c->H / (2.f * s->tanfovy);
     int nr = 0;
@@ -985,17 +1192,35 @@ extern "C" int dgs_raster_forward(const dgs_raster_settings *s, int P, int M, co
                 // the last pass also gathers tiles[order[j]] (the scan input) into tiles_sorted
                 int alt = 0;
                 uint32_t *gid = c->gid, *ord = c->order;
-                if (int rc = radix::sort_pairs<uint32_t>(c->dkey, c->dkey_alt, gid, ord, P, 32, stream, &alt, c->tiles,
-                                                         c->tiles_sorted))
+                if (int rc = radix::sort_pairs<uint32_t>(c->dkey, c->dkey_alt, gid, ord, P, 32, stream, &alt,
+                                                         c->rect_mode ? nullptr : c->tiles,
+                                                         c->rect_mode ? nullptr : c->tiles_sorted))
                     return rc;
                 c->order = alt ? ord : gid;
             }
         }
         DGS_LAUNCH_CHECK("depth_sort", dbg, stream);
-        DGS_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(g + off_st, scan_tmp, c->tiles_sorted, c->offsets, P, stream));
         if (!c->h_total) DGS_HIP_CHECK(hipHostMalloc((void **)&c->h_total, sizeof(uint32_t), hipHostMallocDefault));
         if (!c->count_ev) DGS_HIP_CHECK(hipEventCreateWithFlags(&c->count_ev, hipEventDisableTiming));
-        DGS_HIP_CHECK(hipMemcpyAsync(c->h_total, c->offsets + (P - 1), 4, hipMemcpyDeviceToHost, stream));
+        if (c->rect_mode) {
+            const int nb = div_up(P, 256);
+            {
+                ScopedTimer tm("count", stream);
+                hipLaunchKernelGGL(k_rect_count, dim3(nb), dim3(256), 4ull * T, stream, P, c->order, c->xy, c->radii, c->gx,
+                                   c->gy, c->rect_cnt, c->rect_total);
+            }
+            DGS_LAUNCH_CHECK("k_rect_count", dbg, stream);
+            {
+                ScopedTimer tm("scan", stream);
+                hipLaunchKernelGGL(k_rect_colscan, dim3(div_up(T, 64)), dim3(1024), 0, stream, nb, T, c->rect_cnt, c->rect_tot,
+                                   c->rect_total);
+            }
+            DGS_LAUNCH_CHECK("k_rect_colscan", dbg, stream);
+            DGS_HIP_CHECK(hipMemcpyAsync(c->h_total, c->rect_total, 4, hipMemcpyDeviceToHost, stream));
+        } else {
+            DGS_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(g + off_st, scan_tmp, c->tiles_sorted, c->offsets, P, stream));
+            DGS_HIP_CHECK(hipMemcpyAsync(c->h_total, c->offsets + (P - 1), 4, hipMemcpyDeviceToHost, stream));
+        }
         DGS_HIP_CHECK(hipEventRecord(c->count_ev, stream));
         int cap = pair_cap_get(device);
         const bool speculative = cap > 0 && !dbg;
@@ -1081,7 +1306,7 @@ extern "C" void dgs_raster_ctx_free(dgs_raster_ctx *c) {
     if (g_pool.size() < 64) {
         g_pool.push_back(c);
     } else {
-        c->geom.release(); c->bin.release(); c->img.release(); c->acc.release(); c->tmp.release();
+        c->geom.release(); c->bin.release(); c->img.release(); c->acc.release(); c->tmp.release(); c->rect.release();
         if (c->h_total) (void)hipHostFree(c->h_total);
         delete c;
     }
@@ -1091,6 +1316,10 @@ extern "C" void dgs_debug_set_pair_cap(int device, int cap) {
     std::lock_guard<std::mutex> lk(g_cap_mu);
     g_pair_cap[device] = cap < 0 ? 0 : cap;
 }
+
+extern "C" int dgs_debug_pair_cap(int device) { return pair_cap_get(device); }
+
+extern "C" void dgs_debug_set_binning(int mode) { g_binning.store(mode == 1 ? 1 : 0); }
 
 extern "C" long long dgs_debug_binning_redos(void) {
     std::lock_guard<std::mutex> lk(g_cap_mu);

@@ -45,6 +45,8 @@ _SIGS = {
     "dgs_mark_visible": ([I, P, P, P, P, P], I),
     "dgs_debug_set_pair_cap": ([I, I], None),
     "dgs_debug_binning_redos": ([], ctypes.c_longlong),
+    "dgs_debug_pair_cap": ([I], I),
+    "dgs_debug_set_binning": ([I], None),
     "dgs_timing_enable": ([I], None),
     "dgs_timing_query": ([ctypes.c_char_p, ctypes.POINTER(I)], ctypes.c_double),
     "dgs_timing_reset": ([], None),

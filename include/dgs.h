@@ -94,8 +94,14 @@ int dgs_mark_visible(int P, const float *means3D, const float *viewmatrix, const
  * The forward launches tile binning for a learned per-device pair capacity before it knows the
  * pair count (speculative binning) and redoes binning at the exact size when the count is larger.
  * dgs_debug_set_pair_cap overrides that capacity for `device` (0 = none: the next forward runs
- * synchronously); dgs_debug_binning_redos counts the redone (overflowing) launches so far. */
+ * synchronously); dgs_debug_pair_cap reads it back; dgs_debug_binning_redos counts the redone
+ * (overflowing) launches so far. dgs_debug_set_binning selects the binning: 0 = rect binning
+ * (count -> column scan -> place; the default where its LDS bound allows), 1 = duplicate + tile-key
+ * radix sort + ranges (the scheme of the external upstream rasterizer's duplicateWithKeys / SortPairs /
+ * identifyTileRanges, SURVEY.md section 3 kernel table). */
 void dgs_debug_set_pair_cap(int device, int cap);
+int dgs_debug_pair_cap(int device);
+void dgs_debug_set_binning(int mode);
 long long dgs_debug_binning_redos(void);
 
 /* ---- timing hooks (bench.py): per-kernel-class HIP event accumulation on the launch stream ---- */

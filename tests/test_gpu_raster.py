@@ -23,6 +23,17 @@ CONFIGS = [
 ]
 
 
+@pytest.fixture(params=["rect", "sort"])
+def binning(request):
+    """Both tile binnings: rect (count -> column scan -> place, the default) and sort (duplicate +
+    tile-key radix sort + ranges, the upstream scheme). Restores the default afterwards."""
+    from deformgs import _lib
+    lib = _lib.load()
+    lib.dgs_debug_set_binning(0 if request.param == "rect" else 1)
+    yield request.param
+    lib.dgs_debug_set_binning(0)
+
+
 def _run_gpu(inputs, rs, dcolor, ddepth, use_cov=False, use_colors=False, requires=True):
     from diff_gaussian_rasterization import GaussianRasterizer
     dev = "cuda"
@@ -65,7 +76,7 @@ def _check(o, g, color, radii, depth, grads, keys):
 
 
 @pytest.mark.parametrize("cfg", CONFIGS)
-def test_raster_sh_scale_rot(cfg):
+def test_raster_sh_scale_rot(cfg, binning):
     N, H, W, ci, boost, bg = cfg
     inputs, rs, _ = scene(N, H, W, cam_index=ci, scale_boost=boost, bg=bg)
     rng = np.random.default_rng(1)
@@ -168,7 +179,7 @@ def test_speculative_binning_matches_exact():
     assert np.abs(c - o.color).mean() <= 1e-5
 
 
-def test_speculative_overflow_redo_is_exact():
+def test_speculative_overflow_redo_is_exact(binning):
     """Force the overflow path: the per-device pair capacity is overridden with a small value that
     is not a multiple of 256 (so the ranges/sort grids overhang it), and with a capacity left over
     from a much larger frame (stale keys past the new pairs). Every forced overflow must be redone
@@ -227,3 +238,33 @@ def _grads_of(inputs, rs, debug):
     w = torch.linspace(-1, 1, color.numel(), device="cuda").reshape(color.shape)
     (color * w).sum().backward()
     return {k: v.grad.cpu().numpy() for k, v in t.items()}
+
+
+@pytest.mark.parametrize("case", [
+    # N, H, W, cam, scale_boost: small Gaussians, ragged tiles, big Gaussians (rects of many tiles),
+    # a wide image (2772 tiles), more Gaussians than one count block column (> 256 blocks)
+    (3000, 128, 96, 5, 0.0), (2000, 61, 83, 3, 1.0), (1500, 100, 120, 2, 3.0), (5000, 700, 1000, 0, 0.5),
+    (150000, 160, 160, 1, 0.0)])
+def test_rect_binning_equals_sort_binning(case):
+    """The rect binning places every (tile, Gaussian) pair where the stable tile sort of the depth-
+    ordered pairs puts it, so images, depth, radii, the pair count and every gradient must equal the
+    sort binning's bit for bit (same pair lists -> same blend order -> same float sums; gradient
+    atomics can differ in arrival order, so gradients are compared to 1e-5 relative)."""
+    from deformgs import _lib
+    lib = _lib.load()
+    N, H, W, ci, boost = case
+    inputs, rs, _ = scene(N, H, W, cam_index=ci, scale_boost=boost, seed=11)
+    out = {}
+    try:
+        for mode in (1, 0):
+            lib.dgs_debug_set_binning(mode)
+            out[mode] = (_forward_only(inputs, rs, debug=False), _forward_only(inputs, rs, debug=True),
+                         _num_rendered(inputs, rs), _grads_of(inputs, rs, debug=False))
+    finally:
+        lib.dgs_debug_set_binning(0)
+    (fs, fsd, ns, gs), (fr, frd, nr, gr) = out[1], out[0]
+    assert ns == nr and nr > 0
+    for a, b in zip(fs + fsd, fr + frd):
+        np.testing.assert_array_equal(a, b)
+    for k in gs:
+        np.testing.assert_allclose(gr[k], gs[k], rtol=1e-5, atol=1e-6 * max(1.0, np.abs(gs[k]).max()))
