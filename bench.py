@@ -95,9 +95,7 @@ def kernel_algorithmic(name, N, P, HW, cap=None, T=None):
     if name == "count":
         return 16.0 * N + 4.0 * NB * T, "byte", "hbm"      # order, xy, radii in; count matrix out
     if name == "scan":
-        return 8.0 * NB * T + 4.0 * T, "byte", "hbm"       # count matrix in + offsets out; tile totals
-    if name == "starts":
-        return 16.0 * T, "byte", "hbm"                      # totals in; starts + ranges out
+        return 8.0 * NB * T + 24.0 * T, "byte", "hbm"      # count matrix in + offsets out; totals, starts, ranges
     if name == "place":
         return 16.0 * N + 4.0 * NB * T + 4.0 * T + 4.0 * P, "byte", "hbm"  # + pair ids out
     # sort binning (DGS_BINNING=sort): loops cover the launched capacity
@@ -115,7 +113,7 @@ def kernel_algorithmic(name, N, P, HW, cap=None, T=None):
 
 
 KERNEL_CLASSES = ["mlp_fwd", "mlp_bwd", "mlp_dw", "mlp_dw_reduce", "preprocess_fwd", "depth_sort", "count", "scan",
-                  "starts", "place", "duplicate", "sort", "ranges",
+                  "place", "duplicate", "sort", "ranges",
                   "blend_fwd", "blend_bwd", "preprocess_bwd", "ssim_fwd", "ssim_bwd"]
 
 

@@ -180,8 +180,8 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t *__rest
 // tile rectangle of its 3-sigma radius, so the position of pair (j, t) in the stable tile sort is
 //   tile_start[t] + #{j' < j : t in rect(j')}
 // counted hierarchically over blocks of 256 depth-ordered Gaussians: k_rect_count (per block and
-// tile), k_rect_colscan (exclusive down each tile's column of blocks, tile totals, pair count),
-// k_rect_starts (tile starts = scan of the totals; the ranges), k_rect_place (per wave and tile in
+// tile), k_rect_colscan (exclusive down each tile's column of blocks, tile totals, pair count; its
+// last workgroup scans the totals into the tile starts and ranges), k_rect_place (per wave and tile in
 // LDS, then the lanes below in the wave). Same order as the sort, bit for bit; no keys.
 // ------------------------------------------------------------------------------------------------
 constexpr int RECT_MAX_TILES = 12288;     // LDS of the count/place kernels: 4 B per tile (<= 64 KiB)
@@ -198,10 +198,10 @@ __device__ inline bool gauss_rect(uint32_t g, const float2 *xy, const int *radii
 __global__ __launch_bounds__(256) void k_rect_count(int P, const uint32_t *__restrict__ order, const float2 *__restrict__ xy,
                                                     const int *__restrict__ radii, int gx, int gy,
                                                     uint32_t *__restrict__ cnt, uint32_t *__restrict__ total) {
-    extern __shared__ uint32_t h[];  // [T]
+    extern __shared__ uint32_t h[];  // [T]  (total[0] = pair count, total[1] = column-scan ticket)
     const int T = gx * gy;
     for (int t = threadIdx.x; t < T; t += 256) h[t] = 0;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *total = 0;  // k_rect_colscan adds into it
+    if (blockIdx.x == 0 && threadIdx.x < 2) total[threadIdx.x] = 0;  // k_rect_colscan adds into them
     __syncthreads();
     const int j = blockIdx.x * 256 + threadIdx.x;
     int4 rc;
@@ -213,11 +213,56 @@ __global__ __launch_bounds__(256) void k_rect_count(int P, const uint32_t *__res
     for (int t = threadIdx.x; t < T; t += 256) row[t] = h[t];
 }
 
+// tile starts = exclusive scan of the tile totals, and the (unclipped) ranges; one workgroup of
+// 1024 threads (the column scan's last workgroup). The totals come as agent-scope atomic words
+// tagged with the launch generation (written by the other workgroups, no fences): spin on the tag.
+__device__ inline uint32_t tagged_total(const unsigned long long *tot, int t, uint32_t gen) {
+    unsigned long long v;
+    do {
+        v = __hip_atomic_load(tot + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } while ((uint32_t)(v >> 32) != gen);
+    return (uint32_t)v;
+}
+
+__device__ void rect_starts(int T, const unsigned long long *__restrict__ tot, uint32_t gen, uint32_t *__restrict__ tile_start,
+                            uint2 *__restrict__ ranges, uint32_t *wsum) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    constexpr int MAXPER = 12;  // RECT_MAX_TILES / 1024
+    const int per = div_up(T, 1024);
+    const int t0 = tid * per;
+    uint32_t c[MAXPER], local = 0;
+#pragma unroll
+    for (int k = 0; k < MAXPER; k++) {
+        c[k] = (k < per && t0 + k < T) ? tagged_total(tot, t0 + k, gen) : 0u;
+        local += c[k];
+    }
+    uint32_t x = local;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    uint32_t run = x - local;
+    for (int k = 0; k < w; k++) run += wsum[k];
+#pragma unroll
+    for (int k = 0; k < MAXPER; k++) {
+        const int t = t0 + k;
+        if (k < per && t < T) {
+            tile_start[t] = run;
+            ranges[t] = make_uint2(run, run + c[k]);
+            run += c[k];
+        }
+    }
+}
+
 // the column of block counts of 64 tiles per workgroup -> exclusive offsets (in place), the tile
-// totals and the pair count: 16 waves take 32 rows each per 512-row chunk (loads all in flight),
+// totals, the pair count, then the tile starts and ranges (last workgroup): 16 waves take 32 rows each per 512-row chunk (loads all in flight),
 // cross-wave prefix in LDS, carry between chunks
-__global__ __launch_bounds__(1024) void k_rect_colscan(int nb, int T, uint32_t *__restrict__ cnt, uint32_t *__restrict__ tot,
-                                                       uint32_t *__restrict__ total) {
+__global__ __launch_bounds__(1024) void k_rect_colscan(int nb, int T, uint32_t *__restrict__ cnt, unsigned long long *__restrict__ tot, uint32_t gen,
+                                                       uint32_t *__restrict__ total, uint32_t *__restrict__ ticket,
+                                                       uint32_t *__restrict__ tile_start, uint2 *__restrict__ ranges) {
     __shared__ uint32_t part[16][64];
     __shared__ uint32_t carry[64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -247,42 +292,19 @@ __global__ __launch_bounds__(1024) void k_rect_colscan(int nb, int T, uint32_t *
     }
     if (w == 0) {
         const uint32_t c = carry[lane];
-        if (ok) tot[t] = c;
+        if (ok) __hip_atomic_store(tot + t, ((unsigned long long)gen << 32) | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         uint32_t s = c;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) s += (uint32_t)__shfl_xor((int)s, o);
         if (lane == 0) atomicAdd(total, s);
     }
-}
-
-// tile starts = exclusive scan of the tile totals; ranges clipped to the launched pair capacity
-__global__ __launch_bounds__(1024) void k_rect_starts(int T, const uint32_t *__restrict__ tot, uint32_t cap,
-                                                      uint32_t *__restrict__ tile_start, uint2 *__restrict__ ranges) {
+    // the last workgroup to take a ticket scans the tile totals
     __shared__ uint32_t wsum[16];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int per = div_up(T, 1024);
-    const int t0 = tid * per;
-    uint32_t local = 0;
-    for (int k = 0; k < per; k++)
-        if (t0 + k < T) local += tot[t0 + k];
-    uint32_t x = local;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) wsum[w] = x;
+    __shared__ bool last;
+    if (threadIdx.x == 0) last = atomicAdd(ticket, 1u) == gridDim.x - 1;
     __syncthreads();
-    uint32_t run = x - local;
-    for (int k = 0; k < w; k++) run += wsum[k];
-    for (int k = 0; k < per; k++) {
-        const int t = t0 + k;
-        if (t >= T) break;
-        const uint32_t c = tot[t];
-        tile_start[t] = run;
-        ranges[t] = make_uint2(min(run, cap), min(run + c, cap));
-        run += c;
-    }
+    if (!last) return;
+    rect_starts(T, tot, gen, tile_start, ranges, wsum);
 }
 
 __host__ __device__ inline size_t rect_place_lds(int gx, int gy) {
@@ -353,7 +375,7 @@ __global__ __launch_bounds__(256) void k_ranges(const uint32_t *__restrict__ cou
 }
 
 __global__ __launch_bounds__(256) void k_blend_fwd(const uint2 *__restrict__ ranges, const uint32_t *__restrict__ vals,
-                                                   int W, int H, int gx, const float2 *__restrict__ xy,
+                                                   uint32_t cap, int W, int H, int gx, const float2 *__restrict__ xy,
                                                    const float4 *__restrict__ conic_o, const float4 *__restrict__ rgbd,
                                                    const float *bg, float *__restrict__ final_T,
                                                    uint32_t *__restrict__ n_contrib, float *__restrict__ out_color,
@@ -368,6 +390,8 @@ __global__ __launch_bounds__(256) void k_blend_fwd(const uint2 *__restrict__ ran
     const bool inside = px < W && py < H;
     const float pfx = (float)px, pfy = (float)py;
     uint2 range = ranges[tile];
+    range.x = min(range.x, cap);  // a speculative launch under capacity (redone at the exact size)
+    range.y = min(range.y, cap);
     const int todo_total = (int)(range.y - range.x);
     const int rounds = div_up(todo_total, TILE_PIX);
     bool done = !inside;
@@ -840,7 +864,8 @@ struct dgs_raster_ctx {
     uint8_t *clamped = nullptr;
     uint32_t *vals = nullptr;
     bool rect_mode = false;  // rect binning (k_rect_*) instead of duplicate + tile sort
-    uint32_t *rect_cnt = nullptr, *rect_tot = nullptr, *rect_start = nullptr, *rect_total = nullptr;
+    uint32_t *rect_cnt = nullptr, *rect_start = nullptr, *rect_total = nullptr;
+    unsigned long long *rect_tot = nullptr;  // tile totals tagged with a launch generation (k_rect_colscan)
     uint2 *ranges = nullptr;
     float *final_T = nullptr;
     uint32_t *n_contrib = nullptr;
@@ -880,6 +905,15 @@ int binning_mode() {
         g_binning.store(m);
     }
     return m;
+}
+
+// process-wide launch generations of k_rect_colscan: a tag never repeats across contexts whose
+// buffers may be recycled
+uint32_t next_rect_gen() {
+    static std::atomic<uint32_t> g{0};
+    uint32_t v = ++g;
+    if (v == 0) v = ++g;
+    return v;
 }
 
 bool rect_binning(int gx, int gy, int P) {
@@ -1048,12 +1082,6 @@ static int bin_and_blend(dgs_raster_ctx *c, int cap, int P, int device, hipStrea
         if (int rc = c->bin.ensure(4ull * std::max(cap, 1) + 256)) return rc;
         c->vals = (uint32_t *)c->bin.p;
         const int nb = div_up(P, 256);
-        {
-            ScopedTimer tm("starts", stream);
-            hipLaunchKernelGGL(k_rect_starts, dim3(1), dim3(1024), 0, stream, T, c->rect_tot, (uint32_t)cap, c->rect_start,
-                               c->ranges);
-        }
-        DGS_LAUNCH_CHECK("k_rect_starts", dbg, stream);
         if (cap > 0) {
             ScopedTimer tm("place", stream);
             hipLaunchKernelGGL(k_rect_place, dim3(nb), dim3(256), rect_place_lds(c->gx, c->gy), stream, P, c->order, c->xy, c->radii,
@@ -1071,7 +1099,7 @@ static int bin_and_blend(dgs_raster_ctx *c, int cap, int P, int device, hipStrea
     }
     {
         ScopedTimer tm("blend_fwd", stream);
-        hipLaunchKernelGGL(k_blend_fwd, dim3(T), dim3(TILE_PIX), 0, stream, c->ranges, c->vals, c->W, c->H, c->gx, c->xy,
+        hipLaunchKernelGGL(k_blend_fwd, dim3(T), dim3(TILE_PIX), 0, stream, c->ranges, c->vals, (uint32_t)cap, c->W, c->H, c->gx, c->xy,
                            c->conic_o, c->rgbd, c->s.bg, c->final_T, c->n_contrib, out_color, out_depth);
     }
     DGS_LAUNCH_CHECK("k_blend_fwd", dbg, stream);
@@ -1156,11 +1184,11 @@ extern "C" int dgs_raster_forward(const dgs_raster_settings *s, int P, int M, co
     c->rect_mode = P > 0 && rect_binning(c->gx, c->gy, P);
     if (c->rect_mode) {  // count matrix [blocks][tiles], tile totals, tile starts, pair count
         const size_t nb = div_up(P, 256);
-        size_t o_cnt = 0, o_tot = align_up(4ull * nb * T), o_st = align_up(o_tot + 4ull * T), o_n = align_up(o_st + 4ull * T);
+        size_t o_cnt = 0, o_tot = align_up(4ull * nb * T), o_st = align_up(o_tot + 8ull * T), o_n = align_up(o_st + 4ull * T);
         if (int rc = c->rect.ensure(o_n + 256)) return rc;
         char *r = (char *)c->rect.p;
         c->rect_cnt = (uint32_t *)(r + o_cnt);
-        c->rect_tot = (uint32_t *)(r + o_tot);
+        c->rect_tot = (unsigned long long *)(r + o_tot);
         c->rect_start = (uint32_t *)(r + o_st);
         c->rect_total = (uint32_t *)(r + o_n);
     }
@@ -1213,7 +1241,7 @@ extern "C" int dgs_raster_forward(const dgs_raster_settings *s, int P, int M, co
             {
                 ScopedTimer tm("scan", stream);
                 hipLaunchKernelGGL(k_rect_colscan, dim3(div_up(T, 64)), dim3(1024), 0, stream, nb, T, c->rect_cnt, c->rect_tot,
-                                   c->rect_total);
+                                   next_rect_gen(), c->rect_total, c->rect_total + 1, c->rect_start, c->ranges);
             }
             DGS_LAUNCH_CHECK("k_rect_colscan", dbg, stream);
             DGS_HIP_CHECK(hipMemcpyAsync(c->h_total, c->rect_total, 4, hipMemcpyDeviceToHost, stream));
