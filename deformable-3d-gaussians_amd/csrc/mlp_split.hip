@@ -160,7 +160,15 @@ __device__ unsigned long long *dgs_mlps_prof;
     do {                                                                                               \
         if (threadIdx.x == 0) dgs_mlps_prof[blockIdx.x * 64 + (k)] = __builtin_amdgcn_s_memtime();     \
     } while (0)
+#define DGS_WSTAMP(k, L)                                                                               \
+    do {                                                                                               \
+        if (L == 3 && (threadIdx.x & 63) == 0)                                                         \
+            dgs_mlps_prof[blockIdx.x * 64 + (k) + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memtime();  \
+    } while (0)
 #else
+#define DGS_WSTAMP(k, L) \
+    do {                 \
+    } while (0)
 #define DGS_STAMP(k) \
     do {             \
     } while (0)
@@ -170,15 +178,59 @@ struct NoPre {
     __device__ void operator()() const {}
 };
 
+// LDS hand-off between the waves of a workgroup without a workgroup barrier: monotonically growing
+// per-k-step counters, a relaxed LDS load spun on (wave-uniform), a relaxed LDS add from one lane.
+// A wave executes its LDS operations in issue order, so data written before a signal is visible to
+// a wave that has seen the signal; the empty asm keeps the compiler from moving LDS accesses across.
+// The spin is bounded (a wrong count gives wrong results, never a hung GPU).
+__device__ __forceinline__ uint32_t lds_peek(const uint32_t *f) {
+    return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_wait_ge(const uint32_t *f, uint32_t target, uint32_t seen) {
+    for (int guard = 0; __builtin_amdgcn_readfirstlane(seen) < target && guard < (1 << 20); guard++) {
+        __builtin_amdgcn_s_sleep(1);
+        seen = lds_peek(f);
+    }
+    asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void lds_signal(uint32_t *f, int lane) {
+    asm volatile("" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_add(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+struct NoGate {
+    __device__ uint32_t peek(int) const { return 0; }
+    __device__ void need(int, uint32_t) const {}
+    __device__ void done(int) const {}
+};
+
+// Trunk gate: the H k-steps (GEMM k-steps k0..) may be read once both writer waves of the previous
+// layer have signalled wr[j] (wr[j] >= wt), and each wave signals rd[j] once its reads of H k-step
+// j are consumed (the next layer's writers wait for all 16)
+struct HGate {
+    uint32_t *wr, *rd;
+    int k0;
+    uint32_t wt;
+    bool sig;
+    int lane;
+    __device__ uint32_t peek(int k) const { return k < k0 ? 0xffffffffu : lds_peek(wr + (k - k0)); }
+    __device__ void need(int k, uint32_t seen) const {
+        if (k >= k0) lds_wait_ge(wr + (k - k0), wt, seen);
+    }
+    __device__ void done(int k) const {
+        if (sig && k >= k0) lds_signal(rd + (k - k0), lane);
+    }
+};
+
 // acc[q] += A . X for the column tiles q0 .. q0 + NQ_ - 1 over NK k-steps of this wave's A image
 // (Aw: unit pointer of its n-tile at k-step 0) and of the LDS image from group g0 (k-step c =
 // groups g0 + 4c + kq). Fully unrolled; per k-step: each column tile's six MFMAs followed by its B
 // fragment for the next k-step into the same registers, then the A fragment RING k-steps ahead
 // (register ring: the A stream comes from L2). sched_barrier keeps that order per k-step; the other
 // three waves of the SIMD cover the B reload latency. pre() runs after the A prologue.
-template <int NK, int NQ_, class Pre = NoPre>
+template <int NK, int NQ_, class Pre = NoPre, class Gate = NoGate>
 __device__ inline void gemm(const bf16x8 *__restrict__ Aw, const bf16x8 *lds, int g0, int q0, int lane,
-                            f32x4 (&acc)[NQ_], Pre pre = Pre()) {
+                            f32x4 (&acc)[NQ_], Pre pre = Pre(), Gate gate = Gate()) {
     static_assert(NK >= 1, "empty GEMM");
     const int kq = lane >> 4, col = lane & 15;
     const bf16x8 *Ap = Aw + lane;
@@ -195,6 +247,7 @@ __device__ inline void gemm(const bf16x8 *__restrict__ Aw, const bf16x8 *lds, in
     for (int k = 0; k < RING; k++)
         if (k < NK) ring[k] = load_a(Ap + k * AK);
     pre();
+    gate.need(0, gate.peek(0));
     AFrag b = load_b(Bp, 0);
     f32x4 lo[NQ_];
 #pragma unroll
@@ -202,18 +255,24 @@ __device__ inline void gemm(const bf16x8 *__restrict__ Aw, const bf16x8 *lds, in
 #pragma unroll
     for (int k = 0; k < NK; k++) {
         __builtin_amdgcn_sched_barrier(0);
+        if (k > 0) gate.done(k - 1);  // k-step k-1's B fragments were consumed by its MFMAs
+        const uint32_t seen = k + 1 < NK ? gate.peek(k + 1) : 0u;
 #pragma unroll
         for (int q = 0; q < NQ_; q++) {
             // the next tile's B fragment (or the next k-step's first) is in flight during this tile's MFMAs
             AFrag nb;
             if (q + 1 < NQ_) nb = load_b(Bp + k * BK, q + 1);
-            else if (k + 1 < NK) nb = load_b(Bp + (k + 1) * BK, 0);
+            else if (k + 1 < NK) {
+                gate.need(k + 1, seen);
+                nb = load_b(Bp + (k + 1) * BK, 0);
+            }
             mma6(ring[k % RING], b, acc[q], lo[q]);
             if (q + 1 < NQ_ || k + 1 < NK) b = nb;
         }
         if (k + RING < NK) ring[k % RING] = load_a(Ap + (k + RING) * AK);
         __builtin_amdgcn_sched_barrier(0);
     }
+    gate.done(NK - 1);
 #pragma unroll
     for (int q = 0; q < NQ_; q++) acc[q] += lo[q];
 }
@@ -359,9 +418,18 @@ __global__ __launch_bounds__(256) void k_timenet(FwdArgs a) {
     }
 }
 
+// this lane's bias rows of the layer, loaded ahead of the GEMM
+struct BiasPre {
+    float4 *b;
+    const float *bias;
+    int r, lane;
+    __device__ void operator()() const { *b = load_bias4(bias, r, lane); }
+};
+
 template <bool SAVE>
 __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
     __shared__ bf16x8 lds[G_FWD * UG];
+    __shared__ uint32_t hwr[8], hrd[8];  // trunk hand-off counters (HGate)
     float *lf = reinterpret_cast<float *>(lds);
     float *stage = lf + G_H * UG * 4;  // fp32 [112][BM] feature staging (H region, before the trunk)
     const int tid = threadIdx.x, lane = tid & 63;
@@ -370,6 +438,11 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
     const int p0 = blockIdx.x * BM;
 #ifdef DGS_DIAG_PRIO  // experiment: static priority for the second-dispatched half (MI355X_MICROARCH.md)
     if (r >= 8) __builtin_amdgcn_s_setprio(1);
+#endif
+#ifdef DGS_DIAG_PRIO2  // experiment: graded priority by dispatch order within a SIMD
+    if (r >= 12) __builtin_amdgcn_s_setprio(3);
+    else if (r >= 8) __builtin_amdgcn_s_setprio(2);
+    else if (r >= 4) __builtin_amdgcn_s_setprio(1);
 #endif
     const Flags F = make_flags(a.flags);
     const size_t Ns = a.Ns;
@@ -387,6 +460,10 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
         const int p = p0 + lane;
         const float tv = p < a.N ? a.t[p] : t0;
         uniform_t = __ballot(tv != t0) == 0;
+    }
+    if (tid < 8) {
+        hwr[tid] = 0;
+        hrd[tid] = 0;
     }
     // ---- positional encodings (utils/time_utils.py:42-54) into fp32 staging: feature 3 band + d,
     // band 0 = x, band 1 + 2i = sin(2^i x), band 2 + 2i = cos(2^i x) ----
@@ -491,35 +568,47 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
         lds_barrier();
     }
     // ---- trunk: 8 x (Linear + ReLU), skip cat after layer 4 (time_utils.py:107-112) ----
+    // No workgroup barriers: the four waves of a SIMD finish a GEMM thousands of cycles apart (the
+    // oldest issues first), so each wave runs its epilogue as soon as every wave has read the H
+    // k-step it overwrites (hrd), and the next layer reads an H k-step once its two writer waves
+    // have stored it (hwr): early waves' epilogues overlap late waves' MFMAs.
 #pragma unroll 1
     for (int L = 0; L < 8; L++) {
         const int g0 = (L == 0 || L == 5) ? G_XE : G_H;
         const int nk = layer_kpad(L) / 32;
         zero_tiles(c);
         const bf16x8 *Aw = a.img + (size_t)(a.fL[L] + r * nk) * KSLOT;
-        if (L == 0) gemm<3, NQ>(Aw, lds, g0, 0, lane, c);
-        else if (L == 5) gemm<11, NQ>(Aw, lds, g0, 0, lane, c);
-        else gemm<8, NQ>(Aw, lds, g0, 0, lane, c);
+        float4 bv;  // loaded behind the A prologue: its latency is covered by the GEMM
+        const BiasPre bp{&bv, a.fp + a.bL[L], r, lane};
+        const HGate hg{hwr, hrd, L == 5 ? 3 : 0, 2u * L, true, lane};
+        if (L == 0) gemm<3, NQ>(Aw, lds, g0, 0, lane, c, bp);  // XE | TE only
+        else if (L == 5) gemm<11, NQ>(Aw, lds, g0, 0, lane, c, bp, hg);
+        else gemm<8, NQ>(Aw, lds, g0, 0, lane, c, bp, hg);
         DGS_STAMP(4 + 2 * L);
-        const float4 bv = load_bias4(a.fp + a.bL[L], r, lane);  // in flight across the barrier
-        lds_barrier();  // all waves finished reading H before it is overwritten
+        DGS_WSTAMP(22, L);  // per wave: GEMM end (layer 3)
 #ifndef DGS_DIAG_NO_EPI  // timing experiment only (wrong results): no bias/relu/mask/split/store epilogue
         bias_relu(c, bv, true);
         if (SAVE) {
             store_mask(relu_bits(c), 16 * L + r);
             tile16(a.saved, Ns, s_h(L) + 16 * r, p0, lane).store(c);
         }
+        if (L == 3 && r == 0) DGS_STAMP(54);
+        // this wave's rows are H k-step r / 2: every wave must have read it in this layer
+        if (L > 0) lds_wait_ge(hrd + (r >> 1), 16u * L, lds_peek(hrd + (r >> 1)));
+        if (L == 3 && r == 0) DGS_STAMP(56);
 #pragma unroll
         for (int q = 0; q < NQ; q++) acc_to_lds(c[q], lds, G_H, r, q, lane);
 #endif
-        lds_barrier();
+        lds_signal(hwr + (r >> 1), lane);
+        if (L == 3 && r == 0) DGS_STAMP(55);
         DGS_STAMP(5 + 2 * L);
     }
+    DGS_STAMP(20);
     // ---- heads (no activation): [warp | branch_w, branch_v], rotation, scaling: 16 rows (nout <= 13),
-    // one column tile per wave on waves 0-3 ----
+    // one column tile per wave on waves 0-3, once all 8 layers' writers have signalled ----
     if (r < NQ) {
         f32x4 c1[1] = {zero4()};
-        gemm<8, 1>(a.img + (size_t)a.fHd * KSLOT, lds, G_H, r, lane, c1);
+        gemm<8, 1>(a.img + (size_t)a.fHd * KSLOT, lds, G_H, r, lane, c1, NoPre(), HGate{hwr, hrd, 0, 16u, false, lane});
         const float4 b = load_bias4(a.fp + a.bHd, 0, lane);
         c1[0] += f32x4{b.x, b.y, b.z, b.w};
         const int p = p0 + 16 * r + col;

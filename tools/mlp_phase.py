@@ -43,6 +43,13 @@ def main():
     for a, b in zip(order[:-1], order[1:]):
         d = p[:, b] - p[:, a]
         print(f"  {names[b]:10s} {d.mean():9.0f} cyc  ({100 * d.mean() / tot.mean():5.1f}%)")
+    # layer 3 detail: every wave's GEMM end, then wave 0 through the epilogue
+    L3 = p[:, 9]
+    wend = np.stack([p[:, 22 + w] - L3 for w in range(16)], 1)
+    print("L3 per-wave GEMM end (mean over blocks):", " ".join(f"{v:.0f}" for v in wend.mean(0)))
+    print(f"L3 slowest wave GEMM end {wend.max(1).mean():.0f}, fastest {wend.min(1).mean():.0f}")
+    for nm, a_, b_ in (("barrier1", 10, 56), ("bias/relu/mask/saved", 56, 54), ("split+LDS", 54, 55), ("barrier2", 55, 11)):
+        print(f"  L3 {nm:22s} {(p[:, b_] - p[:, a_]).mean():8.0f} cyc")
     clk = (p[:, 61] - p[:, 0]) / np.maximum(p[:, 60] - p[:, 60].min() + 1, 1)
     start = p[:, 0] - p[:, 0].min()
     end = p[:, 21] - p[:, 0].min()
