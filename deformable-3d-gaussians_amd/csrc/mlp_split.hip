@@ -652,6 +652,7 @@ struct MaskPre {
 template <bool TE_ROWS>
 __global__ __launch_bounds__(NTHR) void k_bwd(BwdArgs a) {
     __shared__ bf16x8 lds[G_BWD * UG];
+    __shared__ uint32_t hwr[8], hrd[8];  // dZ hand-off counters (HGate), as in k_fwd's trunk
     float *lf = reinterpret_cast<float *>(lds);
     float *stage = lf + G_BH * UG * 4;  // fp32 [32][BM] (H region, before the first dZ)
     const int tid = threadIdx.x, lane = tid & 63;
@@ -661,6 +662,10 @@ __global__ __launch_bounds__(NTHR) void k_bwd(BwdArgs a) {
     const size_t Ns = a.Ns;
     const unsigned short *mtiles = reinterpret_cast<const unsigned short *>(a.mask + (size_t)blockIdx.x * 2 * F.nmask);
     auto mask_tile = [&](int mr) { return mtiles + (size_t)mr * 64; };
+    if (tid < 8) {
+        hwr[tid] = 0;
+        hrd[tid] = 0;
+    }
     // dOut -> dz rows Z_G (heads' dW) and the split G image
     for (int e = tid; e < 32 * BM; e += NTHR) {
         const int c = e / BM, m = e % BM;
@@ -679,6 +684,10 @@ __global__ __launch_bounds__(NTHR) void k_bwd(BwdArgs a) {
     }
     lds_barrier();
     f32x4 c[NQ];
+    // The dZ chain runs without workgroup barriers (see k_fwd's trunk): step 0 (heads^T) and steps
+    // i = 1..7 (layer L = 8 - i) each write dZ into H; step i reads H once both writers of each
+    // k-step have signalled (hwr >= 2i) and overwrites its own k-step once all 16 waves have read
+    // it (hrd >= 16i).
     // heads^T: dH7 = W_h^T dOut (K = 32 from G) -> mask H7 -> dZ7
     {
         uint32_t mk;
@@ -688,32 +697,35 @@ __global__ __launch_bounds__(NTHR) void k_bwd(BwdArgs a) {
         tile16(a.dz, Ns, Z_L0 + 7 * 256 + 16 * r, p0, lane).store(c);
 #pragma unroll
         for (int q = 0; q < NQ; q++) acc_to_lds(c[q], lds, G_BH, r, q, lane);
-        lds_barrier();
+        lds_signal(hwr + (r >> 1), lane);
     }
     f32x4 te5[1] = {zero4()};  // t_emb tile of layer 5's dX (waves 0-7, TE_ROWS)
 #pragma unroll 1
     for (int L = 7; L >= 1; L--) {
+        const uint32_t step = 8 - L;
         // dX_L = W_L^T dZ_L; the H-part rows of the padded L5 input are n-tiles F_H / 16 + r
         if (TE_ROWS && L == 5 && r < 8)  // t_emb rows (padded 64..95 = n-tiles 4, 5) x column tile r & 3
-            gemm<8, 1>(a.img + (size_t)(a.tL[5] + (F_TE / 16 + (r >> 2)) * 8) * KSLOT, lds, G_BH, r & 3, lane, te5);
+            gemm<8, 1>(a.img + (size_t)(a.tL[5] + (F_TE / 16 + (r >> 2)) * 8) * KSLOT, lds, G_BH, r & 3, lane, te5,
+                       NoPre(), HGate{hwr, hrd, 0, 2u * step, false, lane});
         const int tile0 = (L == 5) ? F_H / 16 : 0;
         uint32_t mk;
         zero_tiles(c);
         gemm<8, NQ>(a.img + (size_t)(a.tL[L] + (tile0 + r) * 8) * KSLOT, lds, G_BH, 0, lane, c,
-                    MaskPre{&mk, mask_tile(16 * (L - 1) + r), lane});
-        lds_barrier();
+                    MaskPre{&mk, mask_tile(16 * (L - 1) + r), lane}, HGate{hwr, hrd, 0, 2u * step, true, lane});
         mask_apply(c, mk);
         tile16(a.dz, Ns, Z_L0 + (L - 1) * 256 + 16 * r, p0, lane).store(c);
+        lds_wait_ge(hrd + (r >> 1), 16u * step, lds_peek(hrd + (r >> 1)));
 #pragma unroll
         for (int q = 0; q < NQ; q++) acc_to_lds(c[q], lds, G_BH, r, q, lane);
-        lds_barrier();
+        lds_signal(hwr + (r >> 1), lane);
     }
     if (!TE_ROWS) return;
     // layer 0's t_emb rows added to layer 5's: dTE tile (n-tile r >> 2, column tile r & 3) -> dz rows
     // Z_TE (timenet.2's dW) and the split G image (dOut's, no longer read)
     if (r < 8) {
         const int nt = r >> 2, q = r & 3;
-        gemm<8, 1>(a.img + (size_t)(a.tL[0] + (F_TE / 16 + nt) * 8) * KSLOT, lds, G_BH, q, lane, te5);
+        gemm<8, 1>(a.img + (size_t)(a.tL[0] + (F_TE / 16 + nt) * 8) * KSLOT, lds, G_BH, q, lane, te5, NoPre(),
+                   HGate{hwr, hrd, 0, 16u, false, lane});
         tile16(a.dz, Ns, Z_TE + 16 * nt, p0, lane).store(te5, q);
         acc_to_lds(te5[0], lds, G_BG, nt, q, lane);
     }
