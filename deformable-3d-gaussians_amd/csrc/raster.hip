@@ -545,7 +545,11 @@ __global__ __launch_bounds__(256) void k_blend_bwd(const uint2 *__restrict__ ran
             float v_r = 0.f, v_g = 0.f, v_b = 0.f, v_d = 0.f;
             if (act) {
                 float4 cd = s_cd[j];
-                const float inv1ma = 1.f / (1.f - alpha);  // one IEEE division for both uses
+                // 1 / (1 - alpha): hardware reciprocal + one Newton step (<= 1 ulp, vs the ~10-op
+                // IEEE division; the gradients' tolerance is 1e-3 relative)
+                const float om = 1.f - alpha;
+                float inv1ma = __builtin_amdgcn_rcpf(om);
+                inv1ma = fmaf(inv1ma, fmaf(-om, inv1ma, 1.f), inv1ma);
                 T = T * inv1ma;
                 float w = alpha * T;
                 acc0 = last_alpha * lc0 + (1.f - last_alpha) * acc0;
@@ -574,6 +578,10 @@ __global__ __launch_bounds__(256) void k_blend_bwd(const uint2 *__restrict__ ran
             }
             // pairs (a, b) fold to rows [a_lo, b_lo, a_hi, b_hi] of w: row r of w_k holds field
             // 4k + {0, 2, 1, 3}[r] (ACC_MX..ACC_DY order)
+#ifdef DGS_DIAG_NORED  // timing experiment only (wrong results): no reduction / atomics
+            if (lane == 0 && v_mx == 1234.5f) acc[0] = v_my + v_cx + v_cy + v_cz + v_op + v_r + v_g + v_b + v_d;
+            continue;
+#endif
             const float w0 = row_sum15(fold16(fold32(v_mx, v_my), fold32(v_cx, v_cy)));
             const float w1 = row_sum15(fold16(fold32(v_cz, v_op), fold32(v_r, v_g)));
             const float w2 = row_sum15(fold16(fold32(v_b, v_d), fold32(fabsf(v_mx), fabsf(v_my))));
