@@ -315,18 +315,20 @@ __device__ inline Tile16 tile16(const float *dst, size_t Ns, int row0, int p0, i
 
 // relu' bits of a wave's 16 x 64 tile: bit 4q + i of lane (kq, col) = [row 4kq + i of point 16q + col
 // > 0] (signed clamp of the float bits: -0.0 and +0.0 give 0); the backward's tiles have the same map
-__device__ inline uint32_t relu_bits(const f32x4 (&v)[NQ]) {
+template <int NQ_>
+__device__ inline uint32_t relu_bits(const f32x4 (&v)[NQ_]) {
     uint32_t w = 0;
 #pragma unroll
-    for (int q = 0; q < NQ; q++)
+    for (int q = 0; q < NQ_; q++)
 #pragma unroll
         for (int i = 0; i < 4; i++) w |= (uint32_t)min(max(__float_as_int(v[q][i]), 0), 1) << (4 * q + i);
     return w;
 }
 
-__device__ inline void mask_apply(f32x4 (&v)[NQ], uint32_t bits) {
+template <int NQ_>
+__device__ inline void mask_apply(f32x4 (&v)[NQ_], uint32_t bits) {
 #pragma unroll
-    for (int q = 0; q < NQ; q++)
+    for (int q = 0; q < NQ_; q++)
 #pragma unroll
         for (int i = 0; i < 4; i++)
             v[q][i] = __int_as_float(__float_as_int(v[q][i]) & __builtin_amdgcn_sbfe((int)bits, 4 * q + i, 1));
@@ -337,9 +339,10 @@ __device__ inline float4 load_bias4(const float *bias, int r, int lane) {
     return *reinterpret_cast<const float4 *>(bias + 16 * r + 4 * (lane >> 4));
 }
 
-__device__ inline void bias_relu(f32x4 (&v)[NQ], float4 b, bool relu) {
+template <int NQ_>
+__device__ inline void bias_relu(f32x4 (&v)[NQ_], float4 b, bool relu) {
 #pragma unroll
-    for (int q = 0; q < NQ; q++) {
+    for (int q = 0; q < NQ_; q++) {
         v[q][0] += b.x;
         v[q][1] += b.y;
         v[q][2] += b.z;
@@ -350,9 +353,10 @@ __device__ inline void bias_relu(f32x4 (&v)[NQ], float4 b, bool relu) {
     }
 }
 
-__device__ inline void zero_tiles(f32x4 (&v)[NQ]) {
+template <int NQ_>
+__device__ inline void zero_tiles(f32x4 (&v)[NQ_]) {
 #pragma unroll
-    for (int q = 0; q < NQ; q++) v[q] = zero4();
+    for (int q = 0; q < NQ_; q++) v[q] = zero4();
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -368,6 +372,7 @@ struct FwdArgs {
     float *saved;
     uint32_t *mask;     // relu' bits, [64-point block][row / 16][64 lanes] u16 (after the saved rows)
     float *tc;          // timenet of t[0] (k_timenet), or nullptr
+    int nfull;          // 64-point blocks; the rest of [0, Ns) runs in 16-point blocks (block_split)
     int fT1, fT2, fL[8], fHd;      // image k-slots
     int bT1, bT2, bL[8], bHd;      // fp32 offsets
     int wT1, wT2;                  // fp32 timenet weights [256][16], [32][256]
@@ -426,16 +431,18 @@ struct BiasPre {
     __device__ void operator()() const { *b = load_bias4(bias, r, lane); }
 };
 
-template <bool SAVE>
-__global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
-    __shared__ bf16x8 lds[G_FWD * UG];
-    __shared__ uint32_t hwr[8], hrd[8];  // trunk hand-off counters (HGate)
+// One block of NQB 16-point column tiles (NQB = 4: the 64-point blocks; NQB = 1: the 16-point tail
+// blocks that spread the last, sparse round of blocks over the idle CUs). p0: first point; slot: the
+// block's relu'-mask slot.
+template <bool SAVE, int NQB>
+__device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_t *hwr, uint32_t *hrd, int p0, int slot) {
+    constexpr int BMB = 16 * NQB;  // points of this block (the LDS images keep the BM-point stride)
     float *lf = reinterpret_cast<float *>(lds);
     float *stage = lf + G_H * UG * 4;  // fp32 [112][BM] feature staging (H region, before the trunk)
     const int tid = threadIdx.x, lane = tid & 63;
     const int r = __builtin_amdgcn_readfirstlane(tid >> 6);  // n-tile of this wave (provably uniform)
     const int kq = lane >> 4, col = lane & 15;
-    const int p0 = blockIdx.x * BM;
+    const int pend = min(a.N, p0 + BMB);  // real points of the block: [p0, pend)
 #ifdef DGS_DIAG_PRIO  // experiment: static priority for the second-dispatched half (MI355X_MICROARCH.md)
     if (r >= 8) __builtin_amdgcn_s_setprio(1);
 #endif
@@ -447,18 +454,18 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
     const Flags F = make_flags(a.flags);
     const size_t Ns = a.Ns;
     const __amdgpu_buffer_rsrc_t mrsrc = __builtin_amdgcn_make_buffer_rsrc(
-        a.mask + (SAVE ? (size_t)blockIdx.x * 2 * F.nmask : 0), 0, 0x7fffffff, 0x00020000);
+        a.mask + (SAVE ? (size_t)slot * 2 * F.nmask : 0), 0, 0x7fffffff, 0x00020000);
     auto store_mask = [&](uint32_t w, int mr) {  // mask tile mr (= row / 16)
         __builtin_amdgcn_raw_buffer_store_b16((unsigned short)w, mrsrc, lane * 2, mr * 128, 0);
     };
     DGS_STAMP(0);
-    // frame-uniform t: all 64 points of the block carry k_timenet's t0 (every wave checks the same
-    // 64 values, so the branch is block-uniform without a barrier)
+    // frame-uniform t: all points of the block carry k_timenet's t0 (every wave checks the same
+    // values, so the branch is block-uniform without a barrier)
     bool uniform_t = F.uniform_t && a.tc;  // the caller's guarantee (DGS_MLP_UNIFORM_T), else checked
     if (F.blender && a.tc && !uniform_t) {
         const float t0 = a.tc[TC_T];
         const int p = p0 + lane;
-        const float tv = p < a.N ? a.t[p] : t0;
+        const float tv = (lane < BMB && p < a.N) ? a.t[p] : t0;
         uniform_t = __ballot(tv != t0) == 0;
     }
     if (tid < 8) {
@@ -467,10 +474,10 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
     }
     // ---- positional encodings (utils/time_utils.py:42-54) into fp32 staging: feature 3 band + d,
     // band 0 = x, band 1 + 2i = sin(2^i x), band 2 + 2i = cos(2^i x) ----
-    for (int e = tid; e < BM * 3 * 11; e += NTHR) {
-        const int m = e % BM, rr = e / BM, d = rr % 3, i = rr / 3;  // i = 10: identity band
+    for (int e = tid; e < BMB * 3 * 11; e += NTHR) {
+        const int m = e % BMB, rr = e / BMB, d = rr % 3, i = rr / 3;  // i = 10: identity band
         const int p = p0 + m;
-        const bool ok = p < a.N;
+        const bool ok = p < pend;
         const float x = ok ? a.xyz[3 * p + d] : 0.f;
         if (i == 10) {
             stage[d * BM + m] = x;
@@ -481,20 +488,20 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
             stage[(3 * (2 + 2 * i) + d) * BM + m] = ok ? cv : 0.f;
         }
     }
-    if (tid < BM) stage[63 * BM + tid] = 0.f;  // padding feature
+    if (tid < BMB) stage[63 * BM + tid] = 0.f;  // padding feature
     if (uniform_t) {  // TE and TIN: k_timenet's values broadcast over the points
-        for (int e = tid; e < 48 * BM; e += NTHR) {
-            const int f = e / BM, m = e % BM;
+        for (int e = tid; e < 48 * BMB; e += NTHR) {
+            const int f = e / BMB, m = e % BMB;
             stage[(ST_TE + f) * BM + m] = f < 32 ? a.tc[TC_TE + f] : a.tc[TC_TIN + f - 32];
         }
     } else {  // per-point t encodings: TIN (blender, 16 rows) or the raw t PE as TE (32 rows)
         const int row0 = F.blender ? ST_TIN : ST_TE, nrow = F.blender ? 16 : 32;
-        for (int e = tid; e < nrow * BM; e += NTHR) {
-            const int f = e / BM, m = e % BM;
+        for (int e = tid; e < nrow * BMB; e += NTHR) {
+            const int f = e / BMB, m = e % BMB;
             const int p = p0 + m;
-            const float x = p < a.N ? a.t[p] : 0.f;
+            const float x = p < pend ? a.t[p] : 0.f;
             float v = 0.f;
-            if (p < a.N && f < F.tin) {
+            if (p < pend && f < F.tin) {
                 if (f == 0) {
                     v = x;
                 } else {
@@ -511,20 +518,20 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
     const bool te_ready = uniform_t || !F.blender;
     if (SAVE) {
         const int nrow = te_ready ? 96 : 64;  // XE | TE rows are adjacent in saved (S_TE = S_XE + 64)
-        for (int e = tid; e < nrow * BM; e += NTHR) {
-            const int f = e / BM, m = e % BM;
+        for (int e = tid; e < nrow * BMB; e += NTHR) {
+            const int f = e / BMB, m = e % BMB;
             a.saved[(size_t)(S_XE + f) * Ns + p0 + m] = stage[f * BM + m];
         }
         if (F.blender)
-            for (int e = tid; e < 16 * BM; e += NTHR) {
-                const int f = e / BM, m = e % BM;
+            for (int e = tid; e < 16 * BMB; e += NTHR) {
+                const int f = e / BMB, m = e % BMB;
                 a.saved[(size_t)(S_TIN + f) * Ns + p0 + m] = stage[(ST_TIN + f) * BM + m];
             }
     }
     {
         const int ngrp = F.blender ? 14 : 12;  // staging groups: XE 0-7 | TE 8-11 | TIN 12-13
-        for (int u = tid; u < ngrp * BM; u += NTHR) {
-            const int g = u / BM, m = u % BM;
+        for (int u = tid; u < ngrp * BMB; u += NTHR) {
+            const int g = u / BMB, m = u % BMB;
             if (g >= G_TE && g < G_H && !te_ready) continue;  // TE comes from the per-point timenet
             float v[8];
 #pragma unroll
@@ -536,28 +543,28 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
     }
     lds_barrier();
     DGS_STAMP(1);
-    f32x4 c[NQ];
+    f32x4 c[NQB];
     if (SAVE && uniform_t && !F.uniform_t) {  // TH tile from k_timenet: relu' bits + saved rows (per-point backward)
         const float4 th = load_bias4(a.tc + TC_TH, r, lane);
 #pragma unroll
-        for (int q = 0; q < NQ; q++) c[q] = f32x4{th.x, th.y, th.z, th.w};
+        for (int q = 0; q < NQB; q++) c[q] = f32x4{th.x, th.y, th.z, th.w};
         store_mask(relu_bits(c), MR_TH + r);
         tile16(a.saved, Ns, S_TH + 16 * r, p0, lane).store(c);
     }
     // ---- per-point timenet (blender, t not frame-uniform): Linear(13,256)+ReLU -> H; Linear(256,30) -> TE
     if (F.blender && !uniform_t) {
         zero_tiles(c);
-        gemm<1, NQ>(a.img + (size_t)(a.fT1 + r) * KSLOT, lds, G_TIN, 0, lane, c);
+        gemm<1, NQB>(a.img + (size_t)(a.fT1 + r) * KSLOT, lds, G_TIN, 0, lane, c);
         bias_relu(c, load_bias4(a.fp + a.bT1, r, lane), true);
         if (SAVE) {
             store_mask(relu_bits(c), MR_TH + r);
             tile16(a.saved, Ns, S_TH + 16 * r, p0, lane).store(c);
         }
 #pragma unroll
-        for (int q = 0; q < NQ; q++) acc_to_lds(c[q], lds, G_H, r, q, lane);
+        for (int q = 0; q < NQB; q++) acc_to_lds(c[q], lds, G_H, r, q, lane);
         lds_barrier();
-        if (r < 8) {  // TE tile (n-tile r >> 2 of 2, column tile r & 3), full K on one wave
-            const int nt = r >> 2, q = r & 3;
+        if (r < 2 * NQB) {  // TE tile (n-tile r / NQB of 2, column tile r % NQB), full K on one wave
+            const int nt = r / NQB, q = r % NQB;
             f32x4 c1[1] = {zero4()};
             gemm<8, 1>(a.img + (size_t)(a.fT2 + nt * 8) * KSLOT, lds, G_H, q, lane, c1);
             const float4 b = load_bias4(a.fp + a.bT2, nt, lane);
@@ -581,9 +588,9 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
         float4 bv;  // loaded behind the A prologue: its latency is covered by the GEMM
         const BiasPre bp{&bv, a.fp + a.bL[L], r, lane};
         const HGate hg{hwr, hrd, L == 5 ? 3 : 0, 2u * L, true, lane};
-        if (L == 0) gemm<3, NQ>(Aw, lds, g0, 0, lane, c, bp);  // XE | TE only
-        else if (L == 5) gemm<11, NQ>(Aw, lds, g0, 0, lane, c, bp, hg);
-        else gemm<8, NQ>(Aw, lds, g0, 0, lane, c, bp, hg);
+        if (L == 0) gemm<3, NQB>(Aw, lds, g0, 0, lane, c, bp);  // XE | TE only
+        else if (L == 5) gemm<11, NQB>(Aw, lds, g0, 0, lane, c, bp, hg);
+        else gemm<8, NQB>(Aw, lds, g0, 0, lane, c, bp, hg);
         DGS_STAMP(4 + 2 * L);
         DGS_WSTAMP(22, L);  // per wave: GEMM end (layer 3)
 #ifndef DGS_DIAG_NO_EPI  // timing experiment only (wrong results): no bias/relu/mask/split/store epilogue
@@ -597,7 +604,7 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
         if (L > 0) lds_wait_ge(hrd + (r >> 1), 16u * L, lds_peek(hrd + (r >> 1)));
         if (L == 3 && r == 0) DGS_STAMP(56);
 #pragma unroll
-        for (int q = 0; q < NQ; q++) acc_to_lds(c[q], lds, G_H, r, q, lane);
+        for (int q = 0; q < NQB; q++) acc_to_lds(c[q], lds, G_H, r, q, lane);
 #endif
         lds_signal(hwr + (r >> 1), lane);
         if (L == 3 && r == 0) DGS_STAMP(55);
@@ -606,7 +613,7 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
     DGS_STAMP(20);
     // ---- heads (no activation): [warp | branch_w, branch_v], rotation, scaling: 16 rows (nout <= 13),
     // one column tile per wave on waves 0-3, once all 8 layers' writers have signalled ----
-    if (r < NQ) {
+    if (r < NQB) {
         f32x4 c1[1] = {zero4()};
         gemm<8, 1>(a.img + (size_t)a.fHd * KSLOT, lds, G_H, r, lane, c1, NoPre(), HGate{hwr, hrd, 0, 16u, false, lane});
         const float4 b = load_bias4(a.fp + a.bHd, 0, lane);
@@ -614,7 +621,7 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
         const int p = p0 + 16 * r + col;
 #pragma unroll
         for (int i = 0; i < 4; i++)
-            if (p < a.N && 4 * kq + i < F.nout) a.out[(size_t)p * F.nout + 4 * kq + i] = c1[0][i];
+            if (p < pend && 4 * kq + i < F.nout) a.out[(size_t)p * F.nout + 4 * kq + i] = c1[0][i];
     }
     DGS_STAMP(21);
 #ifdef DGS_MLP_PROFILE
@@ -624,6 +631,16 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
     }
 #endif
 }
+
+template <bool SAVE>
+__global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
+    __shared__ bf16x8 lds[G_FWD * UG];
+    __shared__ uint32_t hwr[8], hrd[8];  // trunk hand-off counters (HGate)
+    const int b = blockIdx.x;
+    if (b < a.nfull) fwd_block<SAVE, NQ>(a, lds, hwr, hrd, b * BM, b);
+    else fwd_block<SAVE, 1>(a, lds, hwr, hrd, a.nfull * BM + (b - a.nfull) * 16, b);
+}
+
 
 // ------------------------------------------------------------------------------------------------
 // backward (dX chain): dZ_i for every layer -> scratch; deterministic
@@ -635,6 +652,7 @@ struct BwdArgs {
     const uint32_t *mask;
     const float *dout;
     float *dz;
+    int nfull;            // as FwdArgs::nfull
     int tHd, tL[8], tT2;  // image k-slots
     int flags;
 };
@@ -649,41 +667,39 @@ struct MaskPre {
 
 // TE_ROWS: per-point dL/dt_emb (blender, t not frame-uniform); the other instantiation carries no
 // t_emb registers or code (raw t PE has no parameters upstream; uniform t: k_tgrad)
-template <bool TE_ROWS>
-__global__ __launch_bounds__(NTHR) void k_bwd(BwdArgs a) {
-    __shared__ bf16x8 lds[G_BWD * UG];
-    __shared__ uint32_t hwr[8], hrd[8];  // dZ hand-off counters (HGate), as in k_fwd's trunk
+template <bool TE_ROWS, int NQB>
+__device__ __forceinline__ void bwd_block(const BwdArgs &a, bf16x8 *lds, uint32_t *hwr, uint32_t *hrd, int p0, int slot) {
+    constexpr int BMB = 16 * NQB;  // points of this block (fwd_block)
     float *lf = reinterpret_cast<float *>(lds);
     float *stage = lf + G_BH * UG * 4;  // fp32 [32][BM] (H region, before the first dZ)
     const int tid = threadIdx.x, lane = tid & 63;
     const int r = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int p0 = blockIdx.x * BM;
     const Flags F = make_flags(a.flags);
     const size_t Ns = a.Ns;
-    const unsigned short *mtiles = reinterpret_cast<const unsigned short *>(a.mask + (size_t)blockIdx.x * 2 * F.nmask);
+    const unsigned short *mtiles = reinterpret_cast<const unsigned short *>(a.mask + (size_t)slot * 2 * F.nmask);
     auto mask_tile = [&](int mr) { return mtiles + (size_t)mr * 64; };
     if (tid < 8) {
         hwr[tid] = 0;
         hrd[tid] = 0;
     }
     // dOut -> dz rows Z_G (heads' dW) and the split G image
-    for (int e = tid; e < 32 * BM; e += NTHR) {
-        const int c = e / BM, m = e % BM;
+    for (int e = tid; e < 32 * BMB; e += NTHR) {
+        const int c = e / BMB, m = e % BMB;
         const int p = p0 + m;
         const float v = (p < a.N && c < F.nout) ? a.dout[(size_t)p * F.nout + c] : 0.f;
         a.dz[(size_t)(Z_G + c) * Ns + p] = v;
         stage[c * BM + m] = v;
     }
     __syncthreads();
-    if (tid < 4 * BM) {
-        const int g = tid / BM, m = tid % BM;
+    if (tid < 4 * BMB) {
+        const int g = tid / BMB, m = tid % BMB;
         float v[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) v[j] = stage[(8 * g + j) * BM + m];
         put_unit8(lds, G_BG + g, m, v);
     }
     lds_barrier();
-    f32x4 c[NQ];
+    f32x4 c[NQB];
     // The dZ chain runs without workgroup barriers (see k_fwd's trunk): step 0 (heads^T) and steps
     // i = 1..7 (layer L = 8 - i) each write dZ into H; step i reads H once both writers of each
     // k-step have signalled (hwr >= 2i) and overwrites its own k-step once all 16 waves have read
@@ -692,11 +708,11 @@ __global__ __launch_bounds__(NTHR) void k_bwd(BwdArgs a) {
     {
         uint32_t mk;
         zero_tiles(c);
-        gemm<1, NQ>(a.img + (size_t)(a.tHd + r) * KSLOT, lds, G_BG, 0, lane, c, MaskPre{&mk, mask_tile(16 * 7 + r), lane});
+        gemm<1, NQB>(a.img + (size_t)(a.tHd + r) * KSLOT, lds, G_BG, 0, lane, c, MaskPre{&mk, mask_tile(16 * 7 + r), lane});
         mask_apply(c, mk);
         tile16(a.dz, Ns, Z_L0 + 7 * 256 + 16 * r, p0, lane).store(c);
 #pragma unroll
-        for (int q = 0; q < NQ; q++) acc_to_lds(c[q], lds, G_BH, r, q, lane);
+        for (int q = 0; q < NQB; q++) acc_to_lds(c[q], lds, G_BH, r, q, lane);
         lds_signal(hwr + (r >> 1), lane);
     }
     f32x4 te5[1] = {zero4()};  // t_emb tile of layer 5's dX (waves 0-7, TE_ROWS)
@@ -704,26 +720,26 @@ __global__ __launch_bounds__(NTHR) void k_bwd(BwdArgs a) {
     for (int L = 7; L >= 1; L--) {
         const uint32_t step = 8 - L;
         // dX_L = W_L^T dZ_L; the H-part rows of the padded L5 input are n-tiles F_H / 16 + r
-        if (TE_ROWS && L == 5 && r < 8)  // t_emb rows (padded 64..95 = n-tiles 4, 5) x column tile r & 3
-            gemm<8, 1>(a.img + (size_t)(a.tL[5] + (F_TE / 16 + (r >> 2)) * 8) * KSLOT, lds, G_BH, r & 3, lane, te5,
+        if (TE_ROWS && L == 5 && r < 2 * NQB)  // t_emb rows (padded 64..95 = n-tiles 4, 5) x column tile r % NQB
+            gemm<8, 1>(a.img + (size_t)(a.tL[5] + (F_TE / 16 + r / NQB) * 8) * KSLOT, lds, G_BH, r % NQB, lane, te5,
                        NoPre(), HGate{hwr, hrd, 0, 2u * step, false, lane});
         const int tile0 = (L == 5) ? F_H / 16 : 0;
         uint32_t mk;
         zero_tiles(c);
-        gemm<8, NQ>(a.img + (size_t)(a.tL[L] + (tile0 + r) * 8) * KSLOT, lds, G_BH, 0, lane, c,
+        gemm<8, NQB>(a.img + (size_t)(a.tL[L] + (tile0 + r) * 8) * KSLOT, lds, G_BH, 0, lane, c,
                     MaskPre{&mk, mask_tile(16 * (L - 1) + r), lane}, HGate{hwr, hrd, 0, 2u * step, true, lane});
         mask_apply(c, mk);
         tile16(a.dz, Ns, Z_L0 + (L - 1) * 256 + 16 * r, p0, lane).store(c);
         lds_wait_ge(hrd + (r >> 1), 16u * step, lds_peek(hrd + (r >> 1)));
 #pragma unroll
-        for (int q = 0; q < NQ; q++) acc_to_lds(c[q], lds, G_BH, r, q, lane);
+        for (int q = 0; q < NQB; q++) acc_to_lds(c[q], lds, G_BH, r, q, lane);
         lds_signal(hwr + (r >> 1), lane);
     }
     if (!TE_ROWS) return;
-    // layer 0's t_emb rows added to layer 5's: dTE tile (n-tile r >> 2, column tile r & 3) -> dz rows
+    // layer 0's t_emb rows added to layer 5's: dTE tile (n-tile r / NQB, column tile r % NQB) -> dz rows
     // Z_TE (timenet.2's dW) and the split G image (dOut's, no longer read)
-    if (r < 8) {
-        const int nt = r >> 2, q = r & 3;
+    if (r < 2 * NQB) {
+        const int nt = r / NQB, q = r % NQB;
         gemm<8, 1>(a.img + (size_t)(a.tL[0] + (F_TE / 16 + nt) * 8) * KSLOT, lds, G_BH, q, lane, te5, NoPre(),
                    HGate{hwr, hrd, 0, 16u, false, lane});
         tile16(a.dz, Ns, Z_TE + 16 * nt, p0, lane).store(te5, q);
@@ -734,10 +750,19 @@ __global__ __launch_bounds__(NTHR) void k_bwd(BwdArgs a) {
     {
         uint32_t mk;
         zero_tiles(c);
-        gemm<1, NQ>(a.img + (size_t)(a.tT2 + r) * KSLOT, lds, G_BG, 0, lane, c, MaskPre{&mk, mask_tile(MR_TH + r), lane});
+        gemm<1, NQB>(a.img + (size_t)(a.tT2 + r) * KSLOT, lds, G_BG, 0, lane, c, MaskPre{&mk, mask_tile(MR_TH + r), lane});
         mask_apply(c, mk);
         tile16(a.dz, Ns, Z_T1 + 16 * r, p0, lane).store(c);
     }
+}
+
+template <bool TE_ROWS>
+__global__ __launch_bounds__(NTHR) void k_bwd(BwdArgs a) {
+    __shared__ bf16x8 lds[G_BWD * UG];
+    __shared__ uint32_t hwr[8], hrd[8];  // dZ hand-off counters (HGate), as in k_fwd's trunk
+    const int b = blockIdx.x;
+    if (b < a.nfull) bwd_block<TE_ROWS, NQ>(a, lds, hwr, hrd, b * BM, b);
+    else bwd_block<TE_ROWS, 1>(a, lds, hwr, hrd, a.nfull * BM + (b - a.nfull) * 16, b);
 }
 
 // Timenet gradients for a frame-uniform t (DGS_MLP_UNIFORM_T). With one TIN / TH for every point,
@@ -1573,10 +1598,49 @@ static int dw_split(const Flags &F, size_t Ns, const float *dz, const float *sav
 
 static size_t padded_points(int N) { return (size_t)div_up(N, BM) * BM; }
 
+// Block decomposition of the fused forward / dX kernels (one 147 KB workgroup per CU): when the last
+// round of 64-point blocks would occupy at most a quarter of the CUs, those blocks run as four times
+// as many 16-point blocks instead (fwd_block / bwd_block NQB = 1), so the sparse last round ends in
+// roughly a third of a full block's time (the A stream, not the MFMAs, bounds a 16-point block).
+// DGS_MLP_NO_TAIL=1 keeps 64-point blocks throughout. Mask slots: one per block (<= nb + 3 min(nb, 128)).
+constexpr int TAIL_MAX_LAST = 128;
+struct Blocks {
+    int nfull, ntail;
+};
+static int cu_count() {
+    static std::mutex mu;
+    static std::map<int, int> cache;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(dev);
+    if (it != cache.end()) return it->second;
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    cache[dev] = v;
+    return v;
+}
+static Blocks block_split(int N) {
+    const int nb = div_up(N, BM);
+    static const bool off = [] {
+        const char *e = getenv("DGS_MLP_NO_TAIL");
+        return e && e[0] == '1';
+    }();
+    if (off || nb == 0) return {nb, 0};
+    const int ncu = cu_count();
+    const int rounds = div_up(nb, ncu), last = nb - ncu * (rounds - 1);
+    if (rounds < 2 || last > TAIL_MAX_LAST || 4 * last > ncu) return {nb, 0};
+    return {nb - last, 4 * last};
+}
+static size_t mask_words(const Flags &F, size_t Ns) {
+    const size_t nb = Ns / BM;
+    return (size_t)F.nmask * 2 * (nb + 3 * std::min<size_t>(nb, TAIL_MAX_LAST));
+}
+
 size_t saved_floats(int flags, int N) {
     const Flags F = make_flags(flags);
     const size_t Ns = padded_points(N);
-    return (size_t)F.nsaved * Ns + (size_t)F.nmask * (Ns / 32) + TC_FLOATS;
+    return (size_t)F.nsaved * Ns + mask_words(F, Ns) + TC_FLOATS;
 }
 
 // dW arithmetic (DGS_MLP_SPLIT_DW): 3 (default) = the split-bf16 k_dws (private / shared operands,
@@ -1641,16 +1705,19 @@ int forward(int flags, int N, const float *xyz, const float *t, const float *pac
     a.bT1 = P.bT1; a.bT2 = P.bT2; a.bHd = P.bHd; a.wT1 = P.wT1; a.wT2 = P.wT2;
     for (int i = 0; i < 8; i++) { a.fL[i] = P.fL[i]; a.bL[i] = P.bL[i]; }
     a.flags = flags;
+    const Blocks bs = block_split(N);
+    a.nfull = bs.nfull;
+    const int nblk = bs.nfull + bs.ntail;
     {
         ScopedTimer tm("mlp_fwd", stream);
         if (saved && P.F.blender) {
-            a.tc = saved + (size_t)P.F.nsaved * a.Ns + (size_t)P.F.nmask * (a.Ns / 32);
+            a.tc = saved + (size_t)P.F.nsaved * a.Ns + mask_words(P.F, a.Ns);
             hipLaunchKernelGGL(k_timenet, dim3(1), dim3(256), 0, stream, a);
         }
         if (saved)
-            hipLaunchKernelGGL(k_fwd<true>, dim3(div_up(N, BM)), dim3(NTHR), 0, stream, a);
+            hipLaunchKernelGGL(k_fwd<true>, dim3(nblk), dim3(NTHR), 0, stream, a);
         else
-            hipLaunchKernelGGL(k_fwd<false>, dim3(div_up(N, BM)), dim3(NTHR), 0, stream, a);
+            hipLaunchKernelGGL(k_fwd<false>, dim3(nblk), dim3(NTHR), 0, stream, a);
     }
     DGS_LAUNCH_CHECK("k_fwd", false, stream);
     return DGS_OK;
@@ -1670,12 +1737,15 @@ int backward(int flags, int N, const float *packed, const float *saved, const fl
     b.tHd = P.tHd; b.tT2 = P.tT2;
     for (int i = 0; i < 8; i++) b.tL[i] = P.tL[i];
     b.flags = flags;
+    const Blocks bs = block_split(N);
+    b.nfull = bs.nfull;
+    const int nblk = bs.nfull + bs.ntail;
     {
         ScopedTimer tm("mlp_bwd", stream);
         if (F.blender && !F.uniform_t)
-            hipLaunchKernelGGL(k_bwd<true>, dim3(div_up(N, BM)), dim3(NTHR), 0, stream, b);
+            hipLaunchKernelGGL(k_bwd<true>, dim3(nblk), dim3(NTHR), 0, stream, b);
         else
-            hipLaunchKernelGGL(k_bwd<false>, dim3(div_up(N, BM)), dim3(NTHR), 0, stream, b);
+            hipLaunchKernelGGL(k_bwd<false>, dim3(nblk), dim3(NTHR), 0, stream, b);
     }
     DGS_LAUNCH_CHECK("k_bwd", false, stream);
     int rc;
@@ -1691,7 +1761,7 @@ int backward(int flags, int N, const float *packed, const float *saved, const fl
     TGradArgs g{};
     g.fp = packed + P.img_floats();
     g.w0te = P.w0te; g.w5te = P.w5te; g.wT2 = P.wT2;
-    g.tc = saved + (size_t)F.nsaved * Ns + (size_t)F.nmask * (Ns / 32);
+    g.tc = saved + (size_t)F.nsaved * Ns + mask_words(F, Ns);
     g.gb0 = grads[P.pLb[0]]; g.gb5 = grads[P.pLb[5]];
     g.gT0w = grads[P.pT0w]; g.gT0b = grads[P.pT0b]; g.gT2w = grads[P.pT2w]; g.gT2b = grads[P.pT2b];
     g.tin = F.tin;

@@ -218,3 +218,24 @@ def test_uniform_t_flag(name, N):
         tol = 1e-4 * max(np.abs(ref[k]).max(), 1e-6) + 1e-6
         assert np.abs(got - ref[k]).max() <= tol, (k, np.abs(got - ref[k]).max(), tol)
         assert np.abs(got - res["full"][1][k].cpu().numpy()).max() <= 2 * tol, k
+
+
+def test_tail_blocks_bitwise_equal_64_point_blocks(tmp_path):
+    """The fused forward / dX kernels run the sparse last round of 64-point blocks as 16-point
+    blocks (mlp_split.hip block_split); every output and parameter gradient must equal the all-64-
+    point decomposition (DGS_MLP_NO_TAIL=1, read once per process) bit for bit."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = os.path.join(root, "tools", "tail_check.py")
+    outs = []
+    for env_val in ("0", "1"):
+        out = str(tmp_path / f"tail_{env_val}.npz")
+        env = dict(os.environ, DGS_MLP_NO_TAIL=env_val)
+        subprocess.run([sys.executable, script, out], check=True, env=env, timeout=300)
+        outs.append(np.load(out))
+    a, b = outs
+    assert set(a.files) == set(b.files) and len(a.files) > 0
+    for k in a.files:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
