@@ -49,9 +49,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--no-adam", action="store_true", help="time only the reference's span (fwd+bwd)")
-    ap.add_argument("--kernel-timing", choices=["major", "all", "none"], default="major",
-                    help="kernel classes timed with HIP events inside the timed region (each timed launch adds two "
-                         "event records to the stream): the MFMA and blend kernels (default), every class, or none")
+    ap.add_argument("--kernel-timing", choices=["roofline", "major", "all", "none"], default="roofline",
+                    help="kernel classes timed with HIP events inside the timed region. Each event record costs "
+                         "~6 us of GPU idle on the launch stream (profiles/r2c trace), so the default times only the "
+                         "roofline kernel (mlp_dw: the longest launch of the step, 2 records per step); 'major' adds "
+                         "the other MFMA and blend classes, 'all' every class, 'none' nothing")
     ap.add_argument("--raw-init", action="store_true",
                     help="keep nn.Linear's default init on the deformation heads (the iteration-3000 transient: "
                          "deltas O(0.3) make every Gaussian hundreds of pixels wide)")
@@ -228,8 +230,8 @@ def main():
         step(k)
     torch.cuda.synchronize()
     lib.dgs_timing_reset()
-    lib.dgs_timing_select({"major": b"mlp_fwd,mlp_bwd,mlp_dw,blend_fwd,blend_bwd", "all": b"", "none": b""}[
-        args.kernel_timing])
+    lib.dgs_timing_select({"roofline": b"mlp_dw", "major": b"mlp_fwd,mlp_bwd,mlp_dw,blend_fwd,blend_bwd", "all": b"",
+                           "none": b""}[args.kernel_timing])
     lib.dgs_timing_enable(0 if args.kernel_timing == "none" else 1)
     if world > 1:
         dist.barrier()

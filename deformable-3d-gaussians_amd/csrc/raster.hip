@@ -225,7 +225,7 @@ __device__ inline uint32_t tagged_total(const unsigned long long *tot, int t, ui
 }
 
 __device__ void rect_starts(int T, const unsigned long long *__restrict__ tot, uint32_t gen, uint32_t *__restrict__ tile_start,
-                            uint2 *__restrict__ ranges, uint32_t *wsum) {
+                            uint2 *__restrict__ ranges, uint32_t *wsum, uint32_t *host_total) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     constexpr int MAXPER = 12;  // RECT_MAX_TILES / 1024
     const int per = div_up(T, 1024);
@@ -255,6 +255,8 @@ __device__ void rect_starts(int T, const unsigned long long *__restrict__ tot, u
             run += c[k];
         }
     }
+    // the pair count straight into the host's pinned word (no copy launch): the last thread's run
+    if (host_total && tid == 1023) *host_total = run;
 }
 
 // the column of block counts of 64 tiles per workgroup -> exclusive offsets (in place), the tile
@@ -262,7 +264,8 @@ __device__ void rect_starts(int T, const unsigned long long *__restrict__ tot, u
 // cross-wave prefix in LDS, carry between chunks
 __global__ __launch_bounds__(1024) void k_rect_colscan(int nb, int T, uint32_t *__restrict__ cnt, unsigned long long *__restrict__ tot, uint32_t gen,
                                                        uint32_t *__restrict__ total, uint32_t *__restrict__ ticket,
-                                                       uint32_t *__restrict__ tile_start, uint2 *__restrict__ ranges) {
+                                                       uint32_t *__restrict__ tile_start, uint2 *__restrict__ ranges,
+                                                       uint32_t *host_total) {
     __shared__ uint32_t part[16][64];
     __shared__ uint32_t carry[64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -304,7 +307,7 @@ __global__ __launch_bounds__(1024) void k_rect_colscan(int nb, int T, uint32_t *
     if (threadIdx.x == 0) last = atomicAdd(ticket, 1u) == gridDim.x - 1;
     __syncthreads();
     if (!last) return;
-    rect_starts(T, tot, gen, tile_start, ranges, wsum);
+    rect_starts(T, tot, gen, tile_start, ranges, wsum, host_total);
 }
 
 __host__ __device__ inline size_t rect_place_lds(int gx, int gy) {
@@ -882,6 +885,7 @@ struct dgs_raster_ctx {
     hipStream_t last_stream = nullptr;
     bool pending_release = false;
     uint32_t *h_total = nullptr;  // pinned host word: the num_rendered read-back (no staging copy)
+    uint32_t *d_total = nullptr;  // its device address (k_rect_colscan writes the count there)
     hipEvent_t count_ev = nullptr;  // recorded after the read-back copy
 };
 
@@ -1236,7 +1240,10 @@ extern "C" int dgs_raster_forward(const dgs_raster_settings *s, int P, int M, co
             }
         }
         DGS_LAUNCH_CHECK("depth_sort", dbg, stream);
-        if (!c->h_total) DGS_HIP_CHECK(hipHostMalloc((void **)&c->h_total, sizeof(uint32_t), hipHostMallocDefault));
+        if (!c->h_total) {  // coherent + mapped: k_rect_colscan stores the count into it directly
+            DGS_HIP_CHECK(hipHostMalloc((void **)&c->h_total, sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped));
+            DGS_HIP_CHECK(hipHostGetDevicePointer((void **)&c->d_total, c->h_total, 0));
+        }
         if (!c->count_ev) DGS_HIP_CHECK(hipEventCreateWithFlags(&c->count_ev, hipEventDisableTiming));
         if (c->rect_mode) {
             const int nb = div_up(P, 256);
@@ -1249,10 +1256,10 @@ extern "C" int dgs_raster_forward(const dgs_raster_settings *s, int P, int M, co
             {
                 ScopedTimer tm("scan", stream);
                 hipLaunchKernelGGL(k_rect_colscan, dim3(div_up(T, 64)), dim3(1024), 0, stream, nb, T, c->rect_cnt, c->rect_tot,
-                                   next_rect_gen(), c->rect_total, c->rect_total + 1, c->rect_start, c->ranges);
+                                   next_rect_gen(), c->rect_total, c->rect_total + 1, c->rect_start, c->ranges,
+                                   c->d_total);
             }
             DGS_LAUNCH_CHECK("k_rect_colscan", dbg, stream);
-            DGS_HIP_CHECK(hipMemcpyAsync(c->h_total, c->rect_total, 4, hipMemcpyDeviceToHost, stream));
         } else {
             DGS_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(g + off_st, scan_tmp, c->tiles_sorted, c->offsets, P, stream));
             DGS_HIP_CHECK(hipMemcpyAsync(c->h_total, c->offsets + (P - 1), 4, hipMemcpyDeviceToHost, stream));
