@@ -443,8 +443,8 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
     const int r = __builtin_amdgcn_readfirstlane(tid >> 6);  // n-tile of this wave (provably uniform)
     const int kq = lane >> 4, col = lane & 15;
     const int pend = min(a.N, p0 + BMB);  // real points of the block: [p0, pend)
-#ifdef DGS_DIAG_PRIO  // experiment: static priority for the second-dispatched half (MI355X_MICROARCH.md)
-    if (r >= 8) __builtin_amdgcn_s_setprio(1);
+#ifdef DGS_DIAG_PRIO  // experiment: static priority for the last-dispatched wave of each SIMD
+    if (r >= 12) __builtin_amdgcn_s_setprio(1);
 #endif
 #ifdef DGS_DIAG_PRIO2  // experiment: graded priority by dispatch order within a SIMD
     if (r >= 12) __builtin_amdgcn_s_setprio(3);
@@ -593,6 +593,9 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
         else gemm<8, NQB>(Aw, lds, g0, 0, lane, c, bp, hg);
         DGS_STAMP(4 + 2 * L);
         DGS_WSTAMP(22, L);  // per wave: GEMM end (layer 3)
+#ifdef DGS_DIAG_EPI_PRIO  // experiment: raised issue priority through the epilogue
+        __builtin_amdgcn_s_setprio(2);
+#endif
 #ifndef DGS_DIAG_NO_EPI  // timing experiment only (wrong results): no bias/relu/mask/split/store epilogue
         bias_relu(c, bv, true);
         if (SAVE) {
@@ -607,6 +610,9 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
         for (int q = 0; q < NQB; q++) acc_to_lds(c[q], lds, G_H, r, q, lane);
 #endif
         lds_signal(hwr + (r >> 1), lane);
+#ifdef DGS_DIAG_EPI_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
         if (L == 3 && r == 0) DGS_STAMP(55);
         DGS_STAMP(5 + 2 * L);
     }
