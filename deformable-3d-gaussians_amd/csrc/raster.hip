@@ -1039,6 +1039,41 @@ dgs_raster_ctx *ctx_acquire(int device, hipStream_t stream) {
 }
 }  // namespace
 
+// The pair count of this frame on the host. Sort binning: the pinned word behind count_ev. Rect
+// binning: k_rect_colscan stores the count into the coherent pinned word itself, so the host polls
+// the word (no event record in the stream: one costs ~6 us of GPU idle); the stream is queried
+// every 1024 polls so a failed launch cannot spin forever.
+constexpr uint32_t COUNT_PENDING = 0xffffffffu;
+static int wait_count(dgs_raster_ctx *c, hipStream_t stream, int &nr) {
+    if (!c->rect_mode) {
+        DGS_HIP_CHECK(hipEventSynchronize(c->count_ev));
+        nr = (int)*c->h_total;
+        return DGS_OK;
+    }
+    volatile uint32_t *w = c->h_total;
+    for (uint32_t i = 1;; i++) {
+        uint32_t v = *w;
+        if (v == COUNT_PENDING && (i & 1023) == 0) {
+            const hipError_t e = hipStreamQuery(stream);
+            if (e == hipSuccess) {
+                v = *w;
+                if (v == COUNT_PENDING) {
+                    set_error("dgs_raster_forward: pair count not written by k_rect_colscan");
+                    return DGS_ERR_HIP;
+                }
+            } else if (e != hipErrorNotReady) {
+                DGS_HIP_CHECK(e);
+            }
+        }
+        if (v != COUNT_PENDING) {
+            std::atomic_thread_fence(std::memory_order_acquire);
+            nr = (int)v;
+            return DGS_OK;
+        }
+        __builtin_ia32_pause();
+    }
+}
+
 // Binning for `cap` pairs (>= num_rendered, or the speculative capacity) + the blend: the key
 // buffer is pre-filled with all-ones (past every tile id, so the unused tail sorts last and leaves
 // the stable order of the real pairs untouched), bounded duplicate in depth order, stable radix sort
@@ -1247,6 +1282,7 @@ extern "C" int dgs_raster_forward(const dgs_raster_settings *s, int P, int M, co
         if (!c->count_ev) DGS_HIP_CHECK(hipEventCreateWithFlags(&c->count_ev, hipEventDisableTiming));
         if (c->rect_mode) {
             const int nb = div_up(P, 256);
+            *(volatile uint32_t *)c->h_total = COUNT_PENDING;  // k_rect_colscan overwrites it
             {
                 ScopedTimer tm("count", stream);
                 hipLaunchKernelGGL(k_rect_count, dim3(nb), dim3(256), 4ull * T, stream, P, c->order, c->xy, c->radii, c->gx,
@@ -1264,18 +1300,16 @@ extern "C" int dgs_raster_forward(const dgs_raster_settings *s, int P, int M, co
             DGS_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(g + off_st, scan_tmp, c->tiles_sorted, c->offsets, P, stream));
             DGS_HIP_CHECK(hipMemcpyAsync(c->h_total, c->offsets + (P - 1), 4, hipMemcpyDeviceToHost, stream));
         }
-        DGS_HIP_CHECK(hipEventRecord(c->count_ev, stream));
+        if (!c->rect_mode) DGS_HIP_CHECK(hipEventRecord(c->count_ev, stream));
         int cap = pair_cap_get(device);
         const bool speculative = cap > 0 && !dbg;
         if (!speculative) {
-            DGS_HIP_CHECK(hipEventSynchronize(c->count_ev));
-            nr = (int)*c->h_total;
+            if (int rc = wait_count(c, stream, nr)) return rc;
             cap = nr;
         }
         if (int rc = bin_and_blend(c, cap, P, device, stream, dbg, out_color, out_depth)) return rc;
         if (speculative) {
-            DGS_HIP_CHECK(hipEventSynchronize(c->count_ev));
-            nr = (int)*c->h_total;
+            if (int rc = wait_count(c, stream, nr)) return rc;
             if (nr > cap) {  // overflow: redo binning + blend at the exact size
                 {
                     std::lock_guard<std::mutex> lk(g_cap_mu);
