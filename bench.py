@@ -167,7 +167,7 @@ def cpu_baseline(N, res, steps):
 def main():
     args = parse()
     from deformgs import _lib
-    from deformgs.dist import GradAllReduce, init_from_env
+    from deformgs.dist import OverlappedGradAllReduce, init_from_env
     from deformgs.deform_model import DeformModelBaseline
     from deformgs.gaussian_model import GaussianModel
     from deformgs.arguments import OptimizationParams, PipelineParams
@@ -212,14 +212,17 @@ def main():
             d = deform.step(gaussians.get_xyz.detach(), cam.fid.unsqueeze(0).expand(N, -1))
             img = render(cam, gaussians, pipe, bg, d[0], d[1], d[2])["render"]
             gts.append((img + 0.02 * torch.randn(img.shape, device=dev, generator=gen)).clamp_(0.0, 1.0))
-    allreduce = GradAllReduce(lambda: list(deform.deform.parameters()) + [
-        gaussians._xyz, gaussians._features_dc, gaussians._features_rest, gaussians._scaling, gaussians._rotation,
-        gaussians._opacity])
+    # Gaussian gradients are all-reduced during the MLP backward (their hooks fire first), the MLP's after
+    allreduce = OverlappedGradAllReduce(
+        lambda: [gaussians._xyz, gaussians._features_dc, gaussians._features_rest, gaussians._scaling,
+                 gaussians._rotation, gaussians._opacity],
+        lambda: list(deform.deform.parameters()))
 
     state = {"it": 3000, "P": 0}
 
     def step(k):
         cam = cams[k % len(cams)]
+        allreduce.arm()
         loss, pkg = forward_backward(gaussians, deform, cam, gts[k % len(cams)], pipe, bg)
         allreduce()
         if not args.no_adam:

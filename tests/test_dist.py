@@ -9,7 +9,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from deformgs.dist import GradAllReduce, init_from_env, rank_identical_generator, sync_densification_stats
+from deformgs.dist import (GradAllReduce, OverlappedGradAllReduce, init_from_env, rank_identical_generator,
+                           sync_densification_stats)
 
 
 def _free_port():
@@ -20,13 +21,31 @@ def _free_port():
     return port
 
 
+def _to_np(v):
+    """Tensors cross the queue as numpy arrays: a tensor travels as a shared-memory fd that the
+    parent can only fetch while the (already exiting) worker still serves it."""
+    if isinstance(v, torch.Tensor):
+        return ("__t__", v.detach().cpu().numpy())
+    if isinstance(v, (list, tuple)):
+        return type(v)(_to_np(x) for x in v)
+    return v
+
+
+def _from_np(v):
+    if isinstance(v, tuple) and len(v) == 2 and v[0] == "__t__":
+        return torch.from_numpy(v[1])
+    if isinstance(v, (list, tuple)):
+        return type(v)(_from_np(x) for x in v)
+    return v
+
+
 def _worker(rank, world, port, fn, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     try:
         r, w, _ = init_from_env("gloo")
         assert (r, w) == (rank, world)
-        q.put((rank, fn(rank, world)))
+        q.put((rank, _to_np(fn(rank, world))))
     except Exception as e:  # surfaced in the parent
         q.put((rank, e))
     finally:
@@ -44,7 +63,7 @@ def _run(fn, world=2):
     out = {}
     for _ in range(world):
         r, v = q.get(timeout=120)
-        out[r] = v
+        out[r] = _from_np(v)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -133,3 +152,40 @@ def test_single_process_is_noop():
     GradAllReduce(lambda: [p])()
     torch.testing.assert_close(p.grad, torch.full((3,), 2.0))
     sync_densification_stats(types.SimpleNamespace())  # not initialised -> untouched
+
+
+def _overlap_case(rank, world):
+    """Early group (a, b) reduced by the post-accumulate hooks during backward, late group (c) after;
+    step 2: on rank 1 `b` gets no gradient, so its hook group never completes there (fallback)."""
+    a = torch.nn.Parameter(torch.zeros(7))
+    b = torch.nn.Parameter(torch.zeros(3, 2))
+    c = torch.nn.Parameter(torch.zeros(5))
+    ar = OverlappedGradAllReduce(lambda: [a, b], lambda: [c])
+    out = []
+    for step in range(2):
+        for p in (a, b, c):
+            p.grad = None
+        ar.arm()
+        s = (rank + 1.0)
+        loss = (s * torch.arange(7.0) * a).sum() + (2 * s * c).sum()
+        if not (step == 1 and rank == 1):
+            loss = loss + (3 * s * b).sum()
+        loss.backward()
+        fired = ar._pending is not None
+        ar()
+        out.append((fired, a.grad.clone(), None if b.grad is None else b.grad.clone(), c.grad.clone()))
+    return out
+
+
+def test_overlapped_grad_allreduce():
+    out = _run(_overlap_case)
+    for rank in (0, 1):
+        (f0, a0, b0, c0), (f1, a1, b1, c1) = out[rank]
+        assert f0, "the early group's hook must start the collective during backward"
+        torch.testing.assert_close(a0, 1.5 * torch.arange(7.0))
+        torch.testing.assert_close(b0, torch.full((3, 2), 4.5))
+        torch.testing.assert_close(c0, torch.full((5,), 3.0))
+        assert f1 == (rank == 0)  # rank 1 had no b gradient in step 2: reduced in __call__ instead
+        torch.testing.assert_close(a1, 1.5 * torch.arange(7.0))
+        torch.testing.assert_close(b1, torch.full((3, 2), 1.5))  # (3 * 1 + 0) / 2
+        torch.testing.assert_close(c1, torch.full((5,), 3.0))
