@@ -15,6 +15,10 @@ def init_from_env(backend=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of N ranks on fewer GPUs (tests / a one-GPU box): DGS_DEVICE pins every rank's device,
+    # DGS_DIST_BACKEND=gloo replaces RCCL (which refuses two ranks on one GPU)
+    local = int(os.environ.get("DGS_DEVICE", local))
+    backend = backend or os.environ.get("DGS_DIST_BACKEND") or None
     if world > 1 and not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
