@@ -36,6 +36,11 @@ class AdamTensor(ctypes.Structure):
     ]
 
 
+class RowJob(ctypes.Structure):
+    """dgs_row_job (include/dgs.h)."""
+    _fields_ = [("src", P), ("dst", P), ("width", I)]
+
+
 _SIGS = {
     "dgs_last_error": ([], ctypes.c_char_p),
     "dgs_version": ([], ctypes.c_char_p),
@@ -64,6 +69,7 @@ _SIGS = {
     "dgs_l1_ssim_forward": ([I, I, I, P, P, F, P, P, P], I),
     "dgs_l1_ssim_backward": ([I, I, I, P, P, F, P, P, P, P], I),
     "dgs_adam_step": ([I, ctypes.POINTER(AdamTensor), ctypes.c_double, ctypes.c_double, ctypes.c_double, P], I),
+    "dgs_select_rows": ([I, P, I, ctypes.POINTER(RowJob), P], I),
     "dgs_gaussian_inputs_forward": ([I, I] + [P] * 7 + [I] + [P] * 5 + [P], I),
     "dgs_gaussian_inputs_backward": ([I, I] + [P] * 15 + [I, P], I),
 }

@@ -13,6 +13,7 @@ import numpy as np
 import torch
 from torch import nn
 
+from .compact import select_rows
 from . import _lib
 from .general import build_rotation, get_expon_lr_func, inverse_sigmoid, strip_symmetric, build_scaling_rotation
 from .adam import Adam
@@ -203,20 +204,30 @@ class GaussianModel:
         new = inverse_sigmoid(torch.min(self.get_opacity, torch.ones_like(self.get_opacity) * 0.01))
         self._opacity = self.replace_tensor_to_optimizer(new, "opacity")["opacity"]
 
-    def _prune_optimizer(self, mask):
-        out = {}
+    def _prune_optimizer(self, mask, extra=()):
+        """Keeps the rows of `mask` in every parameter and its Adam moments (and in the tensors of
+        `extra`, returned second) with ONE row-selection launch (deformgs/compact.py)."""
+        groups, srcs = [], []
         for group in self.optimizer.param_groups:
             st = self.optimizer.state.get(group['params'][0], None)
+            groups.append((group, st))
+            srcs.append(group["params"][0].detach())
             if st is not None:
-                st["exp_avg"] = st["exp_avg"][mask]
-                st["exp_avg_sq"] = st["exp_avg_sq"][mask]
+                srcs += [st["exp_avg"], st["exp_avg_sq"]]
+        sel = select_rows(mask, srcs + list(extra))
+        out, k = {}, 0
+        for group, st in groups:
+            new_p = sel[k]
+            k += 1
+            if st is not None:
+                st["exp_avg"], st["exp_avg_sq"] = sel[k], sel[k + 1]
+                k += 2
                 del self.optimizer.state[group['params'][0]]
-                group["params"][0] = nn.Parameter(group["params"][0][mask].requires_grad_(True))
+            group["params"][0] = nn.Parameter(new_p.requires_grad_(True))
+            if st is not None:
                 self.optimizer.state[group['params'][0]] = st
-            else:
-                group["params"][0] = nn.Parameter(group["params"][0][mask].requires_grad_(True))
             out[group["name"]] = group["params"][0]
-        return out
+        return out, sel[k:]
 
     def _assign(self, t):
         self._xyz, self._features_dc, self._features_rest = t["xyz"], t["f_dc"], t["f_rest"]
@@ -224,10 +235,9 @@ class GaussianModel:
 
     def prune_points(self, mask):
         valid = ~mask
-        self._assign(self._prune_optimizer(valid))
-        self.xyz_gradient_accum = self.xyz_gradient_accum[valid]
-        self.denom = self.denom[valid]
-        self.max_radii2D = self.max_radii2D[valid]
+        params, (self.xyz_gradient_accum, self.denom, self.max_radii2D) = self._prune_optimizer(
+            valid, (self.xyz_gradient_accum, self.denom, self.max_radii2D))
+        self._assign(params)
 
     def cat_tensors_to_optimizer(self, d):
         out = {}
@@ -261,23 +271,27 @@ class GaussianModel:
         padded[:grads.shape[0]] = grads.squeeze()
         sel = torch.where(padded >= grad_threshold, True, False)
         sel = torch.logical_and(sel, torch.max(self.get_scaling, dim=1).values > self.percent_dense * scene_extent)
-        stds = self.get_scaling[sel].repeat(N, 1)
+        xyz, fdc, frest, opac, scaling, rot = select_rows(sel, [
+            self._xyz.detach(), self._features_dc.detach(), self._features_rest.detach(), self._opacity.detach(),
+            self._scaling.detach(), self._rotation.detach()])
+        sel_scaling = self.scaling_activation(scaling)
+        stds = sel_scaling.repeat(N, 1)
         means = torch.zeros((stds.size(0), 3), device=dev)
         samples = torch.normal(mean=means, std=stds, generator=generator)
-        rots = build_rotation(self._rotation[sel]).repeat(N, 1, 1)
-        new_xyz = torch.bmm(rots, samples.unsqueeze(-1)).squeeze(-1) + self.get_xyz[sel].repeat(N, 1)
-        new_scaling = self.scaling_inverse_activation(self.get_scaling[sel].repeat(N, 1) / (0.8 * N))
-        self.densification_postfix(new_xyz, self._features_dc[sel].repeat(N, 1, 1),
-                                   self._features_rest[sel].repeat(N, 1, 1), self._opacity[sel].repeat(N, 1),
-                                   new_scaling, self._rotation[sel].repeat(N, 1))
+        rots = build_rotation(rot).repeat(N, 1, 1)
+        new_xyz = torch.bmm(rots, samples.unsqueeze(-1)).squeeze(-1) + xyz.repeat(N, 1)
+        new_scaling = self.scaling_inverse_activation(sel_scaling.repeat(N, 1) / (0.8 * N))
+        self.densification_postfix(new_xyz, fdc.repeat(N, 1, 1), frest.repeat(N, 1, 1), opac.repeat(N, 1),
+                                   new_scaling, rot.repeat(N, 1))
         prune = torch.cat((sel, torch.zeros(N * sel.sum(), device=dev, dtype=bool)))
         self.prune_points(prune)
 
     def densify_and_clone(self, grads, grad_threshold, scene_extent):
         sel = torch.where(torch.norm(grads, dim=-1) >= grad_threshold, True, False)
         sel = torch.logical_and(sel, torch.max(self.get_scaling, dim=1).values <= self.percent_dense * scene_extent)
-        self.densification_postfix(self._xyz[sel], self._features_dc[sel], self._features_rest[sel],
-                                   self._opacity[sel], self._scaling[sel], self._rotation[sel])
+        self.densification_postfix(*select_rows(sel, [
+            self._xyz.detach(), self._features_dc.detach(), self._features_rest.detach(), self._opacity.detach(),
+            self._scaling.detach(), self._rotation.detach()]))
 
     def densify_and_prune(self, max_grad, min_opacity, extent, max_screen_size, generator=None):
         grads = self.xyz_gradient_accum / self.denom

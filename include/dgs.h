@@ -193,6 +193,19 @@ typedef struct dgs_adam_tensor {
 } dgs_adam_tensor;
 int dgs_adam_step(int n, const dgs_adam_tensor *tensors, double beta1, double beta2, double eps, void *stream);
 
+/* ---- Row selection (stream compaction) over many tensors in one launch ----
+ * Replaces the per-tensor boolean indexing of densification: prune_points / _prune_optimizer
+ * (t[mask] for every parameter, both Adam moments and the statistics) and the row gathers of
+ * densify_and_clone / densify_and_split (scene/gaussian_model.py:206-246, 280-312 upstream
+ * layout). For every job, dst[k] = src[i] for the k-th row i (in order) with mask[i] != 0; rows are
+ * `width` contiguous floats, dst holds sum(mask != 0) rows. mask: nrows bytes (0 / 1, device). */
+typedef struct dgs_row_job {
+    const float *src;
+    float *dst;
+    int width;
+} dgs_row_job;
+int dgs_select_rows(int nrows, const uint8_t *mask, int njobs, const dgs_row_job *jobs, void *stream);
+
 #ifdef __cplusplus
 }
 #endif
