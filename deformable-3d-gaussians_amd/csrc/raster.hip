@@ -310,22 +310,31 @@ __global__ __launch_bounds__(1024) void k_rect_colscan(int nb, int T, uint32_t *
     rect_starts(T, tot, gen, tile_start, ranges, wsum, host_total);
 }
 
-__host__ __device__ inline size_t rect_place_lds(int gx, int gy) {
-    return 4ull * ((gx * gy + 1) & ~1) + 4ull * 8ull * (gx + gy);
+__host__ __device__ inline size_t rect_place_lds(int gx, int gy, bool stage) {
+    return 4ull * ((gx * gy + 1) & ~1) * (stage ? 2 : 1) + 4ull * 8ull * (gx + gy);
 }
+// the block's output base per tile (tile start + the block's column offset) staged in LDS when it fits
+__host__ __device__ inline bool rect_place_stage(int gx, int gy) { return rect_place_lds(gx, gy, true) <= 65536; }
 
 __global__ __launch_bounds__(256) void k_rect_place(int P, const uint32_t *__restrict__ order, const float2 *__restrict__ xy,
                                                     const int *__restrict__ radii, int gx, int gy,
                                                     const uint32_t *__restrict__ cnt, const uint32_t *__restrict__ tile_start,
-                                                    uint32_t cap, uint32_t *__restrict__ vals) {
+                                                    uint32_t cap, uint32_t *__restrict__ vals, int stage) {
     extern __shared__ uint32_t lds[];
     const int T = gx * gy, G = gx + gy;
     // per tile, the four waves' counts packed one byte each (a wave adds at most 64 per tile)
+    const int Tp = (T + 1) & ~1;
     uint32_t *wc = lds;  // [T]
+    // stage: the block's first output position per tile (tile start + this block's column offset),
+    // read coalesced once instead of gathered per pair
+    uint32_t *base = lds + Tp;  // [T] (stage)
     // per wave, the lanes whose rectangle spans tile column x ([x]) / tile row y ([gx + y])
-    unsigned long long *span = reinterpret_cast<unsigned long long *>(lds + ((T + 1) & ~1));  // [4][G]
+    unsigned long long *span = reinterpret_cast<unsigned long long *>(lds + (stage ? 2 * Tp : Tp));  // [4][G]
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t *crow = cnt + (size_t)blockIdx.x * T;
     for (int t = tid; t < T; t += 256) wc[t] = 0;
+    if (stage)
+        for (int t = tid; t < T; t += 256) base[t] = tile_start[t] + crow[t];
     for (int t = tid; t < 4 * G; t += 256) span[t] = 0ull;
     const int j = blockIdx.x * 256 + tid;
     const uint32_t g = j < P ? order[j] : 0u;
@@ -340,7 +349,6 @@ __global__ __launch_bounds__(256) void k_rect_place(int P, const uint32_t *__res
         for (int x = rc.x; x < rc.z; x++) atomicAdd(&wc[y * gx + x], 1u << (8 * w));
     }
     __syncthreads();
-    const uint32_t *crow = cnt + (size_t)blockIdx.x * T;
     for (int y = rc.y; y < rc.w; y++) {
         const unsigned long long rows = ws[gx + y] & (me - 1ull);  // lanes below spanning row y
         for (int x = rc.x; x < rc.z; x++) {
@@ -348,7 +356,7 @@ __global__ __launch_bounds__(256) void k_rect_place(int P, const uint32_t *__res
             const uint32_t rank = (uint32_t)__popcll(rows & ws[x]);
             // waves below: byte w-1 of the packed inclusive sums (partial sums <= 192, no carries)
             const uint32_t below = w ? ((wc[t] * 0x01010101u) >> (8 * (w - 1))) & 0xffu : 0u;
-            const uint32_t pos = tile_start[t] + crow[t] + below + rank;
+            const uint32_t pos = (stage ? base[t] : tile_start[t] + crow[t]) + below + rank;
             if (pos < cap) vals[pos] = g;
         }
     }
@@ -930,7 +938,7 @@ uint32_t next_rect_gen() {
 
 bool rect_binning(int gx, int gy, int P) {
     const int T = gx * gy;
-    return binning_mode() == 0 && T <= RECT_MAX_TILES && rect_place_lds(gx, gy) <= 65536 &&
+    return binning_mode() == 0 && T <= RECT_MAX_TILES && rect_place_lds(gx, gy, false) <= 65536 &&
            (long long)div_up(P, 256) * T <= RECT_MAX_CELLS;
 }
 
@@ -1131,8 +1139,10 @@ static int bin_and_blend(dgs_raster_ctx *c, int cap, int P, int device, hipStrea
         const int nb = div_up(P, 256);
         if (cap > 0) {
             ScopedTimer tm("place", stream);
-            hipLaunchKernelGGL(k_rect_place, dim3(nb), dim3(256), rect_place_lds(c->gx, c->gy), stream, P, c->order, c->xy, c->radii,
-                               c->gx, c->gy, c->rect_cnt, c->rect_start, (uint32_t)cap, c->vals);
+            const bool stage = rect_place_stage(c->gx, c->gy);
+            hipLaunchKernelGGL(k_rect_place, dim3(nb), dim3(256), rect_place_lds(c->gx, c->gy, stage), stream, P, c->order,
+                               c->xy, c->radii, c->gx, c->gy, c->rect_cnt, c->rect_start, (uint32_t)cap, c->vals,
+                               (int)stage);
         }
         DGS_LAUNCH_CHECK("k_rect_place", dbg, stream);
     } else if (cap > 0) {  // k_duplicate clears c->ranges

@@ -109,12 +109,13 @@ __global__ __launch_bounds__(256) void k_ssim_fwd(int H, int W, const float *__r
     }
 }
 
-// out[0] = loss, out[1] = mean L1, out[2] = mean SSIM; one workgroup, fixed order (deterministic)
-__global__ __launch_bounds__(256) void k_ssim_final(int nblocks, float n, float lambda, const float *__restrict__ partial,
-                                                    float *__restrict__ out) {
-    __shared__ double red[2][4];
+// out[0] = loss, out[1] = mean L1, out[2] = mean SSIM; one workgroup of 1024 (16 waves: the partial
+// sums are a latency chain of double adds per thread), fixed order (deterministic)
+__global__ __launch_bounds__(1024) void k_ssim_final(int nblocks, float n, float lambda, const float *__restrict__ partial,
+                                                     float *__restrict__ out) {
+    __shared__ double red[2][16];
     double a = 0.0, b = 0.0;
-    for (int i = threadIdx.x; i < nblocks; i += 256) {
+    for (int i = threadIdx.x; i < nblocks; i += 1024) {
         a += (double)partial[2 * i];
         b += (double)partial[2 * i + 1];
     }
@@ -129,8 +130,11 @@ __global__ __launch_bounds__(256) void k_ssim_final(int nblocks, float n, float 
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        double sa = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
-        double sb = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+        double sa = 0.0, sb = 0.0;
+        for (int w = 0; w < 16; w++) {
+            sa += red[0][w];
+            sb += red[1][w];
+        }
         float l1 = (float)(sa / n), ss = (float)(sb / n);
         out[0] = (1.f - lambda) * l1 + lambda * (1.f - ss);
         out[1] = l1;
@@ -226,7 +230,7 @@ extern "C" int dgs_l1_ssim_forward(int C, int H, int W, const float *img, const 
     {
         ScopedTimer tm("ssim_fwd", stream);
         hipLaunchKernelGGL(ssim::k_ssim_fwd, grid, dim3(256), 0, stream, H, W, img, gt, ssim::make_window(), maps, partial);
-        hipLaunchKernelGGL(ssim::k_ssim_final, dim3(1), dim3(256), 0, stream, nb, (float)C * H * W, lambda, partial, out3);
+        hipLaunchKernelGGL(ssim::k_ssim_final, dim3(1), dim3(1024), 0, stream, nb, (float)C * H * W, lambda, partial, out3);
     }
     DGS_LAUNCH_CHECK("k_ssim_fwd", false, stream);
     return DGS_OK;
