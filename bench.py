@@ -60,6 +60,9 @@ def parse():
     return ap.parse_args()
 
 
+SYNC_COUNT = os.environ.get("DGS_BENCH_SYNC_COUNT", "0") == "1"  # A/B: the synchronous pair count
+
+
 def mfma_peak(name):
     """Dense MFMA peak (fp32-equivalent TFLOP/s) of the arithmetic kernel class `name` runs on."""
     exact = os.environ.get("DGS_MLP_EXACT_FP32", "0") not in ("", "0")
@@ -172,7 +175,7 @@ def main():
     from deformgs.gaussian_model import GaussianModel
     from deformgs.arguments import OptimizationParams, PipelineParams
     from deformgs.synthetic import synth_camera, synth_gaussians
-    from deformgs.train_step import forward_backward, optimizer_step
+    from deformgs.train_step import deferred_overflowed, drop_grads, forward_backward, optimizer_step
     import torch.distributed as dist
 
     rank, world, local = init_from_env()
@@ -218,12 +221,21 @@ def main():
                  gaussians._rotation, gaussians._opacity],
         lambda: list(deform.deform.parameters()))
 
-    state = {"it": 3000, "P": 0}
+    state = {"it": 3000, "P": 0, "redos": 0}
 
     def step(k):
         cam = cams[k % len(cams)]
         allreduce.arm()
-        loss, pkg = forward_backward(gaussians, deform, cam, gts[k % len(cams)], pipe, bg)
+        # one rank: the rasterizer does not wait for the pair count (the host keeps issuing); a step
+        # whose speculative pair capacity overflowed is redone synchronously. Several ranks: the
+        # synchronous count (a redo there would have to be agreed on by every rank before the
+        # overlapped all-reduce consumes the gradients)
+        loss, pkg = forward_backward(gaussians, deform, cam, gts[k % len(cams)], pipe, bg,
+                                     deferred_count=(world == 1 and not SYNC_COUNT))
+        if world == 1 and deferred_overflowed():
+            state["redos"] += 1
+            drop_grads(gaussians, deform)
+            loss, pkg = forward_backward(gaussians, deform, cam, gts[k % len(cams)], pipe, bg)
         allreduce()
         if not args.no_adam:
             optimizer_step(gaussians, deform, state["it"])
@@ -311,7 +323,7 @@ def main():
         "config": {"workload": f"synth-100k: {N} Gaussians, {R}x{R}, blender DeformNetworkBaseline, SH3"
                    + (" (raw-init heads)" if args.raw_init else " (heads at 1/100 init: steady-state deltas)"),
                    "global_batch": world, "includes_adam": not args.no_adam, "pairs_per_render": P_pairs,
-                   "pair_capacity": pair_cap,
+                   "pair_capacity": pair_cap, "redone_steps": state["redos"],
                    "parallelism": f"dp{world} (frame-parallel, RCCL grad all-reduce)"},
         "roofline": roofline,
         "kernels_ms_per_step": {k: v[0] / args.steps for k, v in kernels.items()},

@@ -894,6 +894,8 @@ struct dgs_raster_ctx {
     bool pending_release = false;
     uint32_t *h_total = nullptr;  // pinned host word: the num_rendered read-back (no staging copy)
     uint32_t *d_total = nullptr;  // its device address (k_rect_colscan writes the count there)
+    bool count_pending = false;   // deferred count: num_rendered not read yet (resolve_count)
+    int spec_cap = 0;              // the speculative capacity the binning ran with
     hipEvent_t count_ev = nullptr;  // recorded after the read-back copy
 };
 
@@ -1163,6 +1165,41 @@ static int bin_and_blend(dgs_raster_ctx *c, int cap, int P, int device, hipStrea
     return DGS_OK;
 }
 
+// Deferred pair count (dgs_raster_set_deferred_count): the forward returns without waiting for
+// num_rendered; the count is read when the backward starts (the GPU is long past the scan by then)
+// or when the context is freed. An overflow of the speculative capacity is then too late to redo the
+// forward, so it is counted (dgs_raster_deferred_overflows) and the caller redoes the whole training
+// step synchronously (deformgs/train_step.py); the backward runs on ranges clipped to the capacity
+// so it stays in bounds.
+std::atomic<int> g_deferred{0};
+std::atomic<long long> g_deferred_overflows{0};
+
+__global__ void k_clip_ranges(int T, uint2 *ranges, uint32_t cap) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < T) {
+        uint2 r = ranges[t];
+        ranges[t] = make_uint2(min(r.x, cap), min(r.y, cap));
+    }
+}
+
+static int resolve_count(dgs_raster_ctx *c, hipStream_t stream) {
+    if (!c->count_pending) return DGS_OK;
+    c->count_pending = false;
+    int nr = 0;
+    if (int rc = wait_count(c, stream, nr)) return rc;
+    pair_cap_observe(c->device, nr);
+    if (nr > c->spec_cap) {
+        g_deferred_overflows++;
+        const int T = c->gx * c->gy;
+        hipLaunchKernelGGL(k_clip_ranges, dim3(div_up(T, 256)), dim3(256), 0, stream, T, c->ranges, (uint32_t)c->spec_cap);
+        DGS_LAUNCH_CHECK("k_clip_ranges", false, stream);
+        c->num_rendered = c->spec_cap;
+    } else {
+        c->num_rendered = nr;
+    }
+    return DGS_OK;
+}
+
 extern "C" int dgs_raster_forward(const dgs_raster_settings *s, int P, int M, const float *means3D,
                                   const float *shs, const float *colors_precomp, const float *opacities,
                                   const float *scales, const float *rotations, const float *cov3D_precomp,
@@ -1318,6 +1355,14 @@ extern "C" int dgs_raster_forward(const dgs_raster_settings *s, int P, int M, co
             cap = nr;
         }
         if (int rc = bin_and_blend(c, cap, P, device, stream, dbg, out_color, out_depth)) return rc;
+        if (speculative && g_deferred.load()) {  // num_rendered read by the backward (resolve_count)
+            c->count_pending = true;
+            c->spec_cap = cap;
+            c->num_rendered = cap;
+            *ctx_out = c;
+            if (num_rendered) *num_rendered = -1;
+            return DGS_OK;
+        }
         if (speculative) {
             if (int rc = wait_count(c, stream, nr)) return rc;
             if (nr > cap) {  // overflow: redo binning + blend at the exact size
@@ -1360,6 +1405,7 @@ extern "C" int dgs_raster_backward(dgs_raster_ctx *c, const float *dL_dcolor, co
     const int P = c->P;
     c->last_stream = stream;
     if (P == 0) return DGS_OK;
+    if (int rc = resolve_count(c, stream)) return rc;
     const bool dbg = c->s.debug != 0;
     const int T = c->gx * c->gy;
     float *acc = (float *)c->acc.p;  // [P][12], zeroed by the forward's k_preprocess
@@ -1384,6 +1430,7 @@ extern "C" int dgs_raster_backward(dgs_raster_ctx *c, const float *dL_dcolor, co
 
 extern "C" void dgs_raster_ctx_free(dgs_raster_ctx *c) {
     if (!c) return;
+    (void)resolve_count(c, c->last_stream);  // a deferred count nobody read (forward without backward)
     // Buffers stay allocated for reuse by the next forward on this device; a later acquirer waits
     // on this event (recorded on the stream that last used the buffers) before reuse.
     if (!c->released) (void)hipEventCreateWithFlags(&c->released, hipEventDisableTiming);
@@ -1398,6 +1445,10 @@ extern "C" void dgs_raster_ctx_free(dgs_raster_ctx *c) {
         delete c;
     }
 }
+
+extern "C" void dgs_raster_set_deferred_count(int on) { g_deferred.store(on ? 1 : 0); }
+
+extern "C" long long dgs_raster_deferred_overflows(void) { return g_deferred_overflows.load(); }
 
 extern "C" void dgs_debug_set_pair_cap(int device, int cap) {
     std::lock_guard<std::mutex> lk(g_cap_mu);

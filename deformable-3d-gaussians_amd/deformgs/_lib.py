@@ -51,6 +51,8 @@ _SIGS = {
     "dgs_debug_set_pair_cap": ([I, I], None),
     "dgs_debug_binning_redos": ([], ctypes.c_longlong),
     "dgs_debug_pair_cap": ([I], I),
+    "dgs_raster_set_deferred_count": ([I], None),
+    "dgs_raster_deferred_overflows": ([], ctypes.c_longlong),
     "dgs_debug_set_binning": ([I], None),
     "dgs_timing_enable": ([I], None),
     "dgs_timing_query": ([ctypes.c_char_p, ctypes.POINTER(I)], ctypes.c_double),

@@ -3,14 +3,49 @@ harness): deform -> render -> 0.8*L1 + 0.2*(1-SSIM) -> backward [-> grad all-red
 """
 import torch
 
+from . import _lib
 from .adam import step_all
 from .loss import l1_ssim_loss
 from .renderer import render
 
 
+_DEFER = {"before": 0}
+
+
 def forward_backward(gaussians, deform, cam, gt_image, pipe, background, is_6dof=False, lambda_dssim=0.2,
-                     warm=True, ast_noise=0.0):
-    """train_baseline.py:104-128 (timed span of the reference's iter_start/iter_end events)."""
+                     warm=True, ast_noise=0.0, deferred_count=False):
+    """train_baseline.py:104-128 (timed span of the reference's iter_start/iter_end events).
+
+    deferred_count: the rasterizer's forward does not wait for num_rendered (the host keeps issuing
+    the loss and the backward); if the speculative pair capacity overflowed, `deferred_overflowed()`
+    is True afterwards and the caller must redo the step with deferred_count=False after dropping
+    the gradients (`drop_grads`; bench.py). Single-rank only: with several ranks a redo must be
+    agreed on by every rank before the gradients are all-reduced."""
+    if not deferred_count:
+        return _forward_backward(gaussians, deform, cam, gt_image, pipe, background, is_6dof, lambda_dssim, warm,
+                                 ast_noise)
+    lib = _lib.load()
+    _DEFER["before"] = lib.dgs_raster_deferred_overflows()
+    lib.dgs_raster_set_deferred_count(1)
+    try:
+        return _forward_backward(gaussians, deform, cam, gt_image, pipe, background, is_6dof, lambda_dssim, warm,
+                                 ast_noise)
+    finally:
+        lib.dgs_raster_set_deferred_count(0)
+
+
+def deferred_overflowed():
+    """The last deferred_count step overflowed its speculative pair capacity (redo it)."""
+    return _lib.load().dgs_raster_deferred_overflows() != _DEFER["before"]
+
+
+def drop_grads(gaussians, deform):
+    """Gradients of a step that is being redone."""
+    gaussians.optimizer.zero_grad(set_to_none=True)
+    deform.optimizer.zero_grad(set_to_none=True)
+
+
+def _forward_backward(gaussians, deform, cam, gt_image, pipe, background, is_6dof, lambda_dssim, warm, ast_noise):
     if not warm:
         d_xyz, d_rotation, d_scaling = 0.0, 0.0, 0.0
     else:

@@ -99,6 +99,14 @@ int dgs_mark_visible(int P, const float *means3D, const float *viewmatrix, const
  * (count -> column scan -> place; the default where its LDS bound allows), 1 = duplicate + tile-key
  * radix sort + ranges (the scheme of the external upstream rasterizer's duplicateWithKeys / SortPairs /
  * identifyTileRanges, SURVEY.md section 3 kernel table). */
+/* Deferred pair count (training steps that can be redone): with it on, a speculative forward
+ * returns without waiting for num_rendered (*num_rendered = -1); the backward (or ctx_free) reads
+ * it. If it exceeded the speculative capacity the forward's image was computed on truncated tile
+ * lists: dgs_raster_deferred_overflows() counts these, and the caller must redo the step with the
+ * mode off (deformgs/train_step.py does). The backward of such a step stays in bounds. Off by
+ * default (the upstream op's synchronous num_rendered). */
+void dgs_raster_set_deferred_count(int on);
+long long dgs_raster_deferred_overflows(void);
 void dgs_debug_set_pair_cap(int device, int cap);
 int dgs_debug_pair_cap(int device);
 void dgs_debug_set_binning(int mode);

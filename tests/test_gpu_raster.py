@@ -268,3 +268,51 @@ def test_rect_binning_equals_sort_binning(case):
         np.testing.assert_array_equal(a, b)
     for k in gs:
         np.testing.assert_allclose(gr[k], gs[k], rtol=1e-5, atol=1e-6 * max(1.0, np.abs(gs[k]).max()))
+
+
+def test_deferred_count_redo_matches_sync(binning):
+    """Deferred pair count: a forced overflow (tiny speculative capacity) is detected at the
+    backward, counted, stays in bounds, and the redone step equals a synchronous step; without
+    overflow the deferred step equals the synchronous one outright."""
+    from deformgs import _lib
+    from deformgs.arguments import OptimizationParams, PipelineParams
+    from deformgs.deform_model import DeformModelBaseline
+    from deformgs.gaussian_model import GaussianModel
+    from deformgs.synthetic import synth_camera, synth_gaussians
+    from deformgs.train_step import deferred_overflowed, drop_grads, forward_backward
+    lib = _lib.load()
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    g = synth_gaussians(6000, seed=0, device=dev)
+    gs = GaussianModel(3)
+    gs.from_tensors(g["xyz"], g["features_dc"], g["features_rest"], g["scaling"], g["rotation"], g["opacity"])
+    gs.training_setup(OptimizationParams())
+    deform = DeformModelBaseline(is_blender=True, is_6dof=False, device=dev)
+    deform.train_setting(OptimizationParams())
+    cam = synth_camera(160, 128, index=2, fid=0.3, device=dev)
+    gt = torch.rand((3, 128, 160), device=dev)
+    params = [gs._xyz, gs._features_dc, gs._features_rest, gs._scaling, gs._rotation, gs._opacity] + \
+        list(deform.deform.parameters())
+
+    def run(deferred):
+        drop_grads(gs, deform)
+        loss, pkg = forward_backward(gs, deform, cam, gt, PipelineParams(), torch.zeros(3, device=dev),
+                                     deferred_count=deferred)
+        torch.cuda.synchronize()
+        return loss.item(), pkg["render"].detach().clone(), [p.grad.clone() for p in params]
+
+    ref = run(False)
+    # no overflow (capacity learned from the synchronous frame)
+    got = run(True)
+    assert not deferred_overflowed()
+    assert got[0] == ref[0] and torch.equal(got[1], ref[1])
+    for a, b in zip(got[2], ref[2]):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6 * max(1.0, b.abs().max().item()))
+    # forced overflow: detected, then the synchronous redo equals the reference
+    lib.dgs_debug_set_pair_cap(dev.index, 777)
+    run(True)
+    assert deferred_overflowed()
+    redo = run(False)
+    assert redo[0] == ref[0] and torch.equal(redo[1], ref[1])
+    for a, b in zip(redo[2], ref[2]):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6 * max(1.0, b.abs().max().item()))
