@@ -785,35 +785,34 @@ struct TGradArgs {
     int tin;
 };
 
-__global__ __launch_bounds__(256) void k_tgrad(TGradArgs a) {
-    __shared__ float S[32], gb[512];
+__global__ __launch_bounds__(1024) void k_tgrad(TGradArgs a) {
+    __shared__ float S[32], th[256];
     const int j = threadIdx.x;
-    gb[j] = a.gb0[j];
-    gb[256 + j] = a.gb5[j];
-    __syncthreads();
-    {  // S[k]: 8 lanes per k, each over 64 of the 512 (n, layer) terms, then a fixed xor tree
-        const int k = j >> 3, part = j & 7;
+    if (j < 256) th[j] = a.tc[TC_TH + j];
+    {  // S[k]: 32 lanes per k, each over 16 of the 512 (n, layer) terms, then a fixed xor tree
+        const int k = j >> 5, part = j & 31;
         float s = 0.f;
-#pragma unroll 8
-        for (int i = 0; i < 64; i++) {
-            const int n = part * 64 + i;  // n < 256: linear.0, else linear.5
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int n = part * 16 + i;  // n < 256: linear.0, else linear.5
             const float w = n < 256 ? a.fp[a.w0te + n * 32 + k] : a.fp[a.w5te + (n - 256) * 32 + k];
-            s = fmaf(w, gb[n], s);
+            const float gb = n < 256 ? a.gb0[n] : a.gb5[n - 256];
+            s = fmaf(w, gb, s);
         }
-        s += __shfl_xor(s, 1);
-        s += __shfl_xor(s, 2);
-        s += __shfl_xor(s, 4);
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) s += __shfl_xor(s, o);
         if (part == 0) S[k] = s;
     }
     __syncthreads();
-    const float th = a.tc[TC_TH + j];
-    float d = 0.f;
-    for (int k = 0; k < 30; k++) d = fmaf(a.fp[a.wT2 + k * 256 + j], S[k], d);
-    d = th > 0.f ? d : 0.f;
-    a.gT0b[j] = d;
-    for (int f = 0; f < a.tin; f++) a.gT0w[j * a.tin + f] = d * a.tc[TC_TIN + f];
-    for (int k = 0; k < 30; k++) a.gT2w[k * 256 + j] = S[k] * th;
+    for (int e = j; e < 30 * 256; e += 1024) a.gT2w[e] = S[e >> 8] * th[e & 255];
     if (j < 30) a.gT2b[j] = S[j];
+    if (j < 256) {
+        float d = 0.f;
+        for (int k = 0; k < 30; k++) d = fmaf(a.fp[a.wT2 + k * 256 + j], S[k], d);
+        d = th[j] > 0.f ? d : 0.f;
+        a.gT0b[j] = d;
+        for (int f = 0; f < a.tin; f++) a.gT0w[j * a.tin + f] = d * a.tc[TC_TIN + f];
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1771,7 +1770,7 @@ int backward(int flags, int N, const float *packed, const float *saved, const fl
     g.gb0 = grads[P.pLb[0]]; g.gb5 = grads[P.pLb[5]];
     g.gT0w = grads[P.pT0w]; g.gT0b = grads[P.pT0b]; g.gT2w = grads[P.pT2w]; g.gT2b = grads[P.pT2b];
     g.tin = F.tin;
-    hipLaunchKernelGGL(k_tgrad, dim3(1), dim3(256), 0, stream, g);
+    hipLaunchKernelGGL(k_tgrad, dim3(1), dim3(1024), 0, stream, g);
     DGS_LAUNCH_CHECK("k_tgrad", false, stream);
     return DGS_OK;
 }
