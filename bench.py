@@ -11,6 +11,7 @@ Run: python bench.py [--gpus N --steps K --warmup W]; N>1 under torch.distribute
 GPU, RCCL). Rank 0 prints ONE JSON line (value = whole-job iters/s = world * K / max-rank time).
 """
 import argparse
+import ctypes
 import json
 import math
 import os
@@ -54,6 +55,8 @@ def parse():
                          "~6 us of GPU idle on the launch stream (profiles/r2c trace), so the default times only the "
                          "roofline kernel (mlp_dw: the longest launch of the step, 2 records per step); 'major' adds "
                          "the other MFMA and blend classes, 'all' every class, 'none' nothing")
+    ap.add_argument("--6dof", dest="six_dof", action="store_true",
+                    help="6-DoF screw deformation head (config 4, trex --is_6dof) instead of d_xyz")
     ap.add_argument("--raw-init", action="store_true",
                     help="keep nn.Linear's default init on the deformation heads (the iteration-3000 transient: "
                          "deltas O(0.3) make every Gaussian hundreds of pixels wide)")
@@ -192,12 +195,15 @@ def main():
     opt = OptimizationParams()
     gaussians.training_setup(opt)
     torch.manual_seed(0)
-    deform = DeformModelBaseline(is_blender=True, is_6dof=False, device=dev)
+    six = args.six_dof
+    deform = DeformModelBaseline(is_blender=True, is_6dof=six, device=dev)
     if not args.raw_init:
         # steady-state training: the learned deltas are small (O(1e-3)); scale the random heads so the
         # rasterizer sees the Gaussians' own footprint, as in every iteration after the first few
+        net = deform.deform
+        heads = (net.branch_w, net.branch_v) if six else (net.gaussian_warp,)
         with torch.no_grad():
-            for head in (deform.deform.gaussian_warp, deform.deform.gaussian_rotation, deform.deform.gaussian_scaling):
+            for head in heads + (net.gaussian_rotation, net.gaussian_scaling):
                 head.weight.mul_(0.01)
                 head.bias.mul_(0.01)
     deform.train_setting(opt)
@@ -213,7 +219,7 @@ def main():
     with torch.no_grad():
         for cam in cams:
             d = deform.step(gaussians.get_xyz.detach(), cam.fid.unsqueeze(0).expand(N, -1))
-            img = render(cam, gaussians, pipe, bg, d[0], d[1], d[2])["render"]
+            img = render(cam, gaussians, pipe, bg, d[0], d[1], d[2], six)["render"]
             gts.append((img + 0.02 * torch.randn(img.shape, device=dev, generator=gen)).clamp_(0.0, 1.0))
     # Gaussian gradients are all-reduced during the MLP backward (their hooks fire first), the MLP's after
     allreduce = OverlappedGradAllReduce(
@@ -221,24 +227,28 @@ def main():
                  gaussians._rotation, gaussians._opacity],
         lambda: list(deform.deform.parameters()))
 
-    state = {"it": 3000, "P": 0, "redos": 0}
+    state = {"it": 3000, "P": 0, "redos": 0, "host_fb": 0.0, "host_opt": 0.0}
 
     def step(k):
         cam = cams[k % len(cams)]
         allreduce.arm()
+        h0 = time.perf_counter()
         # one rank: the rasterizer does not wait for the pair count (the host keeps issuing); a step
         # whose speculative pair capacity overflowed is redone synchronously. Several ranks: the
         # synchronous count (a redo there would have to be agreed on by every rank before the
         # overlapped all-reduce consumes the gradients)
-        loss, pkg = forward_backward(gaussians, deform, cam, gts[k % len(cams)], pipe, bg,
+        loss, pkg = forward_backward(gaussians, deform, cam, gts[k % len(cams)], pipe, bg, six,
                                      deferred_count=(world == 1 and not SYNC_COUNT))
         if world == 1 and deferred_overflowed():
             state["redos"] += 1
             drop_grads(gaussians, deform)
-            loss, pkg = forward_backward(gaussians, deform, cam, gts[k % len(cams)], pipe, bg)
+            loss, pkg = forward_backward(gaussians, deform, cam, gts[k % len(cams)], pipe, bg, six)
         allreduce()
+        h1 = time.perf_counter()
         if not args.no_adam:
             optimizer_step(gaussians, deform, state["it"])
+        state["host_fb"] += h1 - h0
+        state["host_opt"] += time.perf_counter() - h1
         state["it"] += 1
 
     for k in range(args.warmup):
@@ -251,6 +261,9 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    state["host_fb"] = state["host_opt"] = 0.0
+    waits = ctypes.c_longlong(0)
+    wait0 = lib.dgs_debug_count_wait_ns(waits)
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(k)
@@ -258,6 +271,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    wait_ms = (lib.dgs_debug_count_wait_ns(waits) - wait0) / 1e6
     lib.dgs_timing_enable(0)
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -269,7 +283,7 @@ def main():
         d = deform.step(gaussians.get_xyz.detach(), cams[0].fid.unsqueeze(0).expand(N, -1))
     import diff_gaussian_rasterization as dgr
     # count pairs: rerun one forward through the autograd function to read ctx.num_rendered
-    pk = render(cams[0], gaussians, pipe, bg, d[0], d[1], d[2])
+    pk = render(cams[0], gaussians, pipe, bg, d[0], d[1], d[2], six)
     P_pairs = int(pk["render"].grad_fn.num_rendered) if hasattr(pk["render"].grad_fn, "num_rendered") else 0
     del pk
     pair_cap = int(lib.dgs_debug_pair_cap(local))  # the speculative capacity the sort-path loops cover
@@ -320,13 +334,18 @@ def main():
         "value": value, "unit": "iters/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "fp32", "data": "synthetic (synth-100k, random-init weights, targets = initial renders + noise)",
-        "config": {"workload": f"synth-100k: {N} Gaussians, {R}x{R}, blender DeformNetworkBaseline, SH3"
+        "config": {"workload": f"synth-100k: {N} Gaussians, {R}x{R}, blender DeformNetworkBaseline"
+                   + (" (6-DoF screw head)" if six else "") + ", SH3"
                    + (" (raw-init heads)" if args.raw_init else " (heads at 1/100 init: steady-state deltas)"),
                    "global_batch": world, "includes_adam": not args.no_adam, "pairs_per_render": P_pairs,
                    "pair_capacity": pair_cap, "redone_steps": state["redos"],
                    "parallelism": f"dp{world} (frame-parallel, RCCL grad all-reduce)"},
         "roofline": roofline,
         "kernels_ms_per_step": {k: v[0] / args.steps for k, v in kernels.items()},
+        # host time per step: issuing forward + backward (including the wait for the pair count
+        # inside it) and the optimizer step; a count wait near 0 means the host, not the GPU, paced it
+        "host_ms_per_step": {"fwd_bwd": state["host_fb"] / args.steps * 1e3, "count_wait": wait_ms / args.steps,
+                             "optimizer": state["host_opt"] / args.steps * 1e3},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -21,6 +21,8 @@
 //                  added with 3 four-lane atomics per (wave, Gaussian)
 //   k_preprocess_bwd 1 thread / Gaussian: conic->Sigma2D->(Sigma3D, mean), projection, SH, Sigma3D->(s,q)
 #include <hip/hip_runtime.h>
+
+#include <chrono>
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -1054,7 +1056,18 @@ dgs_raster_ctx *ctx_acquire(int device, hipStream_t stream) {
 // the word (no event record in the stream: one costs ~6 us of GPU idle); the stream is queried
 // every 1024 polls so a failed launch cannot spin forever.
 constexpr uint32_t COUNT_PENDING = 0xffffffffu;
+std::atomic<long long> g_count_wait_ns{0}, g_count_waits{0};  // host time spent waiting for num_rendered
+
+static int wait_count_impl(dgs_raster_ctx *c, hipStream_t stream, int &nr);
 static int wait_count(dgs_raster_ctx *c, hipStream_t stream, int &nr) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const int rc = wait_count_impl(c, stream, nr);
+    g_count_wait_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    g_count_waits++;
+    return rc;
+}
+
+static int wait_count_impl(dgs_raster_ctx *c, hipStream_t stream, int &nr) {
     if (!c->rect_mode) {
         DGS_HIP_CHECK(hipEventSynchronize(c->count_ev));
         nr = (int)*c->h_total;
@@ -1458,6 +1471,11 @@ extern "C" void dgs_debug_set_pair_cap(int device, int cap) {
 extern "C" int dgs_debug_pair_cap(int device) { return pair_cap_get(device); }
 
 extern "C" void dgs_debug_set_binning(int mode) { g_binning.store(mode == 1 ? 1 : 0); }
+
+extern "C" long long dgs_debug_count_wait_ns(long long *waits) {
+    if (waits) *waits = g_count_waits.load();
+    return g_count_wait_ns.load();
+}
 
 extern "C" long long dgs_debug_binning_redos(void) {
     std::lock_guard<std::mutex> lk(g_cap_mu);

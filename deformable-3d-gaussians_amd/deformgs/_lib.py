@@ -50,6 +50,7 @@ _SIGS = {
     "dgs_mark_visible": ([I, P, P, P, P, P], I),
     "dgs_debug_set_pair_cap": ([I, I], None),
     "dgs_debug_binning_redos": ([], ctypes.c_longlong),
+    "dgs_debug_count_wait_ns": ([ctypes.POINTER(ctypes.c_longlong)], ctypes.c_longlong),
     "dgs_debug_pair_cap": ([I], I),
     "dgs_raster_set_deferred_count": ([I], None),
     "dgs_raster_deferred_overflows": ([], ctypes.c_longlong),
@@ -74,6 +75,10 @@ _SIGS = {
     "dgs_select_rows": ([I, P, I, ctypes.POINTER(RowJob), P], I),
     "dgs_gaussian_inputs_forward": ([I, I] + [P] * 7 + [I] + [P] * 5 + [P], I),
     "dgs_gaussian_inputs_backward": ([I, I] + [P] * 15 + [I, P], I),
+    "dgs_gaussian_inputs_se3_forward": ([I, I] + [P] * 7 + [I] + [P] * 5 + [P], I),
+    "dgs_gaussian_inputs_se3_backward": ([I, I, P, P, I] + [P] * 15 + [P], I),
+    "dgs_se3_forward": ([I, P, I, P, P], I),
+    "dgs_se3_backward": ([I, P, I, P, P, I, P], I),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -14,13 +14,16 @@ import torch
 import torch.nn as nn
 
 from . import _lib
-from .rigid import screw_from_raw
 
 FLAG_BLENDER = 1
 FLAG_6DOF = 2
 FLAG_NO_ROTSCALE = 4
 FLAG_EXACT_FP32 = 8  # v_mfma_f32_32x32x2_f32 kernels instead of the split-bf16 (bf16x6) default
 FLAG_UNIFORM_T = 16  # every point carries t[0] (set when t is one value or a stride-0 expand)
+
+
+# DGS_SE3_GLUE=1 (A/B diagnostic): render() applies the 6-DoF matrices with the reference's torch glue
+_SE3_GLUE = os.environ.get("DGS_SE3_GLUE", "0") not in ("", "0")
 
 
 def _exact_default():
@@ -69,6 +72,34 @@ class _FusedDeformMLP(torch.autograd.Function):
                                      _lib.ptr_array(grads), _lib.stream_ptr(dev))
         _lib.check(rc, "deform_backward")
         return (None, None, None, *grads)
+
+
+class _ScrewSE3(torch.autograd.Function):
+    """Raw screw head (w_r, v_r) -> d_xyz (N, 4, 4) = rp_to_se3(exp_se3(...)) (utils/time_utils.py:114-121,
+    utils/rigid_utils.py:4-83) in one HIP launch each way (dgs_se3_*); rigid.screw_from_raw is the torch
+    statement of the same map."""
+
+    @staticmethod
+    def forward(ctx, wv):
+        lib = _lib.load()
+        N = wv.shape[0]
+        assert wv.dim() == 2 and wv.shape[1] == 6 and wv.stride(1) == 1 and wv.dtype == torch.float32
+        M = torch.empty((N, 4, 4), dtype=torch.float32, device=wv.device)
+        _lib.check(lib.dgs_se3_forward(N, _lib.ptr(wv), wv.stride(0), _lib.ptr(M), _lib.stream_ptr(wv.device)),
+                   "se3_forward")
+        ctx.save_for_backward(wv)
+        return M
+
+    @staticmethod
+    def backward(ctx, dM):
+        lib = _lib.load()
+        (wv,) = ctx.saved_tensors
+        N = wv.shape[0]
+        g = torch.empty((N, 6), dtype=torch.float32, device=wv.device)
+        dM = dM.contiguous().float()
+        _lib.check(lib.dgs_se3_backward(N, _lib.ptr(wv), wv.stride(0), _lib.ptr(dM), _lib.ptr(g), 6,
+                                        _lib.stream_ptr(wv.device)), "se3_backward")
+        return g
 
 
 class _DeformBase(nn.Module):
@@ -153,7 +184,11 @@ class _DeformBase(nn.Module):
     def forward(self, x, t):
         out = self.raw(x, t)
         if self.is_6dof:
-            d_xyz = screw_from_raw(out[:, 0:3], out[:, 3:6])
+            d_xyz = _ScrewSE3.apply(out[:, 0:6])
+            # render(..., is_6dof=True) recognises this and applies the screw to xyz inside its own input
+            # launch (dgs_gaussian_inputs_se3_*), reading the raw rows instead of the (N, 4, 4) matrices
+            if not _SE3_GLUE:
+                d_xyz._dgs_se3_raw = out
             rot, scale = out[:, 6:10], out[:, 10:13]
         else:
             d_xyz = out[:, 0:3]

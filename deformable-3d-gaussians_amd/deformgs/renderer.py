@@ -23,7 +23,7 @@ class _GaussianInputs(torch.autograd.Function):
     (means3D, shs, opacities, scales, rotations) of gaussian_renderer/__init__.py:70-112."""
 
     @staticmethod
-    def forward(ctx, xyz, f_dc, f_rest, scaling, rotation, opacity, deform):
+    def forward(ctx, xyz, f_dc, f_rest, scaling, rotation, opacity, deform, se3=False):
         lib = _lib.load()
         P = xyz.shape[0]
         M_rest = f_rest.shape[1]
@@ -31,19 +31,24 @@ class _GaussianInputs(torch.autograd.Function):
         e = lambda *shape: torch.empty(shape, dtype=torch.float32, device=dev)  # noqa: E731
         means3D, shs, scales, rots, opac = e(P, 3), e(P, 1 + M_rest, 3), e(P, 3), e(P, 4), e(P, 1)
         ds = deform.stride(0) if deform is not None else 0
-        _lib.check(lib.dgs_gaussian_inputs_forward(
+        fwd = lib.dgs_gaussian_inputs_se3_forward if se3 else lib.dgs_gaussian_inputs_forward
+        _lib.check(fwd(
             P, M_rest, _lib.ptr(xyz), _lib.ptr(f_dc), _lib.ptr(f_rest), _lib.ptr(scaling), _lib.ptr(rotation),
             _lib.ptr(opacity), _lib.ptr(deform), ds, _lib.ptr(means3D), _lib.ptr(shs), _lib.ptr(scales),
             _lib.ptr(rots), _lib.ptr(opac), _lib.stream_ptr(dev)), "gaussian_inputs_forward")
-        ctx.save_for_backward(scaling, rotation, opacity)
+        if se3:  # the screw rows and xyz are read again by the backward
+            ctx.save_for_backward(scaling, rotation, opacity, xyz, deform)
+        else:
+            ctx.save_for_backward(scaling, rotation, opacity)
         ctx.M_rest = M_rest
         ctx.has_deform = deform is not None
+        ctx.se3 = se3
         return means3D, shs, opac, scales, rots
 
     @staticmethod
     def backward(ctx, g_means, g_shs, g_opac, g_scales, g_rots):
         lib = _lib.load()
-        scaling, rotation, opacity = ctx.saved_tensors
+        scaling, rotation, opacity = ctx.saved_tensors[:3]
         P, M_rest = scaling.shape[0], ctx.M_rest
         dev = scaling.device
         z = lambda t, *shape: (torch.zeros(shape, dtype=torch.float32, device=dev) if t is None  # noqa: E731
@@ -54,13 +59,22 @@ class _GaussianInputs(torch.autograd.Function):
         e = lambda ok, *shape: torch.empty(shape, dtype=torch.float32, device=dev) if ok else None  # noqa: E731
         o_xyz, o_dc, o_rest = e(need[0], P, 3), e(need[1], P, 1, 3), e(need[2], P, M_rest, 3)
         o_sc, o_rot, o_op = e(need[3], P, 3), e(need[4], P, 4), e(need[5], P, 1)
+        if ctx.se3:
+            xyz, deform = ctx.saved_tensors[3:]
+            o_def = e(need[6], P, deform.shape[1])
+            _lib.check(lib.dgs_gaussian_inputs_se3_backward(
+                P, M_rest, _lib.ptr(xyz), _lib.ptr(deform), deform.stride(0), _lib.ptr(scaling), _lib.ptr(rotation),
+                _lib.ptr(opacity), _lib.ptr(g_means), _lib.ptr(g_shs), _lib.ptr(g_scales), _lib.ptr(g_rots),
+                _lib.ptr(g_opac), _lib.ptr(o_xyz), _lib.ptr(o_dc), _lib.ptr(o_rest), _lib.ptr(o_sc), _lib.ptr(o_rot),
+                _lib.ptr(o_op), _lib.ptr(o_def), _lib.stream_ptr(dev)), "gaussian_inputs_se3_backward")
+            return o_xyz, o_dc, o_rest, o_sc, o_rot, o_op, o_def, None
         o_def = e(ctx.has_deform and need[6], P, 10)
         _lib.check(lib.dgs_gaussian_inputs_backward(
             P, M_rest, _lib.ptr(scaling), _lib.ptr(rotation), _lib.ptr(opacity), _lib.ptr(g_means), _lib.ptr(g_shs),
             _lib.ptr(g_scales), _lib.ptr(g_rots), _lib.ptr(g_opac), _lib.ptr(o_xyz), _lib.ptr(o_dc), _lib.ptr(o_rest),
             _lib.ptr(o_sc), _lib.ptr(o_rot), _lib.ptr(o_op), _lib.ptr(o_def), 10, _lib.stream_ptr(dev)),
             "gaussian_inputs_backward")
-        return o_xyz, o_dc, o_rest, o_sc, o_rot, o_op, o_def
+        return o_xyz, o_dc, o_rest, o_sc, o_rot, o_op, o_def, None
 
 
 def _fused_deform_rows(pc, d_xyz, d_rotation, d_scaling):
@@ -79,6 +93,25 @@ def _fused_deform_rows(pc, d_xyz, d_rotation, d_scaling):
     off = b.storage_offset()
     for t, col, w in ((d_xyz, 0, 3), (d_rotation, 3, 4), (d_scaling, 7, 3)):
         if tuple(t.shape) != (N, w) or t.stride() != (10, 1) or t.storage_offset() - off != col:
+            return None
+    return b
+
+
+def _fused_se3_rows(pc, d_xyz, d_rotation, d_scaling):
+    """The (N, 13) raw 6-DoF deformation output [w_r v_r d_rot d_scale] behind d_xyz (the (N, 4, 4)
+    screw matrices DeformNetwork returns, tagged with their source) when d_rotation / d_scaling are
+    its column views, else None (then the generic torch glue runs on the matrices)."""
+    b = getattr(d_xyz, "_dgs_se3_raw", None) if torch.is_tensor(d_xyz) else None
+    if b is None or not (torch.is_tensor(d_rotation) and torch.is_tensor(d_scaling)):
+        return None
+    if d_rotation._base is not b or d_scaling._base is not b:
+        return None
+    N = pc._xyz.shape[0]
+    if b.dim() != 2 or tuple(b.shape) != (N, 13) or not b.is_contiguous() or b.dtype != torch.float32:
+        return None
+    off = b.storage_offset()
+    for t, col, w in ((d_rotation, 6, 4), (d_scaling, 10, 3)):
+        if tuple(t.shape) != (N, w) or t.stride() != (13, 1) or t.storage_offset() - off != col:
             return None
     return b
 
@@ -108,14 +141,20 @@ def render(viewpoint_camera, pc, pipe, bg_color, d_xyz, d_rotation, d_scaling, i
         sh_degree=pc.active_sh_degree, campos=viewpoint_camera.camera_center, prefiltered=False,
         debug=getattr(pipe, "debug", False))
     rasterizer = GaussianRasterizer(raster_settings=raster_settings)
-    rows = None
-    if (not direct_compute and not is_6dof and override_color is None and not getattr(pipe, "compute_cov3D_python", False)
+    rows, se3 = None, False
+    if (not direct_compute and override_color is None and not getattr(pipe, "compute_cov3D_python", False)
             and not getattr(pipe, "convert_SHs_python", False) and _fused_ok(pc)):
-        rows = _fused_deform_rows(pc, d_xyz, d_rotation, d_scaling)
+        if not is_6dof:
+            rows = _fused_deform_rows(pc, d_xyz, d_rotation, d_scaling)
+        elif not torch.is_tensor(d_xyz):  # 6-DoF warm-up: means3D = xyz (no screw yet)
+            rows = _fused_deform_rows(pc, 0.0, d_rotation, d_scaling)
+        else:
+            rows = _fused_se3_rows(pc, d_xyz, d_rotation, d_scaling)
+            se3 = rows is not None
     if rows is not None:
         means3D, shs, opacity, scales, rotations = _GaussianInputs.apply(
             pc._xyz, pc._features_dc, pc._features_rest, pc._scaling, pc._rotation, pc._opacity,
-            rows if torch.is_tensor(rows) else None)
+            rows if torch.is_tensor(rows) else None, se3)
         rendered_image, radii, depth = rasterizer(
             means3D=means3D, means2D=screenspace_points, means2D_densify=screenspace_points_densify, shs=shs,
             colors_precomp=None, opacities=opacity, scales=scales, rotations=rotations, cov3D_precomp=None)

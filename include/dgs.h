@@ -20,7 +20,8 @@
  *   dgs_l1_ssim_*        <- l1_loss + ssim (utils/loss_utils.py:18-73) as used at train_baseline.py:126-127
  *   dgs_gaussian_inputs_* <- the glue of render() (gaussian_renderer/__init__.py:70-112: xyz + d_xyz,
  *                           exp(scaling) + d_scaling, normalize(rotation) + d_rotation, sigmoid(opacity),
- *                           cat(features_dc, features_rest)) and its autograd
+ *                           cat(features_dc, features_rest)) and its autograd; *_se3_* and dgs_se3_*
+ *                           the 6-DoF branch (gaussian_renderer/__init__.py:71-76, utils/rigid_utils.py)
  *   dgs_adam_step        <- torch.optim.Adam(..., eps=1e-15).step() of scene/gaussian_model.py:132 and
  *                           scene/deform_model.py:266 (train_baseline.py:176-182)
  */
@@ -111,6 +112,8 @@ void dgs_debug_set_pair_cap(int device, int cap);
 int dgs_debug_pair_cap(int device);
 void dgs_debug_set_binning(int mode);
 long long dgs_debug_binning_redos(void);
+/* host nanoseconds spent waiting for num_rendered (and the number of waits) since process start */
+long long dgs_debug_count_wait_ns(long long *waits);
 
 /* ---- timing hooks (bench.py): per-kernel-class HIP event accumulation on the launch stream ---- */
 void dgs_timing_enable(int on);
@@ -183,6 +186,27 @@ int dgs_gaussian_inputs_backward(int P, int M_rest, const float *scaling, const 
                                  const float *d_scales, const float *d_rotations, const float *d_opacities,
                                  float *g_xyz, float *g_dc, float *g_rest, float *g_scaling, float *g_rotation,
                                  float *g_opacity, float *g_deform, int deform_stride, void *stream);
+/* 6-DoF variant (render(..., is_6dof=True), gaussian_renderer/__init__.py:71-76 with the screw head of
+ * utils/time_utils.py:114-121 and exp_se3 of utils/rigid_utils.py:4-83 in the same launch): deform rows
+ * (deform_stride >= 13, required) hold [w_r(3) v_r(3) d_rotation(4) d_scaling(3)], the raw head
+ * outputs; theta = |w_r|, w = w_r/theta + 1e-5, v = v_r/theta + 1e-5, (R, p) = exp_se3(w, v, theta),
+ * means3D = R xyz + p. Backward also needs xyz and the deform rows; g_deform uses deform_stride. */
+int dgs_gaussian_inputs_se3_forward(int P, int M_rest, const float *xyz, const float *f_dc, const float *f_rest,
+                                    const float *scaling, const float *rotation, const float *opacity,
+                                    const float *deform, int deform_stride, float *means3D, float *shs,
+                                    float *scales, float *rotations, float *opacities, void *stream);
+int dgs_gaussian_inputs_se3_backward(int P, int M_rest, const float *xyz, const float *deform, int deform_stride,
+                                     const float *scaling, const float *rotation, const float *opacity,
+                                     const float *d_means3D, const float *d_shs, const float *d_scales,
+                                     const float *d_rotations, const float *d_opacities, float *g_xyz, float *g_dc,
+                                     float *g_rest, float *g_scaling, float *g_rotation, float *g_opacity,
+                                     float *g_deform, void *stream);
+/* exp_se3 of the raw screw head -> M (P, 4, 4) = rp_to_se3(R, p) (the d_xyz DeformNetwork returns for
+ * is_6dof, utils/time_utils.py:114-121 / utils/rigid_utils.py:27-35), and its backward: dM (P, 4, 4)
+ * -> g_raw columns 0..5 (rows of g_stride floats); M's constant last row passes no gradient. */
+int dgs_se3_forward(int P, const float *raw, int raw_stride, float *M, void *stream);
+int dgs_se3_backward(int P, const float *raw, int raw_stride, const float *dM, float *g_raw, int g_stride,
+                     void *stream);
 
 /* ---- Adam over many tensors in one launch (torch.optim.Adam, amsgrad/weight_decay off) ----
  * Per tensor (host array of n descriptors, device data pointers):

@@ -61,3 +61,65 @@ def test_fused_inputs_match_torch_glue(warm):
             continue
         scale = y.abs().max().clamp_min(1e-12)
         assert ((x - y).abs().max() / scale) < 2e-4, n
+
+
+def _raw13(n, seed, dev):
+    """(n, 13) raw 6-DoF head rows [w_r v_r d_rot d_scale] of the magnitudes a trained network emits."""
+    gen = torch.Generator(device="cpu").manual_seed(seed)
+    w = torch.randn(n, 3, generator=gen) * 0.3
+    v = torch.randn(n, 3, generator=gen) * 0.01
+    rs = torch.randn(n, 7, generator=gen) * 0.01
+    return torch.cat([w, v, rs], 1).to(dev).requires_grad_(True)
+
+
+@pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")
+def test_se3_matrices_match_rigid_utils():
+    """dgs_se3_*: exp_se3 of the screw head (utils/time_utils.py:114-121, rigid_utils.py:4-83) and its
+    gradient vs the torch statement (deformgs/rigid.py) in float64 on the CPU. Tolerance: values 2e-6
+    absolute (|M| <= ~2), gradients 1e-4 of the tensor's max."""
+    from deformgs.deform_network import _ScrewSE3
+    from deformgs.rigid import screw_from_raw
+    raw = _raw13(5000, 3, "cuda")
+    M = _ScrewSE3.apply(raw[:, 0:6])
+    r64 = raw.detach().cpu().double().requires_grad_(True)
+    M64 = screw_from_raw(r64[:, 0:3], r64[:, 3:6])
+    assert (M.detach().cpu().double() - M64.detach()).abs().max() < 2e-6
+    gM = torch.randn(5000, 4, 4, generator=torch.Generator().manual_seed(4))
+    (M * gM.cuda()).sum().backward()
+    (M64 * gM.double()).sum().backward()
+    g, g64 = raw.grad.cpu().double(), r64.grad
+    assert torch.count_nonzero(g[:, 6:]) == 0
+    err = (g[:, :6] - g64[:, :6]).abs().max() / g64[:, :6].abs().max()
+    assert err < 1e-4, err
+
+
+@pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")
+def test_fused_se3_inputs_match_torch_glue():
+    """render(..., is_6dof=True): the screw applied inside the input launch (dgs_gaussian_inputs_se3_*)
+    vs the reference's glue (bmm of the (N, 4, 4) torch screw with homogeneous xyz,
+    gaussian_renderer/__init__.py:71-76) — images, radii and every gradient, the raw head's included."""
+    from deformgs import renderer
+    from deformgs.deform_network import _ScrewSE3
+    from deformgs.rigid import screw_from_raw
+    gm, cam, pipe, _ = _setup(6)
+    raw = _raw13(3000, 6, "cuda")
+    bg = torch.tensor([0.1, 0.2, 0.3], device="cuda")
+    gt = torch.rand(3, 128, 160, device="cuda")
+    dx = _ScrewSE3.apply(raw[:, 0:6])
+    dx._dgs_se3_raw = raw
+    dr, ds = raw[:, 6:10], raw[:, 10:13]
+    assert renderer._fused_se3_rows(gm, dx, dr, ds) is raw
+    a = renderer.render(cam, gm, pipe, bg, dx, dr, ds, is_6dof=True)
+    ga = _grads(gm, raw, a, gt)
+    cx = screw_from_raw(raw[:, 0:3], raw[:, 3:6])
+    assert renderer._fused_se3_rows(gm, cx, dr, ds) is None
+    b = renderer.render(cam, gm, pipe, bg, cx, raw[:, 6:10] * 1.0, raw[:, 10:13] * 1.0, is_6dof=True)
+    gb = _grads(gm, raw, b, gt)
+    assert a["radii"].gt(0).sum() > 500
+    torch.testing.assert_close(a["render"], b["render"], rtol=1e-4, atol=1e-5)
+    assert (a["radii"] != b["radii"]).float().mean() < 1e-3
+    names = ["xyz", "f_dc", "f_rest", "scaling", "rotation", "opacity", "raw"]
+    for n, x, y in zip(names, ga, gb):
+        scale = y.abs().max().clamp_min(1e-12)
+        frac_ok = (((x - y).abs() / scale) < 2e-3).float().mean()
+        assert frac_ok > 0.999, (n, frac_ok)
