@@ -37,24 +37,52 @@ struct Jobs {
     float omb1, b2, omb2, eps;  // 1 - beta1, beta2, 1 - beta2 (differences taken in double, as torch)
 };
 
+__device__ __forceinline__ void adam1(float &p, float g, float &m, float &v, float c1, float b2, float c2, float eps,
+                                      float step_size, float bc2_sqrt) {
+    m = m + c1 * (g - m);
+    v = v * b2 + c2 * (g * g);
+    const float denom = sqrtf(v) / bc2_sqrt + eps;
+    p = p + (-step_size) * (m / denom);
+}
+
+// Each thread updates PER_THREAD / 4 float4 units (16-byte loads and stores of p, g, m, v) when the
+// tensor's four pointers are 16-byte aligned; otherwise (or for a ragged tail) element by element.
+// Same arithmetic per element either way.
 __global__ __launch_bounds__(THREADS) void k_adam(Jobs J) {
     const long long b = blockIdx.x;
     int q = 0;
     for (int k = 1; k < J.n; k++)  // uniform scan of the kernel-argument table
         if (b >= J.j[k].block0) q = k;
     const Job &T = J.j[q];
-    const long long base = (b - T.block0) * BLOCK_ELEMS + threadIdx.x;
-    const float c1 = J.omb1, c2 = J.omb2;
+    const float c1 = J.omb1, c2 = J.omb2, b2 = J.b2, eps = J.eps, ss = T.step_size, bc = T.bc2_sqrt;
+    const bool vec = ((reinterpret_cast<uintptr_t>(T.p) | reinterpret_cast<uintptr_t>(T.g) |
+                       reinterpret_cast<uintptr_t>(T.m) | reinterpret_cast<uintptr_t>(T.v)) & 15) == 0;
+    const long long e0 = (b - T.block0) * BLOCK_ELEMS;
+    if (vec && e0 + BLOCK_ELEMS <= T.n) {
+#pragma unroll
+        for (int k = 0; k < PER_THREAD / 4; k++) {
+            const long long i = e0 + 4ll * (threadIdx.x + k * THREADS);
+            float4 p = *reinterpret_cast<const float4 *>(T.p + i);
+            const float4 g = *reinterpret_cast<const float4 *>(T.g + i);
+            float4 m = *reinterpret_cast<const float4 *>(T.m + i);
+            float4 v = *reinterpret_cast<const float4 *>(T.v + i);
+            adam1(p.x, g.x, m.x, v.x, c1, b2, c2, eps, ss, bc);
+            adam1(p.y, g.y, m.y, v.y, c1, b2, c2, eps, ss, bc);
+            adam1(p.z, g.z, m.z, v.z, c1, b2, c2, eps, ss, bc);
+            adam1(p.w, g.w, m.w, v.w, c1, b2, c2, eps, ss, bc);
+            *reinterpret_cast<float4 *>(T.p + i) = p;
+            *reinterpret_cast<float4 *>(T.m + i) = m;
+            *reinterpret_cast<float4 *>(T.v + i) = v;
+        }
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < PER_THREAD; k++) {
-        const long long i = base + (long long)k * THREADS;
+        const long long i = e0 + threadIdx.x + (long long)k * THREADS;
         if (i < T.n) {
-            const float g = T.g[i];
-            float m = T.m[i], v = T.v[i];
-            m = m + c1 * (g - m);
-            v = v * J.b2 + c2 * (g * g);
-            const float denom = sqrtf(v) / T.bc2_sqrt + J.eps;
-            T.p[i] = T.p[i] + (-T.step_size) * (m / denom);
+            float p = T.p[i], m = T.m[i], v = T.v[i];
+            adam1(p, T.g[i], m, v, c1, b2, c2, eps, ss, bc);
+            T.p[i] = p;
             T.m[i] = m;
             T.v[i] = v;
         }

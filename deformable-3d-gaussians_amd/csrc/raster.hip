@@ -41,6 +41,10 @@ namespace dgs {
 // ------------------------------------------------------------------------------------------------
 // forward kernels
 // ------------------------------------------------------------------------------------------------
+// STAGE (M = 16, 16-byte aligned SH): the block's SH rows are read into LDS with coalesced
+// 16-byte loads before any thread culls its Gaussian (see k_preprocess_bwd)
+constexpr int SH_ROW = 48, SH_PAD = 49;  // odd LDS row stride: a thread-per-row access is conflict-free
+template <bool STAGE>
 __global__ __launch_bounds__(256) void k_preprocess(
     int P, int D, int M, const float *__restrict__ means3D, const float *__restrict__ scales, float mod,
     const float *__restrict__ rots, const float *__restrict__ cov_pre, const float *__restrict__ opac,
@@ -50,6 +54,19 @@ __global__ __launch_bounds__(256) void k_preprocess(
     float4 *__restrict__ rgbd, uint32_t *__restrict__ tiles, uint8_t *__restrict__ clamped,
     uint32_t *__restrict__ dkey, uint32_t *__restrict__ gid, float4 *__restrict__ acc) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
+    [[maybe_unused]] const float *s_row = nullptr;
+    if constexpr (STAGE) {
+        __shared__ float s_sh[256 * SH_PAD];
+        const int b0 = blockIdx.x * blockDim.x, nrow = min(256, P - b0);
+        const float4 *src = reinterpret_cast<const float4 *>(shs + (size_t)b0 * SH_ROW);
+        for (int u = threadIdx.x; u < nrow * (SH_ROW / 4); u += 256) {
+            const float4 v = src[u];
+            float *d = s_sh + (u / (SH_ROW / 4)) * SH_PAD + (u % (SH_ROW / 4)) * 4;
+            d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+        }
+        __syncthreads();
+        s_row = s_sh + threadIdx.x * SH_PAD;
+    }
     if (i >= P) return;
     // zero this Gaussian's backward accumulator row (the blend backward adds into it): no memset
     // launch in the backward
@@ -99,7 +116,7 @@ __global__ __launch_bounds__(256) void k_preprocess(
         float dx = p.x - cam.c[0], dy = p.y - cam.c[1], dz = p.z - cam.c[2];
         float n = sqrtf(dx * dx + dy * dy + dz * dz);
         float x = dx / n, y = dy / n, z = dz / n;
-        const float *sh = shs + (size_t)i * M * 3;
+        const float *sh = STAGE ? s_row : shs + (size_t)i * M * 3;
         float r[3];
 #pragma unroll
         for (int c = 0; c < 3; c++) {
@@ -617,6 +634,22 @@ __device__ inline void dR_dq(float4 q, const float dR[9], float4 &dq) {
     dq.w = 2.f * (-r * dR[1] + x * dR[2] + r * dR[3] + y * dR[5] + x * dR[6] + y * dR[7]) - 4.f * z * (dR[0] + dR[4]);
 }
 
+// STAGE (degree-3 SH rows, M = 16, 16-byte aligned tensors): the block's SH rows (contiguous in
+// HBM) are read into LDS with coalesced 16-byte loads, and its SH gradient rows are written back the
+// same way (one thread per Gaussian would otherwise store 48 scattered words per row: 3x the HBM
+// write traffic in partial lines).
+template <bool STAGE>
+__device__ __forceinline__ void preprocess_bwd_one(
+    int i, int D, int M, const float *__restrict__ means3D, const float *__restrict__ scales, float mod,
+    const float *__restrict__ rots, const float *__restrict__ cov_pre, const float *__restrict__ shs,
+    const float *view, const float *proj, const float *campos, int W, int H, float tanx, float tany,
+    float fx, float fy, const int *__restrict__ radii, const uint8_t *__restrict__ clamped,
+    const float *__restrict__ acc, float *__restrict__ dL_dmeans3D, float *__restrict__ dL_dmeans2D,
+    float *__restrict__ dL_ddens, float *__restrict__ dL_dcolors, float *__restrict__ dL_dopac,
+    float *__restrict__ dL_dcov3D, float *__restrict__ dL_dshs, float *__restrict__ dL_dscales,
+    float *__restrict__ dL_drots, float *s_row);
+
+template <bool STAGE>
 __global__ __launch_bounds__(256) void k_preprocess_bwd(
     int P, int D, int M, const float *__restrict__ means3D, const float *__restrict__ scales, float mod,
     const float *__restrict__ rots, const float *__restrict__ cov_pre, const float *__restrict__ shs,
@@ -626,8 +659,46 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(
     float *__restrict__ dL_ddens, float *__restrict__ dL_dcolors, float *__restrict__ dL_dopac,
     float *__restrict__ dL_dcov3D, float *__restrict__ dL_dshs, float *__restrict__ dL_dscales,
     float *__restrict__ dL_drots) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P) return;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    [[maybe_unused]] const int b0 = blockIdx.x * blockDim.x, nrow = min(256, P - b0);
+    [[maybe_unused]] float *s_row = nullptr;
+    if constexpr (STAGE) {
+        __shared__ float s_sh[256 * SH_PAD];
+        s_row = s_sh + threadIdx.x * SH_PAD;
+        const float4 *src = reinterpret_cast<const float4 *>(shs + (size_t)b0 * SH_ROW);
+        for (int u = threadIdx.x; u < nrow * (SH_ROW / 4); u += 256) {
+            const float4 v = src[u];
+            float *d = s_sh + (u / (SH_ROW / 4)) * SH_PAD + (u % (SH_ROW / 4)) * 4;
+            d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+        }
+        __syncthreads();
+        if (i < P) preprocess_bwd_one<STAGE>(i, D, M, means3D, scales, mod, rots, cov_pre, shs, view, proj, campos, W, H,
+                                             tanx, tany, fx, fy, radii, clamped, acc, dL_dmeans3D, dL_dmeans2D, dL_ddens,
+                                             dL_dcolors, dL_dopac, dL_dcov3D, dL_dshs, dL_dscales, dL_drots, s_row);
+        __syncthreads();
+        float4 *dst = reinterpret_cast<float4 *>(dL_dshs + (size_t)b0 * SH_ROW);
+        for (int u = threadIdx.x; u < nrow * (SH_ROW / 4); u += 256) {
+            const float *d = s_sh + (u / (SH_ROW / 4)) * SH_PAD + (u % (SH_ROW / 4)) * 4;
+            dst[u] = make_float4(d[0], d[1], d[2], d[3]);
+        }
+    } else {
+        if (i < P) preprocess_bwd_one<STAGE>(i, D, M, means3D, scales, mod, rots, cov_pre, shs, view, proj, campos, W, H,
+                                             tanx, tany, fx, fy, radii, clamped, acc, dL_dmeans3D, dL_dmeans2D, dL_ddens,
+                                             dL_dcolors, dL_dopac, dL_dcov3D, dL_dshs, dL_dscales, dL_drots, nullptr);
+    }
+}
+
+// one Gaussian of k_preprocess_bwd; STAGE: its SH row is s_row in LDS, overwritten by its gradient
+template <bool STAGE>
+__device__ __forceinline__ void preprocess_bwd_one(
+    int i, int D, int M, const float *__restrict__ means3D, const float *__restrict__ scales, float mod,
+    const float *__restrict__ rots, const float *__restrict__ cov_pre, const float *__restrict__ shs,
+    const float *view, const float *proj, const float *campos, int W, int H, float tanx, float tany,
+    float fx, float fy, const int *__restrict__ radii, const uint8_t *__restrict__ clamped,
+    const float *__restrict__ acc, float *__restrict__ dL_dmeans3D, float *__restrict__ dL_dmeans2D,
+    float *__restrict__ dL_ddens, float *__restrict__ dL_dcolors, float *__restrict__ dL_dopac,
+    float *__restrict__ dL_dcov3D, float *__restrict__ dL_dshs, float *__restrict__ dL_dscales,
+    float *__restrict__ dL_drots, float *s_row) {
     const float *a = acc + (size_t)i * ACC_STRIDE;
     float4 a0 = *reinterpret_cast<const float4 *>(a);
     float4 a1 = *reinterpret_cast<const float4 *>(a + 4);
@@ -720,11 +791,17 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(
     }
     // SH backward (also writes zeros for culled Gaussians)
     if (shs) {
-        float *dsh = dL_dshs + (size_t)i * M * 3;
+        float *dsh = STAGE ? s_row : dL_dshs + (size_t)i * M * 3;
         if (!vis) {
             for (int k = 0; k < M * 3; k++) dsh[k] = 0.f;
         } else {
+            float shr[STAGE ? SH_ROW : 1];  // STAGE: the row in registers (the LDS row is overwritten)
             const float *sh = shs + (size_t)i * M * 3;
+            if constexpr (STAGE) {
+#pragma unroll
+                for (int k = 0; k < SH_ROW; k++) shr[k] = s_row[k];
+                sh = shr;
+            }
             float vx = p.x - cam.c[0], vy = p.y - cam.c[1], vz = p.z - cam.c[2];
             float n = sqrtf(vx * vx + vy * vy + vz * vz);
             float x = vx / n, y = vy / n, z = vz / n;
@@ -1043,8 +1120,15 @@ dgs_raster_ctx *ctx_acquire(int device, hipStream_t stream) {
         c = new dgs_raster_ctx();
         c->device = device;
     }
-    if (c->pending_release && c->released) {
-        (void)hipStreamWaitEvent(stream, c->released, 0);
+    if (c->pending_release) {
+        // the previous user's work on its stream precedes this one in stream order when the stream
+        // is the same (the training loop): no marker at all (each costs ~6 us of GPU idle);
+        // otherwise order this stream after everything queued on that stream so far
+        if (c->last_stream != stream) {
+            if (!c->released) (void)hipEventCreateWithFlags(&c->released, hipEventDisableTiming);
+            (void)hipEventRecord(c->released, c->last_stream);
+            (void)hipStreamWaitEvent(stream, c->released, 0);
+        }
         c->pending_release = false;
     }
     return c;
@@ -1308,7 +1392,9 @@ extern "C" int dgs_raster_forward(const dgs_raster_settings *s, int P, int M, co
     if (P > 0) {
         {
             ScopedTimer tm("preprocess_fwd", stream);
-            hipLaunchKernelGGL(k_preprocess, dim3(div_up(P, 256)), dim3(256), 0, stream, P, s->sh_degree, M, means3D, scales,
+            const bool stage = shs && M * 3 == SH_ROW && (reinterpret_cast<uintptr_t>(shs) & 15) == 0;
+            hipLaunchKernelGGL(stage ? k_preprocess<true> : k_preprocess<false>, dim3(div_up(P, 256)), dim3(256), 0, stream,
+                               P, s->sh_degree, M, means3D, scales,
                                s->scale_modifier, rotations, cov3D_precomp, opacities, shs, colors_precomp, s->viewmatrix,
                                s->projmatrix, s->campos, c->W, c->H, s->tanfovx, s->tanfovy, fx, fy, c->gx, c->gy, out_radii,
                                c->xy, c->conic_o, c->rgbd, c->tiles, c->clamped, c->dkey, c->gid, (float4 *)c->acc.p);
@@ -1431,7 +1517,10 @@ extern "C" int dgs_raster_backward(dgs_raster_ctx *c, const float *dL_dcolor, co
     const float fx = c->W / (2.f * c->s.tanfovx), fy = c->H / (2.f * c->s.tanfovy);
     {
         ScopedTimer tm("preprocess_bwd", stream);
-        hipLaunchKernelGGL(k_preprocess_bwd, dim3(div_up(P, 256)), dim3(256), 0, stream, P, c->s.sh_degree, c->M, c->means3D,
+        const bool stage = c->shs && c->M * 3 == SH_ROW &&
+                           ((reinterpret_cast<uintptr_t>(c->shs) | reinterpret_cast<uintptr_t>(dL_dshs)) & 15) == 0;
+        hipLaunchKernelGGL(stage ? k_preprocess_bwd<true> : k_preprocess_bwd<false>, dim3(div_up(P, 256)), dim3(256), 0,
+                           stream, P, c->s.sh_degree, c->M, c->means3D,
                            c->scales, c->s.scale_modifier, c->rots, c->cov, c->shs, c->s.viewmatrix, c->s.projmatrix,
                            c->s.campos, c->W, c->H, c->s.tanfovx, c->s.tanfovy, fx, fy, c->radii, c->clamped, acc,
                            dL_dmeans3D, dL_dmeans2D, dL_dmeans2D_densify, dL_dcolors, dL_dopacity, dL_dcov3D, dL_dshs,
@@ -1444,10 +1533,8 @@ extern "C" int dgs_raster_backward(dgs_raster_ctx *c, const float *dL_dcolor, co
 extern "C" void dgs_raster_ctx_free(dgs_raster_ctx *c) {
     if (!c) return;
     (void)resolve_count(c, c->last_stream);  // a deferred count nobody read (forward without backward)
-    // Buffers stay allocated for reuse by the next forward on this device; a later acquirer waits
-    // on this event (recorded on the stream that last used the buffers) before reuse.
-    if (!c->released) (void)hipEventCreateWithFlags(&c->released, hipEventDisableTiming);
-    (void)hipEventRecord(c->released, c->last_stream);
+    // Buffers stay allocated for reuse by the next forward on this device; an acquirer on another
+    // stream is ordered after the stream that last used them (ctx_acquire).
     c->pending_release = true;
     std::lock_guard<std::mutex> lk(g_pool_mu);
     if (g_pool.size() < 64) {
