@@ -126,6 +126,7 @@ extern "C" int dgs_adam_step(int n, const dgs_adam_tensor *t, double beta1, doub
             set_error("dgs_adam_step: tensor list too large for one grid");
             return DGS_ERR_ARGS;
         }
+        ScopedTimer tm("adam", stream);
         hipLaunchKernelGGL(adam::k_adam, dim3((unsigned)blocks), dim3(adam::THREADS), 0, stream, J);
         DGS_LAUNCH_CHECK("k_adam", false, stream);
     }

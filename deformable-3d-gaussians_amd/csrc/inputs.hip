@@ -338,13 +338,14 @@ int inputs_forward(const char *name, int P, int M_rest, const float *xyz, const 
         return DGS_ERR_ARGS;
     }
     if (P == 0) return DGS_OK;
-    if (!xyz || !f_dc || (M_rest > 0 && !f_rest) || !scaling || !rotation || !opacity || !means3D || !shs || !scales ||
-        !rotations || !opacities) {
+    if (!xyz || (shs && (!f_dc || (M_rest > 0 && !f_rest))) || !scaling || !rotation || !opacity || !means3D ||
+        !scales || !rotations || !opacities) {
         set_error(std::string(name) + ": null argument");
         return DGS_ERR_ARGS;
     }
-    const int C = 1 + M_rest;
+    const int C = shs ? 1 + M_rest : 0;  // shs == NULL: no SH concatenation (split-SH rasterizer)
     const long long n = ((long long)P * 3 * C + 3) / 4 + P;  // SH units + activation threads
+    ScopedTimer tm("inputs_fwd", stream);
     hipLaunchKernelGGL(inputs::k_inputs_fwd<SE3>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, P, C, xyz,
                        f_dc, f_rest, scaling, rotation, opacity, deform, deform_stride, means3D, shs, scales, rotations,
                        opacities);
@@ -364,13 +365,14 @@ int inputs_backward(const char *name, int P, int M_rest, const float *xyz, const
         return DGS_ERR_ARGS;
     }
     if (P == 0) return DGS_OK;
-    if (!scaling || !rotation || !opacity || !d_means3D || !d_shs || !d_scales || !d_rotations || !d_opacities ||
+    if (!scaling || !rotation || !opacity || !d_means3D || !d_scales || !d_rotations || !d_opacities ||
         (SE3 && (!xyz || !deform))) {
         set_error(std::string(name) + ": null argument");
         return DGS_ERR_ARGS;
     }
-    const int C = 1 + M_rest;
+    const int C = d_shs ? 1 + M_rest : 0;  // d_shs == NULL: the SH gradients are written elsewhere
     const long long n = ((long long)P * 3 * C + 3) / 4 + P;  // SH units + activation threads
+    ScopedTimer tm("inputs_bwd", stream);
     hipLaunchKernelGGL(inputs::k_inputs_bwd<SE3>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, P, C, xyz,
                        deform, deform_stride, scaling, rotation, opacity, d_means3D, d_shs, d_scales, d_rotations,
                        d_opacities, g_xyz, g_dc, g_rest, g_scaling, g_rotation, g_opacity, g_deform, g_stride);

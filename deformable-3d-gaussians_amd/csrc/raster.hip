@@ -44,12 +44,88 @@ namespace dgs {
 // STAGE (M = 16, 16-byte aligned SH): the block's SH rows are read into LDS with coalesced
 // 16-byte loads before any thread culls its Gaussian (see k_preprocess_bwd)
 constexpr int SH_ROW = 48, SH_PAD = 49;  // odd LDS row stride: a thread-per-row access is conflict-free
+
+// The block's nrow SH rows into LDS rows of SH_PAD floats: from one (P, 16, 3) tensor, or split
+// (rest != nullptr) from features_dc (P, 1, 3) and features_rest (P, 15, 3) as the Gaussian model
+// stores them (no concatenated copy). All loads are 16-byte units of contiguous row blocks.
+__device__ __forceinline__ void sh_stage_in(float *s_sh, const float *shs, const float *rest, int b0, int nrow) {
+    if (!rest) {
+        const float4 *src = reinterpret_cast<const float4 *>(shs + (size_t)b0 * SH_ROW);
+        for (int u = threadIdx.x; u < nrow * (SH_ROW / 4); u += 256) {
+            const float4 v = src[u];
+            float *d = s_sh + (u / (SH_ROW / 4)) * SH_PAD + (u % (SH_ROW / 4)) * 4;
+            d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+        }
+        return;
+    }
+    auto get = [&](const float *base, int rowlen, int off) {
+        const int n = nrow * rowlen;
+        const float *src = base + (size_t)b0 * rowlen;
+        for (int u = threadIdx.x; u < div_up(n, 4); u += 256) {
+            float w[4];
+            if (4 * u + 3 < n) {
+                const float4 v = reinterpret_cast<const float4 *>(src)[u];
+                w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+            } else {  // the tensor's last partial unit: no read past its end
+#pragma unroll
+                for (int j = 0; j < 4; j++) w[j] = 4 * u + j < n ? src[4 * u + j] : 0.f;
+            }
+            int r = 4 * u / rowlen, c = 4 * u - r * rowlen;  // one division per unit, then carry
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                if (4 * u + j < n) s_sh[r * SH_PAD + off + c] = w[j];
+                if (++c == rowlen) {
+                    c = 0;
+                    r++;
+                }
+            }
+        }
+    };
+    get(shs, 3, 0);
+    get(rest, SH_ROW - 3, 3);
+}
+
+// LDS rows -> the (P, 16, 3) gradient, or split into the dc (P, 1, 3) / rest (P, 15, 3) gradients
+__device__ __forceinline__ void sh_stage_out(const float *s_sh, float *dsh, float *drest, int b0, int nrow) {
+    if (!drest) {
+        float4 *dst = reinterpret_cast<float4 *>(dsh + (size_t)b0 * SH_ROW);
+        for (int u = threadIdx.x; u < nrow * (SH_ROW / 4); u += 256) {
+            const float *d = s_sh + (u / (SH_ROW / 4)) * SH_PAD + (u % (SH_ROW / 4)) * 4;
+            dst[u] = make_float4(d[0], d[1], d[2], d[3]);
+        }
+        return;
+    }
+    auto put = [&](float *base, int rowlen, int off) {
+        const int n = nrow * rowlen;
+        float4 *dst = reinterpret_cast<float4 *>(base + (size_t)b0 * rowlen);
+        for (int u = threadIdx.x; u < div_up(n, 4); u += 256) {
+            float w[4];
+            int r = 4 * u / rowlen, c = 4 * u - r * rowlen;  // one division per unit, then carry
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                w[j] = 4 * u + j < n ? s_sh[r * SH_PAD + off + c] : 0.f;
+                if (++c == rowlen) {
+                    c = 0;
+                    r++;
+                }
+            }
+            if (4 * u + 3 < n) {
+                dst[u] = make_float4(w[0], w[1], w[2], w[3]);
+            } else {
+                for (int j = 0; 4 * u + j < n; j++) base[(size_t)b0 * rowlen + 4 * u + j] = w[j];
+            }
+        }
+    };
+    put(dsh, 3, 0);
+    put(drest, SH_ROW - 3, 3);
+}
+
 template <bool STAGE>
 __global__ __launch_bounds__(256) void k_preprocess(
     int P, int D, int M, const float *__restrict__ means3D, const float *__restrict__ scales, float mod,
     const float *__restrict__ rots, const float *__restrict__ cov_pre, const float *__restrict__ opac,
-    const float *__restrict__ shs, const float *__restrict__ colors_pre, const float *view,
-    const float *proj, const float *campos, int W, int H, float tanx, float tany, float fx, float fy,
+    const float *__restrict__ shs, const float *__restrict__ shs_rest, const float *__restrict__ colors_pre,
+    const float *view, const float *proj, const float *campos, int W, int H, float tanx, float tany, float fx, float fy,
     int gx, int gy, int *__restrict__ radii, float2 *__restrict__ xy, float4 *__restrict__ conic_o,
     float4 *__restrict__ rgbd, uint32_t *__restrict__ tiles, uint8_t *__restrict__ clamped,
     uint32_t *__restrict__ dkey, uint32_t *__restrict__ gid, float4 *__restrict__ acc) {
@@ -58,12 +134,7 @@ __global__ __launch_bounds__(256) void k_preprocess(
     if constexpr (STAGE) {
         __shared__ float s_sh[256 * SH_PAD];
         const int b0 = blockIdx.x * blockDim.x, nrow = min(256, P - b0);
-        const float4 *src = reinterpret_cast<const float4 *>(shs + (size_t)b0 * SH_ROW);
-        for (int u = threadIdx.x; u < nrow * (SH_ROW / 4); u += 256) {
-            const float4 v = src[u];
-            float *d = s_sh + (u / (SH_ROW / 4)) * SH_PAD + (u % (SH_ROW / 4)) * 4;
-            d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
-        }
+        sh_stage_in(s_sh, shs, shs_rest, b0, nrow);
         __syncthreads();
         s_row = s_sh + threadIdx.x * SH_PAD;
     }
@@ -658,29 +729,20 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(
     const float *__restrict__ acc, float *__restrict__ dL_dmeans3D, float *__restrict__ dL_dmeans2D,
     float *__restrict__ dL_ddens, float *__restrict__ dL_dcolors, float *__restrict__ dL_dopac,
     float *__restrict__ dL_dcov3D, float *__restrict__ dL_dshs, float *__restrict__ dL_dscales,
-    float *__restrict__ dL_drots) {
+    float *__restrict__ dL_drots, const float *__restrict__ shs_rest, float *__restrict__ dL_dshs_rest) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     [[maybe_unused]] const int b0 = blockIdx.x * blockDim.x, nrow = min(256, P - b0);
     [[maybe_unused]] float *s_row = nullptr;
     if constexpr (STAGE) {
         __shared__ float s_sh[256 * SH_PAD];
         s_row = s_sh + threadIdx.x * SH_PAD;
-        const float4 *src = reinterpret_cast<const float4 *>(shs + (size_t)b0 * SH_ROW);
-        for (int u = threadIdx.x; u < nrow * (SH_ROW / 4); u += 256) {
-            const float4 v = src[u];
-            float *d = s_sh + (u / (SH_ROW / 4)) * SH_PAD + (u % (SH_ROW / 4)) * 4;
-            d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
-        }
+        sh_stage_in(s_sh, shs, shs_rest, b0, nrow);
         __syncthreads();
         if (i < P) preprocess_bwd_one<STAGE>(i, D, M, means3D, scales, mod, rots, cov_pre, shs, view, proj, campos, W, H,
                                              tanx, tany, fx, fy, radii, clamped, acc, dL_dmeans3D, dL_dmeans2D, dL_ddens,
                                              dL_dcolors, dL_dopac, dL_dcov3D, dL_dshs, dL_dscales, dL_drots, s_row);
         __syncthreads();
-        float4 *dst = reinterpret_cast<float4 *>(dL_dshs + (size_t)b0 * SH_ROW);
-        for (int u = threadIdx.x; u < nrow * (SH_ROW / 4); u += 256) {
-            const float *d = s_sh + (u / (SH_ROW / 4)) * SH_PAD + (u % (SH_ROW / 4)) * 4;
-            dst[u] = make_float4(d[0], d[1], d[2], d[3]);
-        }
+        sh_stage_out(s_sh, dL_dshs, dL_dshs_rest, b0, nrow);
     } else {
         if (i < P) preprocess_bwd_one<STAGE>(i, D, M, means3D, scales, mod, rots, cov_pre, shs, view, proj, campos, W, H,
                                              tanx, tany, fx, fy, radii, clamped, acc, dL_dmeans3D, dL_dmeans2D, dL_ddens,
@@ -953,6 +1015,7 @@ struct dgs_raster_ctx {
     int P = 0, M = 0, H = 0, W = 0, gx = 0, gy = 0, num_rendered = 0;
     const float *means3D = nullptr, *shs = nullptr, *colors = nullptr, *opac = nullptr, *scales = nullptr,
                 *rots = nullptr, *cov = nullptr;
+    const float *shs_rest = nullptr;  // split SH rows (dgs_raster_forward_split_sh): shs = features_dc
     DevBuf geom, bin, img, acc, tmp, rect;
     // carved views
     float2 *xy = nullptr;
@@ -1297,12 +1360,16 @@ static int resolve_count(dgs_raster_ctx *c, hipStream_t stream) {
     return DGS_OK;
 }
 
-extern "C" int dgs_raster_forward(const dgs_raster_settings *s, int P, int M, const float *means3D,
-                                  const float *shs, const float *colors_precomp, const float *opacities,
-                                  const float *scales, const float *rotations, const float *cov3D_precomp,
-                                  float *out_color, float *out_depth, int *out_radii, dgs_raster_ctx **ctx_out,
-                                  int *num_rendered, void *stream_) {
+static int raster_forward(const dgs_raster_settings *s, int P, int M, const float *means3D, const float *shs,
+                          const float *shs_rest, const float *colors_precomp, const float *opacities,
+                          const float *scales, const float *rotations, const float *cov3D_precomp, float *out_color,
+                          float *out_depth, int *out_radii, dgs_raster_ctx **ctx_out, int *num_rendered,
+                          void *stream_) {
     hipStream_t stream = (hipStream_t)stream_;
+    if (shs_rest && (M * 3 != SH_ROW || !shs || ((reinterpret_cast<uintptr_t>(shs) | reinterpret_cast<uintptr_t>(shs_rest)) & 15))) {
+        set_error("dgs_raster_forward_split_sh: needs M = 16 and 16-byte aligned features_dc / features_rest");
+        return DGS_ERR_ARGS;
+    }
     if (!s || !ctx_out || P < 0 || !out_color || !out_depth || (P > 0 && (!means3D || !opacities || !out_radii))) {
         set_error("dgs_raster_forward: null argument");
         return DGS_ERR_ARGS;
@@ -1334,7 +1401,7 @@ extern "C" int dgs_raster_forward(const dgs_raster_settings *s, int P, int M, co
     c->W = s->image_width;
     c->gx = div_up(c->W, TILE_X);
     c->gy = div_up(c->H, TILE_Y);
-    c->means3D = means3D; c->shs = shs; c->colors = colors_precomp; c->opac = opacities;
+    c->means3D = means3D; c->shs = shs; c->shs_rest = shs_rest; c->colors = colors_precomp; c->opac = opacities;
     c->scales = scales; c->rots = rotations; c->cov = cov3D_precomp;
     c->radii = out_radii;
     c->last_stream = stream;
@@ -1395,7 +1462,7 @@ extern "C" int dgs_raster_forward(const dgs_raster_settings *s, int P, int M, co
             const bool stage = shs && M * 3 == SH_ROW && (reinterpret_cast<uintptr_t>(shs) & 15) == 0;
             hipLaunchKernelGGL(stage ? k_preprocess<true> : k_preprocess<false>, dim3(div_up(P, 256)), dim3(256), 0, stream,
                                P, s->sh_degree, M, means3D, scales,
-                               s->scale_modifier, rotations, cov3D_precomp, opacities, shs, colors_precomp, s->viewmatrix,
+                               s->scale_modifier, rotations, cov3D_precomp, opacities, shs, shs_rest, colors_precomp, s->viewmatrix,
                                s->projmatrix, s->campos, c->W, c->H, s->tanfovx, s->tanfovy, fx, fy, c->gx, c->gy, out_radii,
                                c->xy, c->conic_o, c->rgbd, c->tiles, c->clamped, c->dkey, c->gid, (float4 *)c->acc.p);
         }
@@ -1482,11 +1549,19 @@ extern "C" int dgs_raster_forward(const dgs_raster_settings *s, int P, int M, co
     return DGS_OK;
 }
 
-extern "C" int dgs_raster_backward(dgs_raster_ctx *c, const float *dL_dcolor, const float *dL_ddepth,
-                                   float *dL_dmeans3D, float *dL_dmeans2D, float *dL_dmeans2D_densify,
-                                   float *dL_dcolors, float *dL_dopacity, float *dL_dcov3D, float *dL_dshs,
-                                   float *dL_dscales, float *dL_drotations, void *stream_) {
+static int raster_backward(dgs_raster_ctx *c, const float *dL_dcolor, const float *dL_ddepth, float *dL_dmeans3D,
+                           float *dL_dmeans2D, float *dL_dmeans2D_densify, float *dL_dcolors, float *dL_dopacity,
+                           float *dL_dcov3D, float *dL_dshs, float *dL_dshs_rest, float *dL_dscales,
+                           float *dL_drotations, void *stream_) {
     hipStream_t stream = (hipStream_t)stream_;
+    if (c && (c->shs_rest != nullptr) != (dL_dshs_rest != nullptr)) {
+        set_error("dgs_raster_backward: split SH gradients go with a split SH forward");
+        return DGS_ERR_ARGS;
+    }
+    if (c && dL_dshs_rest && ((reinterpret_cast<uintptr_t>(dL_dshs) | reinterpret_cast<uintptr_t>(dL_dshs_rest)) & 15)) {
+        set_error("dgs_raster_backward_split_sh: SH gradients must be 16-byte aligned");
+        return DGS_ERR_ARGS;
+    }
     if (!c || !dL_dcolor) {
         set_error("dgs_raster_backward: null argument");
         return DGS_ERR_ARGS;
@@ -1517,17 +1592,60 @@ extern "C" int dgs_raster_backward(dgs_raster_ctx *c, const float *dL_dcolor, co
     const float fx = c->W / (2.f * c->s.tanfovx), fy = c->H / (2.f * c->s.tanfovy);
     {
         ScopedTimer tm("preprocess_bwd", stream);
-        const bool stage = c->shs && c->M * 3 == SH_ROW &&
-                           ((reinterpret_cast<uintptr_t>(c->shs) | reinterpret_cast<uintptr_t>(dL_dshs)) & 15) == 0;
+        const bool stage = c->shs_rest || (c->shs && c->M * 3 == SH_ROW &&
+                           ((reinterpret_cast<uintptr_t>(c->shs) | reinterpret_cast<uintptr_t>(dL_dshs)) & 15) == 0);
         hipLaunchKernelGGL(stage ? k_preprocess_bwd<true> : k_preprocess_bwd<false>, dim3(div_up(P, 256)), dim3(256), 0,
                            stream, P, c->s.sh_degree, c->M, c->means3D,
                            c->scales, c->s.scale_modifier, c->rots, c->cov, c->shs, c->s.viewmatrix, c->s.projmatrix,
                            c->s.campos, c->W, c->H, c->s.tanfovx, c->s.tanfovy, fx, fy, c->radii, c->clamped, acc,
                            dL_dmeans3D, dL_dmeans2D, dL_dmeans2D_densify, dL_dcolors, dL_dopacity, dL_dcov3D, dL_dshs,
-                           dL_dscales, dL_drotations);
+                           dL_dscales, dL_drotations, c->shs_rest, dL_dshs_rest);
     }
     DGS_LAUNCH_CHECK("k_preprocess_bwd", dbg, stream);
     return DGS_OK;
+}
+
+extern "C" int dgs_raster_forward(const dgs_raster_settings *s, int P, int M, const float *means3D,
+                                  const float *shs, const float *colors_precomp, const float *opacities,
+                                  const float *scales, const float *rotations, const float *cov3D_precomp,
+                                  float *out_color, float *out_depth, int *out_radii, dgs_raster_ctx **ctx_out,
+                                  int *num_rendered, void *stream) {
+    return raster_forward(s, P, M, means3D, shs, nullptr, colors_precomp, opacities, scales, rotations, cov3D_precomp,
+                          out_color, out_depth, out_radii, ctx_out, num_rendered, stream);
+}
+
+extern "C" int dgs_raster_forward_split_sh(const dgs_raster_settings *s, int P, const float *means3D,
+                                           const float *features_dc, const float *features_rest,
+                                           const float *opacities, const float *scales, const float *rotations,
+                                           float *out_color, float *out_depth, int *out_radii,
+                                           dgs_raster_ctx **ctx_out, int *num_rendered, void *stream) {
+    if (P > 0 && (!features_dc || !features_rest)) {
+        set_error("dgs_raster_forward_split_sh: null SH argument");
+        return DGS_ERR_ARGS;
+    }
+    return raster_forward(s, P, SH_ROW / 3, means3D, features_dc, P > 0 ? features_rest : nullptr, nullptr, opacities,
+                          scales, rotations, nullptr, out_color, out_depth, out_radii, ctx_out, num_rendered, stream);
+}
+
+extern "C" int dgs_raster_backward(dgs_raster_ctx *c, const float *dL_dcolor, const float *dL_ddepth,
+                                   float *dL_dmeans3D, float *dL_dmeans2D, float *dL_dmeans2D_densify,
+                                   float *dL_dcolors, float *dL_dopacity, float *dL_dcov3D, float *dL_dshs,
+                                   float *dL_dscales, float *dL_drotations, void *stream) {
+    return raster_backward(c, dL_dcolor, dL_ddepth, dL_dmeans3D, dL_dmeans2D, dL_dmeans2D_densify, dL_dcolors,
+                           dL_dopacity, dL_dcov3D, dL_dshs, nullptr, dL_dscales, dL_drotations, stream);
+}
+
+extern "C" int dgs_raster_backward_split_sh(dgs_raster_ctx *c, const float *dL_dcolor, const float *dL_ddepth,
+                                            float *dL_dmeans3D, float *dL_dmeans2D, float *dL_dmeans2D_densify,
+                                            float *dL_dopacity, float *dL_dfeatures_dc, float *dL_dfeatures_rest,
+                                            float *dL_dscales, float *dL_drotations, void *stream) {
+    if (c && c->P > 0 && (!dL_dfeatures_dc || !dL_dfeatures_rest)) {
+        set_error("dgs_raster_backward_split_sh: null SH gradient");
+        return DGS_ERR_ARGS;
+    }
+    return raster_backward(c, dL_dcolor, dL_ddepth, dL_dmeans3D, dL_dmeans2D, dL_dmeans2D_densify, nullptr,
+                           dL_dopacity, nullptr, dL_dfeatures_dc, c && c->P > 0 ? dL_dfeatures_rest : nullptr,
+                           dL_dscales, dL_drotations, stream);
 }
 
 extern "C" void dgs_raster_ctx_free(dgs_raster_ctx *c) {

@@ -8,10 +8,12 @@ deformation network or absent) it runs as one HIP launch each way (dgs_gaussian_
 backward writes the deformation network's (N, 10) output gradient directly.
 """
 import math
+import os
 
 import torch
 
-from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+from diff_gaussian_rasterization import (GaussianRasterizationSettings, GaussianRasterizer,
+                                         rasterize_gaussians_split_sh, split_sh_ok)
 
 from . import _lib
 from .rigid import from_homogenous, to_homogenous
@@ -23,13 +25,15 @@ class _GaussianInputs(torch.autograd.Function):
     (means3D, shs, opacities, scales, rotations) of gaussian_renderer/__init__.py:70-112."""
 
     @staticmethod
-    def forward(ctx, xyz, f_dc, f_rest, scaling, rotation, opacity, deform, se3=False):
+    def forward(ctx, xyz, f_dc, f_rest, scaling, rotation, opacity, deform, se3=False, with_sh=True):
         lib = _lib.load()
         P = xyz.shape[0]
         M_rest = f_rest.shape[1]
         dev = xyz.device
         e = lambda *shape: torch.empty(shape, dtype=torch.float32, device=dev)  # noqa: E731
-        means3D, shs, scales, rots, opac = e(P, 3), e(P, 1 + M_rest, 3), e(P, 3), e(P, 4), e(P, 1)
+        means3D, scales, rots, opac = e(P, 3), e(P, 3), e(P, 4), e(P, 1)
+        # with_sh False: the split-SH rasterizer reads features_dc / features_rest itself (no cat)
+        shs = e(P, 1 + M_rest, 3) if with_sh else None
         ds = deform.stride(0) if deform is not None else 0
         fwd = lib.dgs_gaussian_inputs_se3_forward if se3 else lib.dgs_gaussian_inputs_forward
         _lib.check(fwd(
@@ -43,6 +47,7 @@ class _GaussianInputs(torch.autograd.Function):
         ctx.M_rest = M_rest
         ctx.has_deform = deform is not None
         ctx.se3 = se3
+        ctx.with_sh = with_sh
         return means3D, shs, opac, scales, rots
 
     @staticmethod
@@ -53,11 +58,13 @@ class _GaussianInputs(torch.autograd.Function):
         dev = scaling.device
         z = lambda t, *shape: (torch.zeros(shape, dtype=torch.float32, device=dev) if t is None  # noqa: E731
                                else t.contiguous())
-        g_means, g_shs, g_opac = z(g_means, P, 3), z(g_shs, P, 1 + M_rest, 3), z(g_opac, P, 1)
+        g_means, g_opac = z(g_means, P, 3), z(g_opac, P, 1)
+        g_shs = z(g_shs, P, 1 + M_rest, 3) if ctx.with_sh else None
         g_scales, g_rots = z(g_scales, P, 3), z(g_rots, P, 4)
         need = ctx.needs_input_grad
         e = lambda ok, *shape: torch.empty(shape, dtype=torch.float32, device=dev) if ok else None  # noqa: E731
-        o_xyz, o_dc, o_rest = e(need[0], P, 3), e(need[1], P, 1, 3), e(need[2], P, M_rest, 3)
+        o_xyz = e(need[0], P, 3)
+        o_dc, o_rest = e(need[1] and ctx.with_sh, P, 1, 3), e(need[2] and ctx.with_sh, P, M_rest, 3)
         o_sc, o_rot, o_op = e(need[3], P, 3), e(need[4], P, 4), e(need[5], P, 1)
         if ctx.se3:
             xyz, deform = ctx.saved_tensors[3:]
@@ -67,14 +74,18 @@ class _GaussianInputs(torch.autograd.Function):
                 _lib.ptr(opacity), _lib.ptr(g_means), _lib.ptr(g_shs), _lib.ptr(g_scales), _lib.ptr(g_rots),
                 _lib.ptr(g_opac), _lib.ptr(o_xyz), _lib.ptr(o_dc), _lib.ptr(o_rest), _lib.ptr(o_sc), _lib.ptr(o_rot),
                 _lib.ptr(o_op), _lib.ptr(o_def), _lib.stream_ptr(dev)), "gaussian_inputs_se3_backward")
-            return o_xyz, o_dc, o_rest, o_sc, o_rot, o_op, o_def, None
+            return o_xyz, o_dc, o_rest, o_sc, o_rot, o_op, o_def, None, None, None
         o_def = e(ctx.has_deform and need[6], P, 10)
         _lib.check(lib.dgs_gaussian_inputs_backward(
             P, M_rest, _lib.ptr(scaling), _lib.ptr(rotation), _lib.ptr(opacity), _lib.ptr(g_means), _lib.ptr(g_shs),
             _lib.ptr(g_scales), _lib.ptr(g_rots), _lib.ptr(g_opac), _lib.ptr(o_xyz), _lib.ptr(o_dc), _lib.ptr(o_rest),
             _lib.ptr(o_sc), _lib.ptr(o_rot), _lib.ptr(o_op), _lib.ptr(o_def), 10, _lib.stream_ptr(dev)),
             "gaussian_inputs_backward")
-        return o_xyz, o_dc, o_rest, o_sc, o_rot, o_op, o_def, None
+        return o_xyz, o_dc, o_rest, o_sc, o_rot, o_op, o_def, None, None
+
+
+# DGS_SPLIT_SH=0 (A/B diagnostic): the fused path concatenates the SH rows for the plain rasterizer
+_SPLIT_SH = os.environ.get("DGS_SPLIT_SH", "1") not in ("", "0")
 
 
 def _fused_deform_rows(pc, d_xyz, d_rotation, d_scaling):
@@ -152,12 +163,18 @@ def render(viewpoint_camera, pc, pipe, bg_color, d_xyz, d_rotation, d_scaling, i
             rows = _fused_se3_rows(pc, d_xyz, d_rotation, d_scaling)
             se3 = rows is not None
     if rows is not None:
+        split = _SPLIT_SH and split_sh_ok(pc._features_dc, pc._features_rest)
         means3D, shs, opacity, scales, rotations = _GaussianInputs.apply(
             pc._xyz, pc._features_dc, pc._features_rest, pc._scaling, pc._rotation, pc._opacity,
-            rows if torch.is_tensor(rows) else None, se3)
-        rendered_image, radii, depth = rasterizer(
-            means3D=means3D, means2D=screenspace_points, means2D_densify=screenspace_points_densify, shs=shs,
-            colors_precomp=None, opacities=opacity, scales=scales, rotations=rotations, cov3D_precomp=None)
+            rows if torch.is_tensor(rows) else None, se3, not split)
+        if split:  # SH rows read / written in place by the rasterizer (no (N, 16, 3) cat either way)
+            rendered_image, radii, depth = rasterize_gaussians_split_sh(
+                means3D, screenspace_points, screenspace_points_densify, pc._features_dc, pc._features_rest, opacity,
+                scales, rotations, raster_settings)
+        else:
+            rendered_image, radii, depth = rasterizer(
+                means3D=means3D, means2D=screenspace_points, means2D_densify=screenspace_points_densify, shs=shs,
+                colors_precomp=None, opacities=opacity, scales=scales, rotations=rotations, cov3D_precomp=None)
         return {"render": rendered_image, "viewspace_points": screenspace_points,
                 "viewspace_points_densify": screenspace_points_densify, "visibility_filter": radii > 0,
                 "radii": radii, "depth": depth}

@@ -169,6 +169,77 @@ class _RasterizeGaussians(torch.autograd.Function):
         return (d_means3D, d_means2D, d_dens, d_shs, d_col, d_opac.view_as(opacities), d_scales, d_rots, d_cov, None)
 
 
+class _RasterizeGaussiansSplitSH(torch.autograd.Function):
+    """The same op with the SH rows read from (features_dc (P,1,3), features_rest (P,15,3)) and their
+    gradients written back to both (dgs_raster_*_split_sh): render()'s training path, where the
+    reference concatenates them every call (scene/gaussian_model.py:71-74). Not part of the upstream
+    module's interface; results are those of shs = cat(features_dc, features_rest)."""
+
+    @staticmethod
+    def forward(ctx, means3D, means2D, means2D_densify, f_dc, f_rest, opacities, scales, rotations, raster_settings):
+        lib = _lib.load()
+        keep = []
+        s = _settings_struct(raster_settings, keep)
+        P = means3D.shape[0]
+        H, W = int(raster_settings.image_height), int(raster_settings.image_width)
+        dev = means3D.device
+        color = torch.empty((3, H, W), dtype=torch.float32, device=dev)
+        depth = torch.empty((1, H, W), dtype=torch.float32, device=dev)
+        radii = torch.empty((P,), dtype=torch.int32, device=dev)
+        handle = _lib.P()
+        nr = _lib.I(0)
+        rc = lib.dgs_raster_forward_split_sh(s, P, _lib.ptr(means3D), _lib.ptr(f_dc), _lib.ptr(f_rest),
+                                             _lib.ptr(opacities), _lib.ptr(scales), _lib.ptr(rotations),
+                                             _lib.ptr(color), _lib.ptr(depth), _lib.ptr(radii), handle, nr,
+                                             _lib.stream_ptr(dev))
+        _lib.check(rc, "rasterize_gaussians")
+        ctx.raster = _Ctx(handle)
+        ctx.raster_hw = (H, W)
+        ctx.keep = keep
+        ctx.num_rendered = nr.value
+        ctx.P = P
+        # the saved C context points at these inputs: keep them alive (and version-checked) until backward
+        ctx.save_for_backward(radii, means3D, f_dc, f_rest, opacities, scales, rotations)
+        ctx.mark_non_differentiable(radii)
+        ctx.set_materialize_grads(False)
+        return color, radii, depth
+
+    @staticmethod
+    def backward(ctx, grad_color, grad_radii, grad_depth):
+        lib = _lib.load()
+        radii = ctx.saved_tensors[0]
+        P, dev = ctx.P, radii.device
+        e = lambda *shape: torch.empty(shape, dtype=torch.float32, device=dev)  # noqa: E731
+        d_means3D, d_means2D, d_dens, d_opac = e(P, 3), e(P, 3), e(P, 3), e(P, 1)
+        d_dc, d_rest, d_scales, d_rots = e(P, 1, 3), e(P, 15, 3), e(P, 3), e(P, 4)
+        if grad_color is None:
+            grad_color = torch.zeros((3, ctx.raster_hw[0], ctx.raster_hw[1]), dtype=torch.float32, device=dev)
+        gc = _f32(grad_color)
+        gd = _f32(grad_depth) if grad_depth is not None else None
+        rc = lib.dgs_raster_backward_split_sh(ctx.raster.handle, _lib.ptr(gc), _lib.ptr(gd), _lib.ptr(d_means3D),
+                                              _lib.ptr(d_means2D), _lib.ptr(d_dens), _lib.ptr(d_opac),
+                                              _lib.ptr(d_dc), _lib.ptr(d_rest), _lib.ptr(d_scales),
+                                              _lib.ptr(d_rots), _lib.stream_ptr(dev))
+        _lib.check(rc, "rasterize_gaussians_backward")
+        ctx.raster.free()
+        return d_means3D, d_means2D, d_dens, d_dc, d_rest, d_opac, d_scales, d_rots, None
+
+
+def split_sh_ok(f_dc, f_rest):
+    """(features_dc, features_rest) the split-SH op takes: fp32 CUDA, contiguous (P,1,3) / (P,15,3),
+    16-byte aligned."""
+    return (f_dc.is_cuda and f_dc.dtype == torch.float32 and f_rest.dtype == torch.float32 and f_dc.is_contiguous()
+            and f_rest.is_contiguous() and f_dc.dim() == 3 and tuple(f_dc.shape[1:]) == (1, 3)
+            and f_rest.dim() == 3 and tuple(f_rest.shape[1:]) == (15, 3) and f_rest.shape[0] == f_dc.shape[0]
+            and f_dc.data_ptr() % 16 == 0 and f_rest.data_ptr() % 16 == 0)
+
+
+def rasterize_gaussians_split_sh(means3D, means2D, means2D_densify, f_dc, f_rest, opacities, scales, rotations,
+                                 raster_settings):
+    return _RasterizeGaussiansSplitSH.apply(means3D, means2D, means2D_densify, f_dc, f_rest, opacities, scales,
+                                            rotations, raster_settings)
+
+
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
                         raster_settings, means2D_densify=None):
     if means2D_densify is None:

@@ -85,6 +85,21 @@ int dgs_raster_backward(dgs_raster_ctx *ctx, const float *dL_dcolor, const float
                         float *dL_dcolors, float *dL_dopacity, float *dL_dcov3D, float *dL_dshs,
                         float *dL_dscales, float *dL_drotations, void *stream);
 
+/* Split-SH variant used by render()'s training path: the SH rows come straight from the Gaussian
+ * model's features_dc (P,1,3) and features_rest (P,15,3) (scene/gaussian_model.py:71-74 concatenates
+ * them per call; here the preprocess kernels read and write both tensors directly, so no (P,16,3)
+ * copy is made either way). Degree <= 3, 16 coefficients; all four SH pointers 16-byte aligned.
+ * Same outputs and semantics as dgs_raster_forward(shs = cat(features_dc, features_rest)); the
+ * backward writes the two SH gradients. */
+int dgs_raster_forward_split_sh(const dgs_raster_settings *s, int P, const float *means3D,
+                                const float *features_dc, const float *features_rest, const float *opacities,
+                                const float *scales, const float *rotations, float *out_color, float *out_depth,
+                                int *out_radii, dgs_raster_ctx **ctx, int *num_rendered, void *stream);
+int dgs_raster_backward_split_sh(dgs_raster_ctx *ctx, const float *dL_dcolor, const float *dL_ddepth,
+                                 float *dL_dmeans3D, float *dL_dmeans2D, float *dL_dmeans2D_densify,
+                                 float *dL_dopacity, float *dL_dfeatures_dc, float *dL_dfeatures_rest,
+                                 float *dL_dscales, float *dL_drotations, void *stream);
+
 void dgs_raster_ctx_free(dgs_raster_ctx *ctx);
 
 /* Frustum test only (p_view.z > 0.2): visible (P,) uint8. */
@@ -176,7 +191,8 @@ int dgs_knn_dist2(int P, const float *points, float *dist2, void *stream);
  * opacities = sigmoid(opacity); shs (P, 1 + M_rest, 3) = cat(features_dc (P,1,3), features_rest (P,M_rest,3)).
  * deform: rows of deform_stride floats holding [d_xyz(3) d_rotation(4) d_scaling(3)] (the deformation
  * network output), or NULL for no deformation. Backward: g_* outputs may be NULL (not needed);
- * g_deform receives the same row layout. */
+ * g_deform receives the same row layout. shs == NULL (forward) / d_shs == NULL (backward): the SH
+ * rows are not concatenated / split (dgs_raster_*_split_sh reads and writes them in place). */
 int dgs_gaussian_inputs_forward(int P, int M_rest, const float *xyz, const float *f_dc, const float *f_rest,
                                 const float *scaling, const float *rotation, const float *opacity,
                                 const float *deform, int deform_stride, float *means3D, float *shs,
