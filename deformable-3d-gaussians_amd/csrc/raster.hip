@@ -475,6 +475,46 @@ __global__ __launch_bounds__(256) void k_ranges(const uint32_t *__restrict__ cou
     if (idx == L - 1) ranges[t].y = L;
 }
 
+// Tile culling of a staged batch (blend fwd / bwd): a Gaussian of the tile's list whose
+// alpha >= 1/255 ellipse misses every pixel centre of the tile is skipped by every pixel anyway
+// (alpha < 1/255 -> `continue`), so the batch is compacted to the Gaussians that can reach the tile
+// before the per-pixel loop. alpha = min(0.99, o exp(-Q/2)) with Q = c_x dx^2 + 2 c_y dx dy + c_z dy^2
+// (the blend's power): a pixel can take part only if Q <= 2 ln(255 o). The minimum of the convex Q
+// over the tile's pixel-centre rectangle is 0 when the centre is inside, else on an edge at the
+// clamped 1-D stationary point. The bound is widened by 1 % + 1e-3 so the fp32 rounding of either
+// side can never cull a contributor: images and gradients are unchanged (the list positions kept in
+// n_contrib are those of the full list).
+__device__ __forceinline__ bool tile_reach(float2 g, float4 co, float x0, float y0) {
+    if (!(co.w >= 1.f / 255.f)) return false;  // alpha <= o < 1/255 on every pixel
+    const float thr = 2.f * __logf(255.f * co.w) * 1.01f + 1e-3f;
+    const float dxl = g.x - (x0 + (float)(TILE_X - 1)), dxh = g.x - x0;
+    const float dyl = g.y - (y0 + (float)(TILE_Y - 1)), dyh = g.y - y0;
+    if (dxl <= 0.f && dxh >= 0.f && dyl <= 0.f && dyh >= 0.f) return true;
+    auto Q = [&](float dx, float dy) { return co.x * dx * dx + 2.f * co.y * dx * dy + co.z * dy * dy; };
+    float q = Q(dxl, fminf(fmaxf(-co.y * dxl / co.z, dyl), dyh));
+    q = fminf(q, Q(dxh, fminf(fmaxf(-co.y * dxh / co.z, dyl), dyh)));
+    q = fminf(q, Q(fminf(fmaxf(-co.y * dyl / co.x, dxl), dxh), dyl));
+    q = fminf(q, Q(fminf(fmaxf(-co.y * dyh / co.x, dxl), dxh), dyh));
+    return q <= thr;
+}
+
+// Block-wide stable compaction slot of a kept item (tid order): (slot, kept count); two barriers
+__device__ __forceinline__ int2 compact_slot(bool keep, int tid, uint32_t *s_wcnt) {
+    const unsigned long long m = __ballot(keep);
+    const int lane = tid & 63, wave = tid >> 6;
+    const int below = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) s_wcnt[wave] = (uint32_t)__popcll(m);
+    __syncthreads();
+    int base = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < TILE_PIX / 64; w++) {
+        const int c = (int)s_wcnt[w];
+        base += w < wave ? c : 0;
+        tot += c;
+    }
+    return make_int2(base + below, tot);
+}
+
 __global__ __launch_bounds__(256) void k_blend_fwd(const uint2 *__restrict__ ranges, const uint32_t *__restrict__ vals,
                                                    uint32_t cap, int W, int H, int gx, const float2 *__restrict__ xy,
                                                    const float4 *__restrict__ conic_o, const float4 *__restrict__ rgbd,
@@ -484,8 +524,11 @@ __global__ __launch_bounds__(256) void k_blend_fwd(const uint2 *__restrict__ ran
     __shared__ float2 s_xy[TILE_PIX];
     __shared__ float4 s_co[TILE_PIX];
     __shared__ float4 s_cd[TILE_PIX];
+    __shared__ int s_pos[TILE_PIX];
+    __shared__ uint32_t s_wcnt[TILE_PIX / 64];
     const int tile = blockIdx.x;
     const int tid = threadIdx.x;
+    const float tx0 = (float)((tile % gx) * TILE_X), ty0 = (float)((tile / gx) * TILE_Y);
     const int px = (tile % gx) * TILE_X + (tid % TILE_X);
     const int py = (tile / gx) * TILE_Y + (tid / TILE_X);
     const bool inside = px < W && py < H;
@@ -501,16 +544,27 @@ __global__ __launch_bounds__(256) void k_blend_fwd(const uint2 *__restrict__ ran
     for (int r = 0; r < rounds; r++) {
         if (__syncthreads_count(done) == TILE_PIX) break;
         int prog = r * TILE_PIX + tid;
+        bool keep = false;
+        uint32_t id = 0;
+        float2 gl;
+        float4 cl;
         if ((int)range.x + prog < (int)range.y) {
-            uint32_t id = vals[range.x + prog];
-            s_xy[tid] = xy[id];
-            s_co[tid] = conic_o[id];
-            s_cd[tid] = rgbd[id];
+            id = vals[range.x + prog];
+            gl = xy[id];
+            cl = conic_o[id];
+            keep = tile_reach(gl, cl, tx0, ty0);
+        }
+        const int2 sl = compact_slot(keep, tid, s_wcnt);
+        if (keep) {
+            s_xy[sl.x] = gl;
+            s_co[sl.x] = cl;
+            s_cd[sl.x] = rgbd[id];
+            s_pos[sl.x] = prog;
         }
         __syncthreads();
-        int n = min(TILE_PIX, todo_total - r * TILE_PIX);
+        const int n = sl.y;
         for (int j = 0; !done && j < n; j++) {
-            contributor++;
+            contributor = (uint32_t)s_pos[j] + 1u;  // list position + 1 (n_contrib of the full list)
             float2 g = s_xy[j];
             float4 co = s_co[j];
             float dx = g.x - pfx, dy = g.y - pfy;
@@ -585,10 +639,13 @@ __global__ __launch_bounds__(256) void k_blend_bwd(const uint2 *__restrict__ ran
     __shared__ float4 s_co[TILE_PIX];
     __shared__ float4 s_cd[TILE_PIX];
     __shared__ uint32_t s_id[TILE_PIX];
+    __shared__ int s_pos[TILE_PIX];
+    __shared__ uint32_t s_wcnt[TILE_PIX / 64];
     __shared__ uint32_t s_maxlast;
     const int tile = blockIdx.x;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
+    const float tx0 = (float)((tile % gx) * TILE_X), ty0 = (float)((tile / gx) * TILE_Y);
     const int px = (tile % gx) * TILE_X + (tid % TILE_X);
     const int py = (tile / gx) * TILE_Y + (tid / TILE_X);
     const bool inside = px < W && py < H;
@@ -623,17 +680,28 @@ __global__ __launch_bounds__(256) void k_blend_bwd(const uint2 *__restrict__ ran
     for (int r = 0; r < rounds; r++) {
         __syncthreads();
         int prog = r * TILE_PIX + tid;
+        bool keep = false;
+        uint32_t id = 0;
+        float2 gl;
+        float4 cl;
         if (prog < todo_total) {
-            uint32_t id = vals[end - prog - 1];
-            s_id[tid] = id;
-            s_xy[tid] = xy[id];
-            s_co[tid] = conic_o[id];
-            s_cd[tid] = rgbd[id];
+            id = vals[end - prog - 1];
+            gl = xy[id];
+            cl = conic_o[id];
+            keep = tile_reach(gl, cl, tx0, ty0);
+        }
+        const int2 sl = compact_slot(keep, tid, s_wcnt);
+        if (keep) {
+            s_id[sl.x] = id;
+            s_xy[sl.x] = gl;
+            s_co[sl.x] = cl;
+            s_cd[sl.x] = rgbd[id];
+            s_pos[sl.x] = prog;
         }
         __syncthreads();
-        int n = min(TILE_PIX, todo_total - r * TILE_PIX);
+        const int n = sl.y;
         for (int j = 0; j < n; j++) {
-            contributor--;
+            contributor = todo_total - 1 - s_pos[j];  // position in the full list
             float2 g = s_xy[j];
             float4 co = s_co[j];
             float dx = g.x - pfx, dy = g.y - pfy;
