@@ -4,7 +4,8 @@
 // (train_baseline.py:126-128), which PyTorch runs as 5+3 MIOpen convolutions per direction.
 //
 // The 2-D window is the outer product of the 1-D one, so every filtered map is a separable
-// 11-tap row pass + 11-tap column pass through LDS (16x16 output tile, 26x26 halo tile).
+// 11-tap row pass + 11-tap column pass through LDS (32x32 output tile, 42x42 halo tile; each thread
+// keeps a register window per pass: 18 inputs for 8 row outputs, 14 for 4 column outputs).
 // Forward: 5 maps (mu1, mu2, E[I^2], E[G^2], E[IG]) -> per pixel SSIM and the three coefficient
 // maps A, B, C of dSSIM/d(mu1, E[I^2], E[IG]) -> HBM; per-block partial sums (deterministic).
 // Backward: dSSIM_sum/dI = w*A + 2 I (w*B) + G (w*C) (window symmetric), plus the L1 sign term.
@@ -15,9 +16,13 @@
 namespace dgs {
 namespace ssim {
 
-constexpr int T = 16;            // output tile
+constexpr int T = 32;            // output tile (32 x 32 pixels per 256-thread workgroup)
 constexpr int R = 5;             // window radius
-constexpr int S = T + 2 * R;     // 26: input tile with halo
+constexpr int S = T + 2 * R;     // 42: input tile with halo
+constexpr int SP = S + 1;        // padded LDS row of the input tile
+constexpr int HP = T + 1;        // padded LDS row of the row-filtered maps
+constexpr int HX = 8;            // row pass: outputs per thread (one row, 8 columns: 168 items)
+constexpr int VY = 4;            // column pass: outputs per thread (one column, 4 rows: 256 items)
 constexpr float C1 = 0.01f * 0.01f;
 constexpr float C2 = 0.03f * 0.03f;
 
@@ -31,68 +36,100 @@ __device__ inline float wave_sum(float v) {
     return v;
 }
 
+// NM maps of the halo tile (zero outside the image) from `src` planes (plane stride `plane`) into
+// LDS, 42 x 42 each
+template <int NM>
+__device__ __forceinline__ void load_tile(float (*sm)[S][SP], const float *const src[NM], int H, int W, int x0,
+                                          int y0) {
+    for (int e = threadIdx.x; e < S * S; e += 256) {
+        const int ly = e / S, lx = e - ly * S;
+        const int gy = y0 + ly - R, gx = x0 + lx - R;
+        const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
+        const size_t p = (size_t)gy * W + gx;
+#pragma unroll
+        for (int q = 0; q < NM; q++) sm[q][ly][lx] = in ? src[q][p] : 0.f;
+    }
+}
+
+// forward: 5 maps (mu1, mu2, E[I^2], E[G^2], E[IG]); the products are formed on the fly from the two
+// input tiles. Row pass: each item = one tile row x 8 columns from 18 inputs held in registers;
+// column pass: each thread slides 14 row-filtered values down one column for 4 outputs.
 // block (tile) partial sums: [blocks][2] = (sum |I-G|, sum ssim)
 __global__ __launch_bounds__(256) void k_ssim_fwd(int H, int W, const float *__restrict__ I, const float *__restrict__ G,
                                                   Win win, float *__restrict__ maps, float *__restrict__ partial) {
-    __shared__ float sI[S][S + 1], sG[S][S + 1];
-    __shared__ float hq[5][S][T + 1];
+    __shared__ float sx[2][S][SP];
+    __shared__ float hq[5][S][HP];
     __shared__ float red[2][4];
     const int c = blockIdx.z;
     const int x0 = blockIdx.x * T, y0 = blockIdx.y * T;
     const int tid = threadIdx.x;
     const size_t plane = (size_t)H * W;
-    const float *Ic = I + c * plane, *Gc = G + c * plane;
-    for (int e = tid; e < S * S; e += 256) {
-        int ly = e / S, lx = e % S;
-        int gy = y0 + ly - R, gx = x0 + lx - R;
-        bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
-        sI[ly][lx] = in ? Ic[(size_t)gy * W + gx] : 0.f;
-        sG[ly][lx] = in ? Gc[(size_t)gy * W + gx] : 0.f;
-    }
+    const float *src[2] = {I + c * plane, G + c * plane};
+    load_tile<2>(sx, src, H, W, x0, y0);
     __syncthreads();
-    for (int e = tid; e < S * T; e += 256) {
-        int ly = e / T, lx = e % T;
-        float a = 0.f, b = 0.f, aa = 0.f, bb = 0.f, ab = 0.f;
+    if (tid < S * (T / HX)) {
+        const int ly = tid / (T / HX), lx0 = (tid % (T / HX)) * HX;
+        float a[HX + 10], b[HX + 10];
 #pragma unroll
-        for (int k = 0; k < 11; k++) {
-            float i = sI[ly][lx + k], g = sG[ly][lx + k], w = win.w[k];
-            a += w * i;
-            b += w * g;
-            aa += w * (i * i);
-            bb += w * (g * g);
-            ab += w * (i * g);
+        for (int k = 0; k < HX + 10; k++) {
+            a[k] = sx[0][ly][lx0 + k];
+            b[k] = sx[1][ly][lx0 + k];
         }
-        hq[0][ly][lx] = a; hq[1][ly][lx] = b; hq[2][ly][lx] = aa; hq[3][ly][lx] = bb; hq[4][ly][lx] = ab;
+#pragma unroll
+        for (int j = 0; j < HX; j++) {
+            float m0 = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f, m4 = 0.f;
+#pragma unroll
+            for (int k = 0; k < 11; k++) {
+                const float i = a[j + k], g = b[j + k], w = win.w[k];
+                m0 += w * i;
+                m1 += w * g;
+                m2 += w * (i * i);
+                m3 += w * (g * g);
+                m4 += w * (i * g);
+            }
+            hq[0][ly][lx0 + j] = m0; hq[1][ly][lx0 + j] = m1; hq[2][ly][lx0 + j] = m2;
+            hq[3][ly][lx0 + j] = m3; hq[4][ly][lx0 + j] = m4;
+        }
     }
     __syncthreads();
-    const int lx = tid % T, ly = tid / T;
-    const int x = x0 + lx, y = y0 + ly;
-    float mu1 = 0.f, mu2 = 0.f, m11 = 0.f, m22 = 0.f, m12 = 0.f;
+    const int lx = tid % T, ly0 = (tid / T) * VY;
+    const int x = x0 + lx;
+    float mu[5][VY];
 #pragma unroll
-    for (int k = 0; k < 11; k++) {
-        float w = win.w[k];
-        mu1 += w * hq[0][ly + k][lx];
-        mu2 += w * hq[1][ly + k][lx];
-        m11 += w * hq[2][ly + k][lx];
-        m22 += w * hq[3][ly + k][lx];
-        m12 += w * hq[4][ly + k][lx];
+    for (int m = 0; m < 5; m++) {
+        float v[VY + 10];
+#pragma unroll
+        for (int k = 0; k < VY + 10; k++) v[k] = hq[m][ly0 + k][lx];
+#pragma unroll
+        for (int j = 0; j < VY; j++) {
+            float acc = 0.f;
+#pragma unroll
+            for (int k = 0; k < 11; k++) acc += win.w[k] * v[j + k];
+            mu[m][j] = acc;
+        }
     }
     float l1 = 0.f, s = 0.f;
-    if (x < W && y < H) {
-        float mu1s = mu1 * mu1, mu2s = mu2 * mu2, mu12 = mu1 * mu2;
-        float s11 = m11 - mu1s, s22 = m22 - mu2s, s12 = m12 - mu12;
-        float n1 = 2.f * mu12 + C1, n2 = 2.f * s12 + C2;
-        float d1 = mu1s + mu2s + C1, d2 = s11 + s22 + C2;
-        float inv = 1.f / (d1 * d2);
-        s = n1 * n2 * inv;
-        float A = 2.f * mu2 * n2 * inv - 2.f * mu1 * s / d1 + 2.f * mu1 * s / d2 - mu2 * 2.f * n1 * inv;
-        float B = -s / d2;
-        float Cc = 2.f * n1 * inv;
-        size_t p = (size_t)y * W + x;
-        maps[(3 * c + 0) * plane + p] = A;
-        maps[(3 * c + 1) * plane + p] = B;
-        maps[(3 * c + 2) * plane + p] = Cc;
-        l1 = fabsf(sI[ly + R][lx + R] - sG[ly + R][lx + R]);
+#pragma unroll
+    for (int j = 0; j < VY; j++) {
+        const int y = y0 + ly0 + j;
+        if (x < W && y < H) {
+            const float mu1 = mu[0][j], mu2 = mu[1][j];
+            const float mu1s = mu1 * mu1, mu2s = mu2 * mu2, mu12 = mu1 * mu2;
+            const float s11 = mu[2][j] - mu1s, s22 = mu[3][j] - mu2s, s12 = mu[4][j] - mu12;
+            const float n1 = 2.f * mu12 + C1, n2 = 2.f * s12 + C2;
+            const float d1 = mu1s + mu2s + C1, d2 = s11 + s22 + C2;
+            const float inv = 1.f / (d1 * d2);
+            const float sv = n1 * n2 * inv;
+            const float A = 2.f * mu2 * n2 * inv - 2.f * mu1 * sv / d1 + 2.f * mu1 * sv / d2 - mu2 * 2.f * n1 * inv;
+            const float B = -sv / d2;
+            const float Cc = 2.f * n1 * inv;
+            const size_t p = (size_t)y * W + x;
+            maps[(3 * c + 0) * plane + p] = A;
+            maps[(3 * c + 1) * plane + p] = B;
+            maps[(3 * c + 2) * plane + p] = Cc;
+            l1 += fabsf(sx[0][ly0 + j + R][lx + R] - sx[1][ly0 + j + R][lx + R]);
+            s += sv;
+        }
     }
     l1 = wave_sum(l1);
     s = wave_sum(s);
@@ -142,55 +179,63 @@ __global__ __launch_bounds__(1024) void k_ssim_final(int nblocks, float n, float
     }
 }
 
-// grad = dloss * [ (1-l)/n sign(I-G) - l/n (w*A + 2 I w*B + G w*C) ]
+// grad = dloss * [ (1-l)/n sign(I-G) - l/n (w*A + 2 I w*B + G w*C) ]  (same row / column passes)
 __global__ __launch_bounds__(256) void k_ssim_bwd(int H, int W, const float *__restrict__ I, const float *__restrict__ G,
                                                   const float *__restrict__ maps, Win win, float wl1, float wss,
                                                   const float *__restrict__ dloss, float *__restrict__ grad) {
-    __shared__ float sm[3][S][S + 1];
-    __shared__ float hq[3][S][T + 1];
+    __shared__ float sm[3][S][SP];
+    __shared__ float hq[3][S][HP];
     const int c = blockIdx.z;
     const int x0 = blockIdx.x * T, y0 = blockIdx.y * T;
     const int tid = threadIdx.x;
     const size_t plane = (size_t)H * W;
-    for (int e = tid; e < S * S; e += 256) {
-        int ly = e / S, lx = e % S;
-        int gy = y0 + ly - R, gx = x0 + lx - R;
-        bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
-        size_t p = (size_t)gy * W + gx;
-#pragma unroll
-        for (int q = 0; q < 3; q++) sm[q][ly][lx] = in ? maps[(3 * c + q) * plane + p] : 0.f;
-    }
+    const float *src[3] = {maps + (3 * c) * plane, maps + (3 * c + 1) * plane, maps + (3 * c + 2) * plane};
+    load_tile<3>(sm, src, H, W, x0, y0);
     __syncthreads();
-    for (int e = tid; e < S * T; e += 256) {
-        int ly = e / T, lx = e % T;
-        float a = 0.f, b = 0.f, cc = 0.f;
+    if (tid < S * (T / HX)) {
+        const int ly = tid / (T / HX), lx0 = (tid % (T / HX)) * HX;
 #pragma unroll
-        for (int k = 0; k < 11; k++) {
-            float w = win.w[k];
-            a += w * sm[0][ly][lx + k];
-            b += w * sm[1][ly][lx + k];
-            cc += w * sm[2][ly][lx + k];
+        for (int m = 0; m < 3; m++) {
+            float v[HX + 10];
+#pragma unroll
+            for (int k = 0; k < HX + 10; k++) v[k] = sm[m][ly][lx0 + k];
+#pragma unroll
+            for (int j = 0; j < HX; j++) {
+                float acc = 0.f;
+#pragma unroll
+                for (int k = 0; k < 11; k++) acc += win.w[k] * v[j + k];
+                hq[m][ly][lx0 + j] = acc;
+            }
         }
-        hq[0][ly][lx] = a; hq[1][ly][lx] = b; hq[2][ly][lx] = cc;
     }
     __syncthreads();
-    const int lx = tid % T, ly = tid / T;
-    const int x = x0 + lx, y = y0 + ly;
-    if (x >= W || y >= H) return;
-    float fa = 0.f, fb = 0.f, fc = 0.f;
+    const int lx = tid % T, ly0 = (tid / T) * VY;
+    const int x = x0 + lx;
+    float f[3][VY];
 #pragma unroll
-    for (int k = 0; k < 11; k++) {
-        float w = win.w[k];
-        fa += w * hq[0][ly + k][lx];
-        fb += w * hq[1][ly + k][lx];
-        fc += w * hq[2][ly + k][lx];
+    for (int m = 0; m < 3; m++) {
+        float v[VY + 10];
+#pragma unroll
+        for (int k = 0; k < VY + 10; k++) v[k] = hq[m][ly0 + k][lx];
+#pragma unroll
+        for (int j = 0; j < VY; j++) {
+            float acc = 0.f;
+#pragma unroll
+            for (int k = 0; k < 11; k++) acc += win.w[k] * v[j + k];
+            f[m][j] = acc;
+        }
     }
-    size_t p = c * plane + (size_t)y * W + x;
-    float i = I[p], g = G[p];
-    float d = i - g;
-    float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
-    float dl = dloss ? dloss[0] : 1.f;
-    grad[p] = dl * (wl1 * sg - wss * (fa + 2.f * i * fb + g * fc));
+    const float dl = dloss ? dloss[0] : 1.f;
+#pragma unroll
+    for (int j = 0; j < VY; j++) {
+        const int y = y0 + ly0 + j;
+        if (x >= W || y >= H) continue;
+        const size_t p = c * plane + (size_t)y * W + x;
+        const float i = I[p], g = G[p];
+        const float d = i - g;
+        const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+        grad[p] = dl * (wl1 * sg - wss * (f[0][j] + 2.f * i * f[1][j] + g * f[2][j]));
+    }
 }
 
 Win make_window() {

@@ -24,32 +24,58 @@ class Adam(torch.optim.Adam):
                              "Gaussian and deformation optimizers use none)")
 
     def _collect(self, out):
-        """Append (betas, eps, AdamTensor) for every parameter with a gradient; advances 'step'."""
+        """Append (betas, eps, AdamTensor) for every parameter with a gradient; advances 'step'.
+
+        Per-parameter "step" state stays a CPU tensor (torch.optim.Adam's layout), but parameters
+        that always step together share ONE step tensor (created for the optimizer's first step), so
+        a step costs one tensor update per optimizer instead of one per parameter (each CPU tensor op
+        is several microseconds of host time). A parameter without a gradient while its step tensor
+        is shared with stepping ones gets its own copy first, so the counts stay exactly torch's."""
         keep = []
+        stepping, idle = [], []
         for group in self.param_groups:
+            for p in group["params"]:
+                (stepping if p.grad is not None else idle).append((group, p))
+        if not stepping:
+            return keep
+        fresh = None
+        for group, p in stepping:
+            st = self.state[p]
+            if len(st) == 0:
+                if fresh is None:
+                    fresh = torch.tensor(0.0)
+                st["step"] = fresh
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+        moving = {id(self.state[p]["step"]) for _, p in stepping}
+        for _, p in idle:
+            st = self.state.get(p)
+            if st and id(st["step"]) in moving:
+                st["step"] = st["step"].clone()
+        counts = {}
+        for _, p in stepping:
+            t = self.state[p]["step"]
+            if id(t) not in counts:
+                v = float(t) + 1.0
+                t.fill_(v)
+                counts[id(t)] = v
+        for group, p in stepping:
             b1, b2 = group["betas"]
             lr, eps = float(group["lr"]), float(group["eps"])
-            for p in group["params"]:
-                g = p.grad
-                if g is None:
-                    continue
-                if g.is_sparse:
-                    raise RuntimeError("dgs Adam does not support sparse gradients")
-                st = self.state[p]
-                if len(st) == 0:
-                    st["step"] = torch.tensor(0.0)
-                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
-                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
-                st["step"] += 1
-                t = float(st["step"])
-                if not (p.is_contiguous() and st["exp_avg"].is_contiguous() and st["exp_avg_sq"].is_contiguous()):
-                    raise RuntimeError("dgs Adam: parameters and state must be contiguous")
-                if not g.is_contiguous():
-                    g = g.contiguous()
-                    keep.append(g)
-                d = _lib.AdamTensor(p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
-                                    p.numel(), lr / (1.0 - b1 ** t), math.sqrt(1.0 - b2 ** t))
-                out.append(((float(b1), float(b2), eps), d))
+            st = self.state[p]
+            t = counts[id(st["step"])]
+            m, v = st["exp_avg"], st["exp_avg_sq"]
+            g = p.grad
+            if g.is_sparse:
+                raise RuntimeError("dgs Adam does not support sparse gradients")
+            if not (p.is_contiguous() and m.is_contiguous() and v.is_contiguous()):
+                raise RuntimeError("dgs Adam: parameters and state must be contiguous")
+            if not g.is_contiguous():
+                g = g.contiguous()
+                keep.append(g)
+            d = _lib.AdamTensor(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(),
+                                lr / (1.0 - b1 ** t), math.sqrt(1.0 - b2 ** t))
+            out.append(((float(b1), float(b2), eps), d))
         return keep
 
     @torch.no_grad()
