@@ -1007,9 +1007,12 @@ __global__ __launch_bounds__(256) void k_dw_reduce(RJobs R, const float *__restr
             if (c >= J.seg[k].s0 && c < J.seg[k].s0 + J.seg[k].len) f = J.seg[k].p0 + (c - J.seg[k].s0);
         int kt = f / WT, kl = f % WT;
         const float *sl = slabs + (size_t)J.block0[kt] * SLAB + n * WT + kl;
+        // unrolled: the slab loads are issued together, the adds stay in slab order (deterministic)
+#pragma unroll 8
         for (int sp = 0; sp < J.nsplit[kt]; sp++) s += sl[(size_t)sp * SLAB];
     } else {
         const float *sl = slabs + (size_t)J.block0[0] * SLAB + WT * WT + n;
+#pragma unroll 8
         for (int sp = 0; sp < J.nsplit[0]; sp++) s += sl[(size_t)sp * SLAB];
     }
     J.dst[idx] = s;

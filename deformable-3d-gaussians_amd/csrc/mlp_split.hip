@@ -786,7 +786,7 @@ struct TGradArgs {
 };
 
 __global__ __launch_bounds__(1024) void k_tgrad(TGradArgs a) {
-    __shared__ float S[32], th[256];
+    __shared__ float S[32], th[256], dz1[256];
     const int j = threadIdx.x;
     if (j < 256) th[j] = a.tc[TC_TH + j];
     {  // S[k]: 32 lanes per k, each over 16 of the 512 (n, layer) terms, then a fixed xor tree
@@ -806,12 +806,26 @@ __global__ __launch_bounds__(1024) void k_tgrad(TGradArgs a) {
     __syncthreads();
     for (int e = j; e < 30 * 256; e += 1024) a.gT2w[e] = S[e >> 8] * th[e & 255];
     if (j < 30) a.gT2b[j] = S[j];
-    if (j < 256) {
+    {  // dZ_T1[n]: 4 lanes per n over 8 of the 30 (+2 zero) k terms each, then a fixed xor tree
+        const int n = j >> 2, q = j & 3;
         float d = 0.f;
-        for (int k = 0; k < 30; k++) d = fmaf(a.fp[a.wT2 + k * 256 + j], S[k], d);
-        d = th[j] > 0.f ? d : 0.f;
-        a.gT0b[j] = d;
-        for (int f = 0; f < a.tin; f++) a.gT0w[j * a.tin + f] = d * a.tc[TC_TIN + f];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int k = q * 8 + i;
+            if (k < 30) d = fmaf(a.fp[a.wT2 + k * 256 + n], S[k], d);
+        }
+        d += __shfl_xor(d, 1);
+        d += __shfl_xor(d, 2);
+        d = th[n] > 0.f ? d : 0.f;
+        if (q == 0) {
+            dz1[n] = d;
+            a.gT0b[n] = d;
+        }
+    }
+    __syncthreads();
+    for (int e = j; e < 256 * a.tin; e += 1024) {  // coalesced [256][tin] outer product
+        const int n = e / a.tin, f = e - n * a.tin;
+        a.gT0w[e] = dz1[n] * a.tc[TC_TIN + f];
     }
 }
 

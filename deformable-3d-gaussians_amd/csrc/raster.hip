@@ -540,7 +540,7 @@ __global__ __launch_bounds__(256) void k_blend_fwd(const uint2 *__restrict__ ran
     const int rounds = div_up(todo_total, TILE_PIX);
     bool done = !inside;
     float T = 1.f, C0 = 0.f, C1 = 0.f, C2 = 0.f, Dd = 0.f;
-    uint32_t contributor = 0, last = 0;
+    uint32_t last = 0;
     for (int r = 0; r < rounds; r++) {
         if (__syncthreads_count(done) == TILE_PIX) break;
         int prog = r * TILE_PIX + tid;
@@ -563,28 +563,30 @@ __global__ __launch_bounds__(256) void k_blend_fwd(const uint2 *__restrict__ ran
         }
         __syncthreads();
         const int n = sl.y;
-        for (int j = 0; !done && j < n; j++) {
-            contributor = (uint32_t)s_pos[j] + 1u;  // list position + 1 (n_contrib of the full list)
-            float2 g = s_xy[j];
-            float4 co = s_co[j];
-            float dx = g.x - pfx, dy = g.y - pfy;
-            float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-            if (power > 0.f) continue;
-            float alpha = fminf(0.99f, co.w * __expf(power));
-            if (alpha < 1.f / 255.f) continue;
-            float testT = T * (1.f - alpha);
-            if (testT < 0.0001f) {
-                done = true;
-                continue;
-            }
-            float4 cd = s_cd[j];
-            float w = alpha * T;
+        // branch-free per lane (a skipped Gaussian adds cd * 0): the skips and the stop of the
+        // reference's loop become predicates, so the wave runs no exec-mask bookkeeping per
+        // Gaussian; it leaves the batch once all of its lanes are done
+        for (int j = 0; j < n; j++) {
+            if (__ballot(!done) == 0ull) break;
+            const float2 g = s_xy[j];
+            const float4 co = s_co[j];
+            const float4 cd = s_cd[j];
+            const uint32_t pos1 = (uint32_t)s_pos[j] + 1u;  // list position + 1 (n_contrib of the full list)
+            const float dx = g.x - pfx, dy = g.y - pfy;
+            const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+            const float alpha = fminf(0.99f, co.w * __expf(power));
+            const float testT = T * (1.f - alpha);
+            bool use = !done && !(power > 0.f) && !(alpha < 1.f / 255.f);
+            const bool stop = use && testT < 0.0001f;
+            done = done || stop;
+            use = use && !stop;
+            const float w = use ? alpha * T : 0.f;
             C0 += cd.x * w;
             C1 += cd.y * w;
             C2 += cd.z * w;
             Dd += cd.w * w;
-            T = testT;
-            last = contributor;
+            T = use ? testT : T;
+            last = use ? pos1 : last;
         }
     }
     if (inside) {
