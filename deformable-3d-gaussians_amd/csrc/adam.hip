@@ -59,20 +59,31 @@ __global__ __launch_bounds__(THREADS) void k_adam(Jobs J) {
                        reinterpret_cast<uintptr_t>(T.m) | reinterpret_cast<uintptr_t>(T.v)) & 15) == 0;
     const long long e0 = (b - T.block0) * BLOCK_ELEMS;
     if (vec && e0 + BLOCK_ELEMS <= T.n) {
+        constexpr int U = PER_THREAD / 4;
+        float4 p[U], g[U], m[U], v[U];
+        // every load of the thread first (the stores could alias other tensors' loads for the
+        // compiler), then the updates, then the stores
 #pragma unroll
-        for (int k = 0; k < PER_THREAD / 4; k++) {
+        for (int k = 0; k < U; k++) {
             const long long i = e0 + 4ll * (threadIdx.x + k * THREADS);
-            float4 p = *reinterpret_cast<const float4 *>(T.p + i);
-            const float4 g = *reinterpret_cast<const float4 *>(T.g + i);
-            float4 m = *reinterpret_cast<const float4 *>(T.m + i);
-            float4 v = *reinterpret_cast<const float4 *>(T.v + i);
-            adam1(p.x, g.x, m.x, v.x, c1, b2, c2, eps, ss, bc);
-            adam1(p.y, g.y, m.y, v.y, c1, b2, c2, eps, ss, bc);
-            adam1(p.z, g.z, m.z, v.z, c1, b2, c2, eps, ss, bc);
-            adam1(p.w, g.w, m.w, v.w, c1, b2, c2, eps, ss, bc);
-            *reinterpret_cast<float4 *>(T.p + i) = p;
-            *reinterpret_cast<float4 *>(T.m + i) = m;
-            *reinterpret_cast<float4 *>(T.v + i) = v;
+            p[k] = *reinterpret_cast<const float4 *>(T.p + i);
+            g[k] = *reinterpret_cast<const float4 *>(T.g + i);
+            m[k] = *reinterpret_cast<const float4 *>(T.m + i);
+            v[k] = *reinterpret_cast<const float4 *>(T.v + i);
+        }
+#pragma unroll
+        for (int k = 0; k < U; k++) {
+            adam1(p[k].x, g[k].x, m[k].x, v[k].x, c1, b2, c2, eps, ss, bc);
+            adam1(p[k].y, g[k].y, m[k].y, v[k].y, c1, b2, c2, eps, ss, bc);
+            adam1(p[k].z, g[k].z, m[k].z, v[k].z, c1, b2, c2, eps, ss, bc);
+            adam1(p[k].w, g[k].w, m[k].w, v[k].w, c1, b2, c2, eps, ss, bc);
+        }
+#pragma unroll
+        for (int k = 0; k < U; k++) {
+            const long long i = e0 + 4ll * (threadIdx.x + k * THREADS);
+            *reinterpret_cast<float4 *>(T.p + i) = p[k];
+            *reinterpret_cast<float4 *>(T.m + i) = m[k];
+            *reinterpret_cast<float4 *>(T.v + i) = v[k];
         }
         return;
     }

@@ -128,7 +128,8 @@ __global__ __launch_bounds__(256) void k_preprocess(
     const float *view, const float *proj, const float *campos, int W, int H, float tanx, float tany, float fx, float fy,
     int gx, int gy, int *__restrict__ radii, float2 *__restrict__ xy, float4 *__restrict__ conic_o,
     float4 *__restrict__ rgbd, uint32_t *__restrict__ tiles, uint8_t *__restrict__ clamped,
-    uint32_t *__restrict__ dkey, uint32_t *__restrict__ gid, float4 *__restrict__ acc) {
+    uint32_t *__restrict__ dkey, uint32_t *__restrict__ gid, float4 *__restrict__ acc,
+    uint8_t *__restrict__ visible) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     [[maybe_unused]] const float *s_row = nullptr;
     if constexpr (STAGE) {
@@ -145,6 +146,7 @@ __global__ __launch_bounds__(256) void k_preprocess(
     Cam cam;
     load_cam(cam, view, proj, campos);
     radii[i] = 0;
+    if (visible) visible[i] = 0;  // render()'s visibility_filter (radii > 0), when asked for
     tiles[i] = 0;
     dkey[i] = 0xffffffffu;  // culled: sorts last, emits no pairs
     gid[i] = (uint32_t)i;
@@ -215,6 +217,7 @@ __global__ __launch_bounds__(256) void k_preprocess(
         rgb = make_float3(r[0], r[1], r[2]);
     }
     radii[i] = rad;
+    if (visible) visible[i] = rad > 0;
     xy[i] = make_float2(px, py);
     conic_o[i] = make_float4(con.x, con.y, con.z, opac[i]);
     rgbd[i] = make_float4(rgb.x, rgb.y, rgb.z, pv.z);
@@ -1434,7 +1437,7 @@ static int raster_forward(const dgs_raster_settings *s, int P, int M, const floa
                           const float *shs_rest, const float *colors_precomp, const float *opacities,
                           const float *scales, const float *rotations, const float *cov3D_precomp, float *out_color,
                           float *out_depth, int *out_radii, dgs_raster_ctx **ctx_out, int *num_rendered,
-                          void *stream_) {
+                          void *stream_, uint8_t *out_visible = nullptr) {
     hipStream_t stream = (hipStream_t)stream_;
     if (shs_rest && (M * 3 != SH_ROW || !shs || ((reinterpret_cast<uintptr_t>(shs) | reinterpret_cast<uintptr_t>(shs_rest)) & 15))) {
         set_error("dgs_raster_forward_split_sh: needs M = 16 and 16-byte aligned features_dc / features_rest");
@@ -1534,7 +1537,8 @@ static int raster_forward(const dgs_raster_settings *s, int P, int M, const floa
                                P, s->sh_degree, M, means3D, scales,
                                s->scale_modifier, rotations, cov3D_precomp, opacities, shs, shs_rest, colors_precomp, s->viewmatrix,
                                s->projmatrix, s->campos, c->W, c->H, s->tanfovx, s->tanfovy, fx, fy, c->gx, c->gy, out_radii,
-                               c->xy, c->conic_o, c->rgbd, c->tiles, c->clamped, c->dkey, c->gid, (float4 *)c->acc.p);
+                               c->xy, c->conic_o, c->rgbd, c->tiles, c->clamped, c->dkey, c->gid, (float4 *)c->acc.p,
+                               out_visible);
         }
         DGS_LAUNCH_CHECK("k_preprocess", dbg, stream);
         {
@@ -1688,13 +1692,15 @@ extern "C" int dgs_raster_forward_split_sh(const dgs_raster_settings *s, int P, 
                                            const float *features_dc, const float *features_rest,
                                            const float *opacities, const float *scales, const float *rotations,
                                            float *out_color, float *out_depth, int *out_radii,
-                                           dgs_raster_ctx **ctx_out, int *num_rendered, void *stream) {
+                                           uint8_t *out_visible, dgs_raster_ctx **ctx_out, int *num_rendered,
+                                           void *stream) {
     if (P > 0 && (!features_dc || !features_rest)) {
         set_error("dgs_raster_forward_split_sh: null SH argument");
         return DGS_ERR_ARGS;
     }
     return raster_forward(s, P, SH_ROW / 3, means3D, features_dc, P > 0 ? features_rest : nullptr, nullptr, opacities,
-                          scales, rotations, nullptr, out_color, out_depth, out_radii, ctx_out, num_rendered, stream);
+                          scales, rotations, nullptr, out_color, out_depth, out_radii, ctx_out, num_rendered, stream,
+                          out_visible);
 }
 
 extern "C" int dgs_raster_backward(dgs_raster_ctx *c, const float *dL_dcolor, const float *dL_ddepth,

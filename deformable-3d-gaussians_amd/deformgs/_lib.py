@@ -46,7 +46,7 @@ _SIGS = {
     "dgs_version": ([], ctypes.c_char_p),
     "dgs_raster_forward": ([ctypes.POINTER(RasterSettings), I, I] + [P] * 10 + [ctypes.POINTER(P), ctypes.POINTER(I), P], I),
     "dgs_raster_backward": ([P] * 12 + [P], I),
-    "dgs_raster_forward_split_sh": ([ctypes.POINTER(RasterSettings), I] + [P] * 9 + [ctypes.POINTER(P), ctypes.POINTER(I), P], I),
+    "dgs_raster_forward_split_sh": ([ctypes.POINTER(RasterSettings), I] + [P] * 10 + [ctypes.POINTER(P), ctypes.POINTER(I), P], I),
     "dgs_raster_backward_split_sh": ([P] * 11 + [P], I),
     "dgs_raster_ctx_free": ([P], None),
     "dgs_mark_visible": ([I, P, P, P, P, P], I),

@@ -84,7 +84,9 @@ class Camera:
         self.projection_matrix = getProjectionMatrix(self.znear, self.zfar, FoVx, FoVy).transpose(0, 1).to(dev)
         self.full_proj_transform = self.world_view_transform.unsqueeze(0).bmm(
             self.projection_matrix.unsqueeze(0)).squeeze(0)
-        self.camera_center = self.world_view_transform.inverse()[3, :3]
+        # (the inverse comes back column-major: its row is a strided view; stored contiguous for the
+        # same reason as above)
+        self.camera_center = self.world_view_transform.inverse()[3, :3].contiguous()
 
 
 class MiniCam:
@@ -94,7 +96,7 @@ class MiniCam:
         self.znear, self.zfar = znear, zfar
         self.world_view_transform = world_view_transform
         self.full_proj_transform = full_proj_transform
-        self.camera_center = torch.inverse(world_view_transform)[3][:3]
+        self.camera_center = torch.inverse(world_view_transform)[3][:3].contiguous()
 
 
 def orbit_camera(azimuth, elevation, radius, fov, width, height, fid=0.0, data_device="cuda"):

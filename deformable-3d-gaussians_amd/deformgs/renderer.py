@@ -168,15 +168,16 @@ def render(viewpoint_camera, pc, pipe, bg_color, d_xyz, d_rotation, d_scaling, i
             pc._xyz, pc._features_dc, pc._features_rest, pc._scaling, pc._rotation, pc._opacity,
             rows if torch.is_tensor(rows) else None, se3, not split)
         if split:  # SH rows read / written in place by the rasterizer (no (N, 16, 3) cat either way)
-            rendered_image, radii, depth = rasterize_gaussians_split_sh(
+            rendered_image, radii, depth, visible = rasterize_gaussians_split_sh(
                 means3D, screenspace_points, screenspace_points_densify, pc._features_dc, pc._features_rest, opacity,
                 scales, rotations, raster_settings)
         else:
             rendered_image, radii, depth = rasterizer(
                 means3D=means3D, means2D=screenspace_points, means2D_densify=screenspace_points_densify, shs=shs,
                 colors_precomp=None, opacities=opacity, scales=scales, rotations=rotations, cov3D_precomp=None)
+            visible = radii > 0
         return {"render": rendered_image, "viewspace_points": screenspace_points,
-                "viewspace_points_densify": screenspace_points_densify, "visibility_filter": radii > 0,
+                "viewspace_points_densify": screenspace_points_densify, "visibility_filter": visible,
                 "radii": radii, "depth": depth}
     if direct_compute:
         means3D = d_xyz

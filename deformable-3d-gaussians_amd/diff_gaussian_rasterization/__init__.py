@@ -186,12 +186,13 @@ class _RasterizeGaussiansSplitSH(torch.autograd.Function):
         color = torch.empty((3, H, W), dtype=torch.float32, device=dev)
         depth = torch.empty((1, H, W), dtype=torch.float32, device=dev)
         radii = torch.empty((P,), dtype=torch.int32, device=dev)
+        visible = torch.empty((P,), dtype=torch.bool, device=dev)  # radii > 0, written by the preprocess
         handle = _lib.P()
         nr = _lib.I(0)
         rc = lib.dgs_raster_forward_split_sh(s, P, _lib.ptr(means3D), _lib.ptr(f_dc), _lib.ptr(f_rest),
                                              _lib.ptr(opacities), _lib.ptr(scales), _lib.ptr(rotations),
-                                             _lib.ptr(color), _lib.ptr(depth), _lib.ptr(radii), handle, nr,
-                                             _lib.stream_ptr(dev))
+                                             _lib.ptr(color), _lib.ptr(depth), _lib.ptr(radii), _lib.ptr(visible),
+                                             handle, nr, _lib.stream_ptr(dev))
         _lib.check(rc, "rasterize_gaussians")
         ctx.raster = _Ctx(handle)
         ctx.raster_hw = (H, W)
@@ -200,12 +201,12 @@ class _RasterizeGaussiansSplitSH(torch.autograd.Function):
         ctx.P = P
         # the saved C context points at these inputs: keep them alive (and version-checked) until backward
         ctx.save_for_backward(radii, means3D, f_dc, f_rest, opacities, scales, rotations)
-        ctx.mark_non_differentiable(radii)
+        ctx.mark_non_differentiable(radii, visible)
         ctx.set_materialize_grads(False)
-        return color, radii, depth
+        return color, radii, depth, visible
 
     @staticmethod
-    def backward(ctx, grad_color, grad_radii, grad_depth):
+    def backward(ctx, grad_color, grad_radii, grad_depth, grad_visible):
         lib = _lib.load()
         radii = ctx.saved_tensors[0]
         P, dev = ctx.P, radii.device
@@ -236,6 +237,7 @@ def split_sh_ok(f_dc, f_rest):
 
 def rasterize_gaussians_split_sh(means3D, means2D, means2D_densify, f_dc, f_rest, opacities, scales, rotations,
                                  raster_settings):
+    """-> (color, radii, depth, visible = radii > 0)"""
     return _RasterizeGaussiansSplitSH.apply(means3D, means2D, means2D_densify, f_dc, f_rest, opacities, scales,
                                             rotations, raster_settings)
 

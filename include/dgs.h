@@ -90,11 +90,13 @@ int dgs_raster_backward(dgs_raster_ctx *ctx, const float *dL_dcolor, const float
  * them per call; here the preprocess kernels read and write both tensors directly, so no (P,16,3)
  * copy is made either way). Degree <= 3, 16 coefficients; all four SH pointers 16-byte aligned.
  * Same outputs and semantics as dgs_raster_forward(shs = cat(features_dc, features_rest)); the
- * backward writes the two SH gradients. */
+ * backward writes the two SH gradients. out_visible (P bytes, may be NULL) receives radii > 0, render()'s
+ * visibility_filter (gaussian_renderer/__init__.py:130), from the preprocess kernel itself. */
 int dgs_raster_forward_split_sh(const dgs_raster_settings *s, int P, const float *means3D,
                                 const float *features_dc, const float *features_rest, const float *opacities,
                                 const float *scales, const float *rotations, float *out_color, float *out_depth,
-                                int *out_radii, dgs_raster_ctx **ctx, int *num_rendered, void *stream);
+                                int *out_radii, uint8_t *out_visible, dgs_raster_ctx **ctx, int *num_rendered,
+                                void *stream);
 int dgs_raster_backward_split_sh(dgs_raster_ctx *ctx, const float *dL_dcolor, const float *dL_ddepth,
                                  float *dL_dmeans3D, float *dL_dmeans2D, float *dL_dmeans2D_densify,
                                  float *dL_dopacity, float *dL_dfeatures_dc, float *dL_dfeatures_rest,

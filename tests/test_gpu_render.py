@@ -146,6 +146,9 @@ def test_split_sh_raster_matches_concatenated(degree, monkeypatch):
     (a, ga), (b, gb) = res
     assert torch.equal(a["render"], b["render"]) and torch.equal(a["radii"], b["radii"])
     assert torch.equal(a["depth"], b["depth"])
+    # visibility_filter: written by the preprocess kernel on the split path, radii > 0 on the other
+    assert a["visibility_filter"].dtype == torch.bool and torch.equal(a["visibility_filter"], b["visibility_filter"])
+    assert torch.equal(a["visibility_filter"], a["radii"] > 0)
     for n, x, y in zip(["xyz", "f_dc", "f_rest", "scaling", "rotation", "opacity", "deform"], ga, gb):
         scale = y.abs().max().clamp_min(1e-12)
         assert ((x - y).abs().max() / scale) < 1e-5, n
