@@ -618,13 +618,17 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
     }
     DGS_STAMP(20);
     // ---- heads (no activation): [warp | branch_w, branch_v], rotation, scaling: 16 rows (nout <= 13),
-    // one column tile per wave on waves 0-3, once all 8 layers' writers have signalled ----
-    if (r < NQB) {
+    // one column tile per wave, once all 8 layers' writers have signalled ----
+    // on the LAST wave of each SIMD (waves NWAVE - NQB ..): they finish layer 7 last (the MFMA pipe
+    // serves the oldest wave of a SIMD first), so they start the heads without waiting on a signal,
+    // while the earlier waves are already done
+    const int hq = r - (NWAVE - NQB);
+    if (hq >= 0) {
         f32x4 c1[1] = {zero4()};
-        gemm<8, 1>(a.img + (size_t)a.fHd * KSLOT, lds, G_H, r, lane, c1, NoPre(), HGate{hwr, hrd, 0, 16u, false, lane});
+        gemm<8, 1>(a.img + (size_t)a.fHd * KSLOT, lds, G_H, hq, lane, c1, NoPre(), HGate{hwr, hrd, 0, 16u, false, lane});
         const float4 b = load_bias4(a.fp + a.bHd, 0, lane);
         c1[0] += f32x4{b.x, b.y, b.z, b.w};
-        const int p = p0 + 16 * r + col;
+        const int p = p0 + 16 * hq + col;
 #pragma unroll
         for (int i = 0; i < 4; i++)
             if (p < pend && 4 * kq + i < F.nout) a.out[(size_t)p * F.nout + 4 * kq + i] = c1[0][i];
