@@ -634,7 +634,7 @@ __device__ inline float row_sum15(float v) {
 }
 
 __global__ __launch_bounds__(256) void k_blend_bwd(const uint2 *__restrict__ ranges, const uint32_t *__restrict__ vals,
-                                                   int W, int H, int gx, const float *bg,
+                                                   uint32_t cap, int W, int H, int gx, const float *bg,
                                                    const float2 *__restrict__ xy, const float4 *__restrict__ conic_o,
                                                    const float4 *__restrict__ rgbd, const float *__restrict__ final_T,
                                                    const uint32_t *__restrict__ n_contrib,
@@ -655,7 +655,9 @@ __global__ __launch_bounds__(256) void k_blend_bwd(const uint2 *__restrict__ ran
     const int py = (tile / gx) * TILE_Y + (tid / TILE_X);
     const bool inside = px < W && py < H;
     const float pfx = (float)px, pfy = (float)py;
-    const uint2 range = ranges[tile];
+    uint2 range = ranges[tile];
+    range.x = min(range.x, cap);  // a deferred count not resolved yet: the launched capacity bounds the list
+    range.y = min(range.y, cap);
     const int pid = py * W + px;
     const int HW = H * W;
     float Tfinal = 1.f, dp0 = 0.f, dp1 = 0.f, dp2 = 0.f, ddep = 0.f;
@@ -1653,14 +1655,18 @@ static int raster_backward(dgs_raster_ctx *c, const float *dL_dcolor, const floa
     const int P = c->P;
     c->last_stream = stream;
     if (P == 0) return DGS_OK;
-    if (int rc = resolve_count(c, stream)) return rc;
+    // A deferred pair count stays unresolved here (the host does not wait mid-step): the blend
+    // backward clips the tile ranges to the speculative capacity the binning ran with, which is exact
+    // unless it overflowed; dgs_raster_ctx_free resolves the count and counts an overflow (the
+    // caller then redoes the step).
+    const uint32_t cap = c->count_pending ? (uint32_t)c->spec_cap : (uint32_t)c->num_rendered;
     const bool dbg = c->s.debug != 0;
     const int T = c->gx * c->gy;
     float *acc = (float *)c->acc.p;  // [P][12], zeroed by the forward's k_preprocess
-    if (c->num_rendered > 0) {
+    if (cap > 0) {
         ScopedTimer tm("blend_bwd", stream);
-        hipLaunchKernelGGL(k_blend_bwd, dim3(T), dim3(TILE_PIX), 0, stream, c->ranges, c->vals, c->W, c->H, c->gx, c->s.bg,
-                           c->xy, c->conic_o, c->rgbd, c->final_T, c->n_contrib, dL_dcolor, dL_ddepth, acc);
+        hipLaunchKernelGGL(k_blend_bwd, dim3(T), dim3(TILE_PIX), 0, stream, c->ranges, c->vals, cap, c->W, c->H, c->gx,
+                           c->s.bg, c->xy, c->conic_o, c->rgbd, c->final_T, c->n_contrib, dL_dcolor, dL_ddepth, acc);
     }
     DGS_LAUNCH_CHECK("k_blend_bwd", dbg, stream);
     const float fx = c->W / (2.f * c->s.tanfovx), fy = c->H / (2.f * c->s.tanfovy);

@@ -3,6 +3,8 @@ harness): deform -> render -> 0.8*L1 + 0.2*(1-SSIM) -> backward [-> grad all-red
 """
 import torch
 
+import diff_gaussian_rasterization as dgr
+
 from . import _lib
 from .adam import step_all
 from .loss import l1_ssim_loss
@@ -16,8 +18,9 @@ def forward_backward(gaussians, deform, cam, gt_image, pipe, background, is_6dof
                      warm=True, ast_noise=0.0, deferred_count=False):
     """train_baseline.py:104-128 (timed span of the reference's iter_start/iter_end events).
 
-    deferred_count: the rasterizer's forward does not wait for num_rendered (the host keeps issuing
-    the loss and the backward); if the speculative pair capacity overflowed, `deferred_overflowed()`
+    deferred_count: the rasterizer does not wait for num_rendered in the forward nor in the backward
+    (the host keeps issuing the loss and the whole backward; the count is read once that is queued);
+    if the speculative pair capacity overflowed, `deferred_overflowed()`
     is True afterwards and the caller must redo the step with deferred_count=False after dropping
     the gradients (`drop_grads`; bench.py). Single-rank only: with several ranks a redo must be
     agreed on by every rank before the gradients are all-reduced."""
@@ -27,10 +30,18 @@ def forward_backward(gaussians, deform, cam, gt_image, pipe, background, is_6dof
     lib = _lib.load()
     _DEFER["before"] = lib.dgs_raster_deferred_overflows()
     lib.dgs_raster_set_deferred_count(1)
+    # the raster backward neither waits for the pair count nor frees its context: the host issues the
+    # whole backward (render inputs, MLP dX, dW) first and resolves the count here, at the end
+    dgr._KEEP_CTX["on"] = True
+    pkg = None
     try:
-        return _forward_backward(gaussians, deform, cam, gt_image, pipe, background, is_6dof, lambda_dssim, warm,
-                                 ast_noise)
+        loss, pkg = _forward_backward(gaussians, deform, cam, gt_image, pipe, background, is_6dof, lambda_dssim,
+                                      warm, ast_noise)
+        return loss, pkg
     finally:
+        dgr._KEEP_CTX["on"] = False
+        if pkg is not None:
+            dgr.release_context(pkg["render"])
         lib.dgs_raster_set_deferred_count(0)
 
 

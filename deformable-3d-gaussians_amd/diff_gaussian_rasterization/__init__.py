@@ -36,6 +36,20 @@ class GaussianRasterizationSettings(NamedTuple):
     debug: bool
 
 
+# Set by deformgs.train_step during a deferred-pair-count step: the backward leaves the context
+# alive (freeing it resolves the pair count, a host wait) and the training step frees it once the
+# whole backward has been issued (release_context).
+_KEEP_CTX = {"on": False}
+
+
+def release_context(color):
+    """Free the rasterizer context behind a rendered image (resolving a deferred pair count)."""
+    fn = getattr(color, "grad_fn", None)
+    r = getattr(fn, "raster", None) if fn is not None else None
+    if isinstance(r, _Ctx):
+        r.free()
+
+
 class _Ctx:
     """Owns one dgs_raster_ctx (geometry/binning/image buffers kept for backward)."""
 
@@ -165,7 +179,8 @@ class _RasterizeGaussians(torch.autograd.Function):
                                      _lib.ptr(d_cov), _lib.ptr(d_shs), _lib.ptr(d_scales), _lib.ptr(d_rots),
                                      _lib.stream_ptr(dev))
         _lib.check(rc, "rasterize_gaussians_backward")
-        ctx.raster.free()
+        if not _KEEP_CTX["on"]:
+            ctx.raster.free()
         return (d_means3D, d_means2D, d_dens, d_shs, d_col, d_opac.view_as(opacities), d_scales, d_rots, d_cov, None)
 
 
@@ -222,7 +237,8 @@ class _RasterizeGaussiansSplitSH(torch.autograd.Function):
                                               _lib.ptr(d_dc), _lib.ptr(d_rest), _lib.ptr(d_scales),
                                               _lib.ptr(d_rots), _lib.stream_ptr(dev))
         _lib.check(rc, "rasterize_gaussians_backward")
-        ctx.raster.free()
+        if not _KEEP_CTX["on"]:
+            ctx.raster.free()
         return d_means3D, d_means2D, d_dens, d_dc, d_rest, d_opac, d_scales, d_rots, None
 
 
