@@ -3,7 +3,6 @@ Adam's shared per-optimizer step tensors keep torch.optim.Adam's per-parameter s
 render() recognises the deformation outputs it can hand to the fused input launches."""
 import types
 
-import pytest
 import torch
 
 from deformgs import adam as dgs_adam
@@ -62,9 +61,7 @@ def test_fused_se3_rows_detection():
     assert renderer._fused_se3_rows(pc, dx, raw[:, 5:9], raw[:, 10:13]) is None
 
 
-@pytest.mark.parametrize("shape_dc,shape_rest,ok", [((4, 1, 3), (4, 15, 3), True), ((4, 3), (4, 15, 3), False),
-                                                    ((4, 1, 3), (4, 8, 3), False)])
-def test_split_sh_shapes(shape_dc, shape_rest, ok):
+def test_split_sh_needs_cuda():
     from diff_gaussian_rasterization import split_sh_ok
-    # CPU tensors never take the HIP split path; the shape rules are those of the CUDA case
-    assert split_sh_ok(torch.zeros(shape_dc), torch.zeros(shape_rest)) is False
+    # the split-SH rasterizer entry is a HIP path: CPU tensors always take the generic one
+    assert split_sh_ok(torch.zeros(4, 1, 3), torch.zeros(4, 15, 3)) is False
