@@ -48,7 +48,10 @@ def parse():
     ap.add_argument("--n", type=int, default=100_000)
     ap.add_argument("--res", type=int, default=800)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-warmup", type=int, default=1)
+    ap.add_argument("--cpu-steps", type=int, default=5,
+                    help="timed CPU-oracle steps (median). SURVEY.md 8d asks 3 warm-up + 20; the default keeps the "
+                         "bench within minutes (~20 s of CPU work) and the line states the protocol used")
     ap.add_argument("--no-adam", action="store_true", help="time only the reference's span (fwd+bwd)")
     ap.add_argument("--kernel-timing", choices=["roofline", "major", "all", "none"], default="roofline",
                     help="kernel classes timed with HIP events inside the timed region. Each event record costs "
@@ -125,9 +128,9 @@ KERNEL_CLASSES = ["mlp_fwd", "mlp_bwd", "mlp_dw", "mlp_dw_reduce", "preprocess_f
                   "blend_fwd", "blend_bwd", "preprocess_bwd", "ssim_fwd", "ssim_bwd", "inputs_fwd", "inputs_bwd", "adam"]
 
 
-def cpu_baseline(N, res, steps):
+def cpu_baseline(N, res, steps, warmup=1):
     """The oracle (oracle/mlp_ref.py float64 numpy MLP + oracle/raster_ref.c OpenMP rasterizer + torch-CPU
-    L1/SSIM) timed on the host for `steps` full steps of the same workload."""
+    L1/SSIM) timed on the host: `warmup` untimed then `steps` timed full steps of the same workload."""
     from deformgs.synthetic import synth_camera, synth_gaussians
     from oracle import mlp_ref
     from oracle.raster import OracleRaster, make_settings
@@ -148,7 +151,7 @@ def cpu_baseline(N, res, steps):
     xyz = g["xyz"].numpy()
     shs = torch.cat([g["features_dc"], g["features_rest"]], 1).numpy()
     times = []
-    for _ in range(steps):
+    for it in range(warmup + steps):
         t0 = time.perf_counter()
         t = np.full((N, 1), 0.5, np.float32)
         out, c = mlp_ref.forward(p, xyz, t, True, False)
@@ -164,21 +167,23 @@ def cpu_baseline(N, res, steps):
         gr = o.backward(img.grad.numpy())
         gout = {"d_xyz": gr["means3D"], "d_rot": gr["rotations"], "d_scale": gr["scales"]}
         mlp_ref.backward(p, c, out, gout, True, False)
-        times.append(time.perf_counter() - t0)
+        if it >= warmup:
+            times.append(time.perf_counter() - t0)
     return dict(value=1.0 / float(np.median(times)), unit="iters/s", cores=threads, kind="port",
-                sample=f"{steps} full step(s) of synth-100k at N={N}, {res}x{res} (median); float64 numpy MLP "
-                       f"(BLAS threads={threads}) + C raster oracle (OpenMP forward, serial backward) + torch-CPU SSIM")
+                sample=f"median of {steps} timed full steps after {warmup} warm-up (SURVEY 8d's 3 + 20 reduced to keep "
+                       f"the CPU leg ~20 s) of synth-{N // 1000}k at {res}x{res}; float64 numpy MLP (BLAS threads="
+                       f"{threads}) + C raster oracle (OpenMP forward, serial backward) + torch-CPU SSIM")
 
 
 def main():
     args = parse()
     from deformgs import _lib
-    from deformgs.dist import OverlappedGradAllReduce, init_from_env
+    from deformgs.dist import OverflowAgreement, OverlappedGradAllReduce, init_from_env
     from deformgs.deform_model import DeformModelBaseline
     from deformgs.gaussian_model import GaussianModel
     from deformgs.arguments import OptimizationParams, PipelineParams
     from deformgs.synthetic import synth_camera, synth_gaussians
-    from deformgs.train_step import deferred_overflowed, drop_grads, forward_backward, optimizer_step
+    from deformgs.train_step import optimizer_step, train_step
     import torch.distributed as dist
 
     rank, world, local = init_from_env()
@@ -226,24 +231,19 @@ def main():
         lambda: [gaussians._xyz, gaussians._features_dc, gaussians._features_rest, gaussians._scaling,
                  gaussians._rotation, gaussians._opacity],
         lambda: list(deform.deform.parameters()))
+    agreement = OverflowAgreement()
 
     state = {"it": 3000, "P": 0, "redos": 0, "host_fb": 0.0, "host_opt": 0.0}
 
     def step(k):
         cam = cams[k % len(cams)]
-        allreduce.arm()
         h0 = time.perf_counter()
-        # one rank: the rasterizer does not wait for the pair count (the host keeps issuing); a step
-        # whose speculative pair capacity overflowed is redone synchronously. Several ranks: the
-        # synchronous count (a redo there would have to be agreed on by every rank before the
-        # overlapped all-reduce consumes the gradients)
-        loss, pkg = forward_backward(gaussians, deform, cam, gts[k % len(cams)], pipe, bg, six,
-                                     deferred_count=(world == 1 and not SYNC_COUNT))
-        if world == 1 and deferred_overflowed():
-            state["redos"] += 1
-            drop_grads(gaussians, deform)
-            loss, pkg = forward_backward(gaussians, deform, cam, gts[k % len(cams)], pipe, bg, six)
-        allreduce()
+        # the rasterizer does not wait for the pair count (the host keeps issuing); a step whose
+        # speculative pair capacity overflowed on any rank is redone synchronously on every rank
+        # (OverflowAgreement: a 1-int host all-reduce), before the gradients are used
+        loss, pkg, redone = train_step(gaussians, deform, cam, gts[k % len(cams)], pipe, bg, six,
+                                       deferred_count=not SYNC_COUNT, allreduce=allreduce, agreement=agreement)
+        state["redos"] += int(redone)
         h1 = time.perf_counter()
         if not args.no_adam:
             optimizer_step(gaussians, deform, state["it"])
@@ -329,8 +329,20 @@ def main():
         except (OSError, ValueError, KeyError):
             pass
     value = world * args.steps / elapsed
+    step_s = elapsed / args.steps
+    if roofline is not None:
+        # SURVEY.md 8d's step-level figure: (MLP FLOPs / MFMA peak + raster bytes / HBM peak) / step time,
+        # on both MFMA bases (the split-bf16 GEMMs' ceiling and the native fp32 MFMA peak)
+        mlp_flop = 2.0 * (MLP_FWD_MAC + MLP_DX_MAC + MLP_DW_MAC) * N
+        raster_bytes = 1000.0 * N + 132.0 * P_pairs + 48.0 * HW
+        roofline["step"] = {
+            "mlp_flop": mlp_flop, "raster_bytes": raster_bytes, "step_ms": step_s * 1e3,
+            "frac_split_basis": (mlp_flop / (SPLIT_MFMA_PEAK_TFLOPS * 1e12) + raster_bytes / (HBM_PEAK_GBS * 1e9)) / step_s,
+            "frac_fp32_basis": (mlp_flop / (FP32_MFMA_PEAK_TFLOPS * 1e12) + raster_bytes / (HBM_PEAK_GBS * 1e9)) / step_s,
+            "note": "kernel frac is vs the split-bf16 ceiling (2.5 PF bf16 / 6); vs the 157.3 TF fp32 MFMA peak the "
+                    "split kernels can exceed 1 (six bf16 products per fp32 product at 16x the fp32 rate)"}
     result = {
-        "metric": "train iters/s (deform+raster fwd+bwd), 100k Gaussians @ 800x800",
+        "metric": f"train iters/s (deform+raster fwd+bwd), {N // 1000}k Gaussians @ {R}x{R}",
         "value": value, "unit": "iters/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "fp32", "data": "synthetic (synth-100k, random-init weights, targets = initial renders + noise)",
@@ -350,7 +362,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            result["cpu_baseline"] = cpu_baseline(N, R, args.cpu_steps)
+            result["cpu_baseline"] = cpu_baseline(N, R, args.cpu_steps, args.cpu_warmup)
         except Exception as e:  # report, never hide
             result["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:

@@ -47,7 +47,8 @@ struct ToInt {  // the scan accumulates in int, not in the mask's byte type
 };
 
 std::mutex g_mu;
-std::map<int, std::pair<void *, size_t>> g_tmp;  // per device: scan temp storage + positions
+// per (device, stream): scan temp storage + positions (launches sharing one run in stream order)
+std::map<std::pair<int, hipStream_t>, std::pair<void *, size_t>> g_tmp;
 
 }  // namespace compact
 }  // namespace dgs
@@ -75,7 +76,7 @@ extern "C" int dgs_select_rows(int nrows, const uint8_t *mask, int njobs, const 
     void *buf = nullptr;
     {
         std::lock_guard<std::mutex> lk(compact::g_mu);
-        auto &e = compact::g_tmp[device];
+        auto &e = compact::g_tmp[{device, stream}];
         if (e.second < need) {
             // the previous buffer may still be read by queued launches on this stream
             if (e.first) DGS_HIP_CHECK(hipStreamSynchronize(stream));

@@ -46,13 +46,14 @@ __global__ __launch_bounds__(256) void k_knn3(int P, const float *__restrict__ p
         }
     }
     if (i < P) {
-        // fewer than 3 other points: average over what exists (upstream pads with large values)
+        // mean of the 3 nearest squared distances; with fewer than 3 other points (P < 4) the mean of
+        // those that exist (upstream averages its FLT_MAX padding in, i.e. returns inf / ~1e38 there)
         float s = 0.f;
         int cnt = 0;
         if (b0 < 3.4e38f) { s += b0; cnt++; }
         if (b1 < 3.4e38f) { s += b1; cnt++; }
         if (b2 < 3.4e38f) { s += b2; cnt++; }
-        out[i] = cnt ? s / 3.f : 0.f;
+        out[i] = cnt ? s / (float)cnt : 0.f;
     }
 }
 

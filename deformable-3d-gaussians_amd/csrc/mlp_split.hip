@@ -182,15 +182,21 @@ struct NoPre {
 // per-k-step counters, a relaxed LDS load spun on (wave-uniform), a relaxed LDS add from one lane.
 // A wave executes its LDS operations in issue order, so data written before a signal is visible to
 // a wave that has seen the signal; the empty asm keeps the compiler from moving LDS accesses across.
-// The spin is bounded (a wrong count gives wrong results, never a hung GPU).
+// The spin is bounded so a wrong count can never hang the GPU; an expired bound is not silent: it
+// counts into dgs_mlps_guard_expired (a global atomic from one lane), which the host reads with
+// dgs_debug_guard_expiries() and every GPU test checks to be 0 (outputs after an expiry are invalid).
+__device__ uint32_t dgs_mlps_guard_expired;
 __device__ __forceinline__ uint32_t lds_peek(const uint32_t *f) {
     return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ void lds_wait_ge(const uint32_t *f, uint32_t target, uint32_t seen) {
-    for (int guard = 0; __builtin_amdgcn_readfirstlane(seen) < target && guard < (1 << 20); guard++) {
+    int guard = 0;
+    for (; __builtin_amdgcn_readfirstlane(seen) < target && guard < (1 << 20); guard++) {
         __builtin_amdgcn_s_sleep(1);
         seen = lds_peek(f);
     }
+    if (guard == (1 << 20) && __builtin_amdgcn_readfirstlane(seen) < target && (threadIdx.x & 63) == 0)
+        __hip_atomic_fetch_add(&dgs_mlps_guard_expired, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("" ::: "memory");
 }
 __device__ __forceinline__ void lds_signal(uint32_t *f, int lane) {
@@ -1862,6 +1868,12 @@ static bool exact_fp32(int flags) { return (flags & DGS_MLP_EXACT_FP32) != 0; }
 static int net_flags(int flags) {
     return exact_fp32(flags) ? flags & (DGS_MLP_BLENDER | DGS_MLP_6DOF | DGS_MLP_NO_ROTSCALE)
                              : flags & (DGS_MLP_BLENDER | DGS_MLP_6DOF | DGS_MLP_NO_ROTSCALE | DGS_MLP_UNIFORM_T);
+}
+
+extern "C" long long dgs_debug_guard_expiries(void) {
+    uint32_t v = 0;
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(dgs::mlps::dgs_mlps_guard_expired), sizeof(v)) != hipSuccess) return -1;
+    return (long long)v;
 }
 
 extern "C" int dgs_deform_outputs(int flags) { return mlpc::make_flags(flags).nout; }

@@ -206,8 +206,10 @@ __global__ __launch_bounds__(RB) void k_scatter(const KT *__restrict__ kin, cons
 }
 
 // ------------------------------------------------------------------------------------------------
-// host: per-device scratch (histograms, tickets, look-back words) and the launch sequence. The
-// scratch is shared by the calls on a device, which the rasterizer issues in stream order.
+// host: scratch (histograms, tickets, look-back words) per (device, stream) and the launch sequence.
+// Calls that share a scratch run in stream order, so a k_scatter's tickets, look-back tags and
+// histogram buffers are never touched by another launch while it runs; sorts on two streams at once
+// (two rasterizer contexts on different streams) use two scratches.
 // ------------------------------------------------------------------------------------------------
 struct State {
     uint32_t *hist = nullptr;    // [2][MAXPASS][DIG]
@@ -217,7 +219,7 @@ struct State {
     uint32_t gen = 0;
 };
 static std::mutex g_mu;
-static std::map<int, State> g_state;
+static std::map<std::pair<int, hipStream_t>, State> g_state;
 
 // items per thread of k_scatter (a workgroup's tile = 256 x items): small tiles for small sorts so
 // a pass has enough workgroups; DGS_RADIX_ITEMS (4 / 8 / 16) overrides (tuning)
@@ -241,7 +243,7 @@ int sort_pairs(KT *k0, KT *k1, uint32_t *v0, uint32_t *v1, int n, int end_bit, h
     int device = 0;
     DGS_HIP_CHECK(hipGetDevice(&device));
     std::lock_guard<std::mutex> lk(g_mu);
-    State &S = g_state[device];
+    State &S = g_state[{device, stream}];
     if (!S.hist) {
         DGS_HIP_CHECK(hipMalloc(&S.hist, sizeof(uint32_t) * 2 * MAXPASS * DIG));
         DGS_HIP_CHECK(hipMalloc(&S.ticket, sizeof(uint32_t) * MAXPASS));
@@ -250,7 +252,7 @@ int sort_pairs(KT *k0, KT *k1, uint32_t *v0, uint32_t *v1, int n, int end_bit, h
     }
     if (S.lb_blocks < nblocks) {
         if (S.lb) {
-            DGS_HIP_CHECK(hipDeviceSynchronize());  // growth only: no launch may still use the old words
+            DGS_HIP_CHECK(hipStreamSynchronize(stream));  // growth only: no launch may still use the old words
             DGS_HIP_CHECK(hipFree(S.lb));
         }
         const int nb = nblocks + nblocks / 4 + 16;

@@ -793,7 +793,7 @@ __device__ __forceinline__ void preprocess_bwd_one(
     const float *__restrict__ acc, float *__restrict__ dL_dmeans3D, float *__restrict__ dL_dmeans2D,
     float *__restrict__ dL_ddens, float *__restrict__ dL_dcolors, float *__restrict__ dL_dopac,
     float *__restrict__ dL_dcov3D, float *__restrict__ dL_dshs, float *__restrict__ dL_dscales,
-    float *__restrict__ dL_drots, float *s_row);
+    float *__restrict__ dL_drots, float *s_row, float dsmul);
 
 template <bool STAGE>
 __global__ __launch_bounds__(256) void k_preprocess_bwd(
@@ -804,7 +804,7 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(
     const float *__restrict__ acc, float *__restrict__ dL_dmeans3D, float *__restrict__ dL_dmeans2D,
     float *__restrict__ dL_ddens, float *__restrict__ dL_dcolors, float *__restrict__ dL_dopac,
     float *__restrict__ dL_dcov3D, float *__restrict__ dL_dshs, float *__restrict__ dL_dscales,
-    float *__restrict__ dL_drots, const float *__restrict__ shs_rest, float *__restrict__ dL_dshs_rest) {
+    float *__restrict__ dL_drots, const float *__restrict__ shs_rest, float *__restrict__ dL_dshs_rest, float dsmul) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     [[maybe_unused]] const int b0 = blockIdx.x * blockDim.x, nrow = min(256, P - b0);
     [[maybe_unused]] float *s_row = nullptr;
@@ -815,13 +815,13 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(
         __syncthreads();
         if (i < P) preprocess_bwd_one<STAGE>(i, D, M, means3D, scales, mod, rots, cov_pre, shs, view, proj, campos, W, H,
                                              tanx, tany, fx, fy, radii, clamped, acc, dL_dmeans3D, dL_dmeans2D, dL_ddens,
-                                             dL_dcolors, dL_dopac, dL_dcov3D, dL_dshs, dL_dscales, dL_drots, s_row);
+                                             dL_dcolors, dL_dopac, dL_dcov3D, dL_dshs, dL_dscales, dL_drots, s_row, dsmul);
         __syncthreads();
         sh_stage_out(s_sh, dL_dshs, dL_dshs_rest, b0, nrow);
     } else {
         if (i < P) preprocess_bwd_one<STAGE>(i, D, M, means3D, scales, mod, rots, cov_pre, shs, view, proj, campos, W, H,
                                              tanx, tany, fx, fy, radii, clamped, acc, dL_dmeans3D, dL_dmeans2D, dL_ddens,
-                                             dL_dcolors, dL_dopac, dL_dcov3D, dL_dshs, dL_dscales, dL_drots, nullptr);
+                                             dL_dcolors, dL_dopac, dL_dcov3D, dL_dshs, dL_dscales, dL_drots, nullptr, dsmul);
     }
 }
 
@@ -835,7 +835,7 @@ __device__ __forceinline__ void preprocess_bwd_one(
     const float *__restrict__ acc, float *__restrict__ dL_dmeans3D, float *__restrict__ dL_dmeans2D,
     float *__restrict__ dL_ddens, float *__restrict__ dL_dcolors, float *__restrict__ dL_dopac,
     float *__restrict__ dL_dcov3D, float *__restrict__ dL_dshs, float *__restrict__ dL_dscales,
-    float *__restrict__ dL_drots, float *s_row) {
+    float *__restrict__ dL_drots, float *s_row, float dsmul) {
     const float *a = acc + (size_t)i * ACC_STRIDE;
     float4 a0 = *reinterpret_cast<const float4 *>(a);
     float4 a1 = *reinterpret_cast<const float4 *>(a + 4);
@@ -1037,7 +1037,7 @@ __device__ __forceinline__ void preprocess_bwd_one(
                     acc_s += dl * R[r * 3 + k];
                     dRm[r * 3 + k] = dl * sp[k];
                 }
-                ds[k] = acc_s * mod;
+                ds[k] = acc_s * dsmul;  // upstream: dL/d(mod s) (dsmul = 1); exact: dL/ds (dsmul = mod)
             }
             ds0 = ds[0]; ds1 = ds[1]; ds2 = ds[2];
             dR_dq(q, dRm, dq);
@@ -1092,6 +1092,11 @@ struct dgs_raster_ctx {
                 *rots = nullptr, *cov = nullptr;
     const float *shs_rest = nullptr;  // split SH rows (dgs_raster_forward_split_sh): shs = features_dc
     DevBuf geom, bin, img, acc, tmp, rect;
+    // k_rect_colscan's generation-tagged tile totals: a buffer of their own, zeroed whenever it is
+    // (re)allocated, so it only ever holds 0 or words a colscan launch wrote (never stale count-matrix
+    // data whose upper half could equal the current generation)
+    DevBuf rtot;
+    bool bwd_done = false;  // a backward already consumed the accumulators (a second one re-zeroes them)
     // carved views
     float2 *xy = nullptr;
     float4 *conic_o = nullptr, *rgbd = nullptr;
@@ -1407,6 +1412,10 @@ static int bin_and_blend(dgs_raster_ctx *c, int cap, int P, int device, hipStrea
 // step synchronously (deformgs/train_step.py); the backward runs on ranges clipped to the capacity
 // so it stays in bounds.
 std::atomic<int> g_deferred{0};
+// dL/dscales: the upstream CUDA op returns the gradient w.r.t. the modified scale (scale_modifier * s),
+// i.e. without the scale_modifier factor; dgs_raster_set_exact_scale_grad(1) applies the chain rule
+// (identical whenever scale_modifier = 1, as in every training call)
+std::atomic<int> g_exact_scale_grad{0};
 std::atomic<long long> g_deferred_overflows{0};
 
 __global__ void k_clip_ranges(int T, uint2 *ranges, uint32_t cap) {
@@ -1480,6 +1489,7 @@ static int raster_forward(const dgs_raster_settings *s, int P, int M, const floa
     c->scales = scales; c->rots = rotations; c->cov = cov3D_precomp;
     c->radii = out_radii;
     c->last_stream = stream;
+    c->bwd_done = false;
     const int T = c->gx * c->gy;
     const int HW = c->H * c->W;
     const bool dbg = s->debug != 0;
@@ -1517,13 +1527,16 @@ static int raster_forward(const dgs_raster_settings *s, int P, int M, const floa
     c->rect_mode = P > 0 && rect_binning(c->gx, c->gy, P);
     if (c->rect_mode) {  // count matrix [blocks][tiles], tile totals, tile starts, pair count
         const size_t nb = div_up(P, 256);
-        size_t o_cnt = 0, o_tot = align_up(4ull * nb * T), o_st = align_up(o_tot + 8ull * T), o_n = align_up(o_st + 4ull * T);
+        size_t o_cnt = 0, o_st = align_up(4ull * nb * T), o_n = align_up(o_st + 4ull * T);
         if (int rc = c->rect.ensure(o_n + 256)) return rc;
         char *r = (char *)c->rect.p;
         c->rect_cnt = (uint32_t *)(r + o_cnt);
-        c->rect_tot = (unsigned long long *)(r + o_tot);
         c->rect_start = (uint32_t *)(r + o_st);
         c->rect_total = (uint32_t *)(r + o_n);
+        const size_t tot_cap = c->rtot.cap;
+        if (int rc = c->rtot.ensure(8ull * T)) return rc;
+        if (c->rtot.cap != tot_cap) DGS_HIP_CHECK(hipMemsetAsync(c->rtot.p, 0, c->rtot.cap, stream));
+        c->rect_tot = (unsigned long long *)c->rtot.p;
     }
 
     const float fx = c->W / (2.f * s->tanfovx), fy = c->H / (2.f * s->tanfovy);
@@ -1663,6 +1676,10 @@ static int raster_backward(dgs_raster_ctx *c, const float *dL_dcolor, const floa
     const bool dbg = c->s.debug != 0;
     const int T = c->gx * c->gy;
     float *acc = (float *)c->acc.p;  // [P][12], zeroed by the forward's k_preprocess
+    // a second backward through the same forward (retain_graph, or a context kept alive): the blend
+    // backward adds into the accumulators, so they are cleared first instead of doubling the gradients
+    if (c->bwd_done) DGS_HIP_CHECK(hipMemsetAsync(acc, 0, 4ull * ACC_STRIDE * P, stream));
+    c->bwd_done = true;
     if (cap > 0) {
         ScopedTimer tm("blend_bwd", stream);
         hipLaunchKernelGGL(k_blend_bwd, dim3(T), dim3(TILE_PIX), 0, stream, c->ranges, c->vals, cap, c->W, c->H, c->gx,
@@ -1679,7 +1696,8 @@ static int raster_backward(dgs_raster_ctx *c, const float *dL_dcolor, const floa
                            c->scales, c->s.scale_modifier, c->rots, c->cov, c->shs, c->s.viewmatrix, c->s.projmatrix,
                            c->s.campos, c->W, c->H, c->s.tanfovx, c->s.tanfovy, fx, fy, c->radii, c->clamped, acc,
                            dL_dmeans3D, dL_dmeans2D, dL_dmeans2D_densify, dL_dcolors, dL_dopacity, dL_dcov3D, dL_dshs,
-                           dL_dscales, dL_drotations, c->shs_rest, dL_dshs_rest);
+                           dL_dscales, dL_drotations, c->shs_rest, dL_dshs_rest,
+                           g_exact_scale_grad.load() ? c->s.scale_modifier : 1.f);
     }
     DGS_LAUNCH_CHECK("k_preprocess_bwd", dbg, stream);
     return DGS_OK;
@@ -1741,12 +1759,15 @@ extern "C" void dgs_raster_ctx_free(dgs_raster_ctx *c) {
         g_pool.push_back(c);
     } else {
         c->geom.release(); c->bin.release(); c->img.release(); c->acc.release(); c->tmp.release(); c->rect.release();
+        c->rtot.release();
         if (c->h_total) (void)hipHostFree(c->h_total);
         delete c;
     }
 }
 
 extern "C" void dgs_raster_set_deferred_count(int on) { g_deferred.store(on ? 1 : 0); }
+
+extern "C" void dgs_raster_set_exact_scale_grad(int on) { g_exact_scale_grad.store(on ? 1 : 0); }
 
 extern "C" long long dgs_raster_deferred_overflows(void) { return g_deferred_overflows.load(); }
 

@@ -55,6 +55,8 @@ _SIGS = {
     "dgs_debug_count_wait_ns": ([ctypes.POINTER(ctypes.c_longlong)], ctypes.c_longlong),
     "dgs_debug_pair_cap": ([I], I),
     "dgs_raster_set_deferred_count": ([I], None),
+    "dgs_raster_set_exact_scale_grad": ([I], None),
+    "dgs_debug_guard_expiries": ([], ctypes.c_longlong),
     "dgs_raster_deferred_overflows": ([], ctypes.c_longlong),
     "dgs_debug_set_binning": ([I], None),
     "dgs_timing_enable": ([I], None),

@@ -32,10 +32,10 @@ class DeformModelBaseline:
     def step(self, xyz, time_emb):
         return self.deform(xyz, time_emb)
 
-    def train_setting(self, training_args):
+    def train_setting(self, training_args, optimizer_cls=None):
         l = [{'params': list(self.deform.parameters()),
               'lr': training_args.position_lr_init * self.spatial_lr_scale, "name": "deform"}]
-        self.optimizer = Adam(l, lr=0.0, eps=1e-15)
+        self.optimizer = (optimizer_cls or Adam)(l, lr=0.0, eps=1e-15)
         self.deform_scheduler_args = get_expon_lr_func(lr_init=training_args.position_lr_init * self.spatial_lr_scale,
                                                        lr_final=training_args.position_lr_final,
                                                        lr_delay_mult=training_args.position_lr_delay_mult,

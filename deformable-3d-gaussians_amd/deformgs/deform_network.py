@@ -181,6 +181,38 @@ class _DeformBase(nn.Module):
         flags = self.flags | (FLAG_EXACT_FP32 if self.exact_fp32 else 0) | (FLAG_UNIFORM_T if uniform else 0)
         return _FusedDeformMLP.apply(flags, x, t, *params)
 
+    def glue_forward(self, x, t):
+        """The reference's own torch forward (utils/time_utils.py:102-127: PE by cat of sin / cos bands,
+        timenet, 8 x Linear + ReLU with the skip cat after layer 4, heads) on these parameters: the
+        torch-glue comparison path of the training loop (deformgs/train.py fused=False), not the product
+        path. rocBLAS fp32 GEMMs; gradients by autograd."""
+        import torch.nn.functional as F
+        from .rigid import screw_from_raw
+
+        def embed(v, L):
+            bands = [v]
+            for i in range(L):
+                f = 2.0 ** i
+                bands += [torch.sin(v * f), torch.cos(v * f)]
+            return torch.cat(bands, -1)
+
+        t_emb = embed(t, self.t_multires)
+        if self.is_blender:
+            t_emb = self.timenet(t_emb)
+        x_emb = embed(x, 10)
+        h = torch.cat([x_emb, t_emb], dim=-1)
+        for i, lin in enumerate(self.linear):
+            h = F.relu(lin(h))
+            if i in self.skips:
+                h = torch.cat([x_emb, t_emb, h], -1)
+        if self.is_6dof:
+            d_xyz = screw_from_raw(self.branch_w(h), self.branch_v(h))
+        else:
+            d_xyz = self.gaussian_warp(h)
+        if not self._rotscale:
+            return d_xyz, 0, 0
+        return d_xyz, self.gaussian_rotation(h), self.gaussian_scaling(h)
+
     def forward(self, x, t):
         out = self.raw(x, t)
         if self.is_6dof:

@@ -141,6 +141,14 @@ class OverlappedGradAllReduce:
             p.grad = flat[off:off + n].view_as(p)
             off += n
 
+    def discard(self):
+        """Drop this step's reduction (the step is being redone): the early collective, if it was
+        started, is waited for (every rank issued it, so the communicator stays in step) and ignored;
+        call arm() again before the redone backward."""
+        if self._pending is not None:
+            self._pending[1].wait()
+        self._pending, self._armed = None, False
+
     def __call__(self):
         """Call after loss.backward(): late group, then the early group's (overlapped) result."""
         if self.world() == 1:
@@ -155,6 +163,27 @@ class OverlappedGradAllReduce:
             self._reduce([p for p in self.late_fn() if p.requires_grad])
             self._reduce(early, *pending)
         self._pending = None
+
+
+class OverflowAgreement:
+    """Rank agreement on redoing a step whose deferred pair count overflowed its speculative capacity
+    (deformgs/train_step.py deferred_count): a 1-int MAX all-reduce over a gloo (host) group, so it
+    neither waits behind the gradient collectives on the RCCL stream nor touches the GPU. Every rank
+    calls it once per deferred step, after its own count is resolved; all redo or none does, so the
+    gradient collectives of the redone step still line up."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self._gloo = None
+
+    def __call__(self, local_overflow):
+        if not dist.is_initialized() or dist.get_world_size(self.group) == 1:
+            return bool(local_overflow)
+        if self._gloo is None:
+            self._gloo = self.group if dist.get_backend(self.group) == "gloo" else dist.new_group(backend="gloo")
+        flag = torch.tensor([1 if local_overflow else 0], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self._gloo)
+        return bool(flag.item())
 
 
 def sync_densification_stats(gaussians, group=None):

@@ -117,7 +117,14 @@ class GaussianModel:
         self.max_radii2D = torch.zeros((xyz.shape[0]), device=xyz.device)
 
     # ---- optimisation (gaussian_model.py:120-152) ----
-    def training_setup(self, training_args):
+    # row selection of densification: the one-launch HIP compaction; the torch-glue training loop
+    # (deformgs/train.py, fused=False) sets torch indexing here, as the reference does it
+    row_select = None
+
+    def _select(self, mask, tensors):
+        return (self.row_select or select_rows)(mask, tensors)
+
+    def training_setup(self, training_args, optimizer_cls=None):
         self.percent_dense = training_args.percent_dense
         dev = self._xyz.device
         self.xyz_gradient_accum = torch.zeros((self.get_xyz.shape[0], 1), device=dev)
@@ -131,7 +138,7 @@ class GaussianModel:
             {'params': [self._scaling], 'lr': training_args.scaling_lr * self.spatial_lr_scale, "name": "scaling"},
             {'params': [self._rotation], 'lr': training_args.rotation_lr, "name": "rotation"},
         ]
-        self.optimizer = Adam(l, lr=0.0, eps=1e-15)
+        self.optimizer = (optimizer_cls or Adam)(l, lr=0.0, eps=1e-15)
         self.xyz_scheduler_args = get_expon_lr_func(lr_init=training_args.position_lr_init * self.spatial_lr_scale,
                                                     lr_final=training_args.position_lr_final * self.spatial_lr_scale,
                                                     lr_delay_mult=training_args.position_lr_delay_mult,
@@ -214,7 +221,7 @@ class GaussianModel:
             srcs.append(group["params"][0].detach())
             if st is not None:
                 srcs += [st["exp_avg"], st["exp_avg_sq"]]
-        sel = select_rows(mask, srcs + list(extra))
+        sel = self._select(mask, srcs + list(extra))
         out, k = {}, 0
         for group, st in groups:
             new_p = sel[k]
@@ -271,7 +278,7 @@ class GaussianModel:
         padded[:grads.shape[0]] = grads.squeeze()
         sel = torch.where(padded >= grad_threshold, True, False)
         sel = torch.logical_and(sel, torch.max(self.get_scaling, dim=1).values > self.percent_dense * scene_extent)
-        xyz, fdc, frest, opac, scaling, rot = select_rows(sel, [
+        xyz, fdc, frest, opac, scaling, rot = self._select(sel, [
             self._xyz.detach(), self._features_dc.detach(), self._features_rest.detach(), self._opacity.detach(),
             self._scaling.detach(), self._rotation.detach()])
         sel_scaling = self.scaling_activation(scaling)
@@ -289,7 +296,7 @@ class GaussianModel:
     def densify_and_clone(self, grads, grad_threshold, scene_extent):
         sel = torch.where(torch.norm(grads, dim=-1) >= grad_threshold, True, False)
         sel = torch.logical_and(sel, torch.max(self.get_scaling, dim=1).values <= self.percent_dense * scene_extent)
-        self.densification_postfix(*select_rows(sel, [
+        self.densification_postfix(*self._select(sel, [
             self._xyz.detach(), self._features_dc.detach(), self._features_rest.detach(), self._opacity.detach(),
             self._scaling.detach(), self._rotation.detach()]))
 

@@ -87,6 +87,25 @@ class _GaussianInputs(torch.autograd.Function):
 # DGS_SPLIT_SH=0 (A/B diagnostic): the fused path concatenates the SH rows for the plain rasterizer
 _SPLIT_SH = os.environ.get("DGS_SPLIT_SH", "1") not in ("", "0")
 
+# override_color: the reference accepts it but never uses it (gaussian_renderer/__init__.py:101-113 test
+# `colors_precomp is None`, which always holds, so SHs are rasterized), and so does render() here by
+# default. DGS_HONOR_OVERRIDE_COLOR=1 / set_honor_override_color(True) rasterizes override_color as the
+# precomputed colours instead (what the argument evidently intends; a different image from the reference).
+_HONOR_OVERRIDE = {"on": os.environ.get("DGS_HONOR_OVERRIDE_COLOR", "0") not in ("", "0")}
+
+
+def set_honor_override_color(on):
+    _HONOR_OVERRIDE["on"] = bool(on)
+
+
+# the fused render-input launches on the training path; off: the reference's torch glue for every call
+# (deformgs/train.py fused=False, the comparison loop)
+_FUSED = {"on": True}
+
+
+def set_fused(on):
+    _FUSED["on"] = bool(on)
+
 
 def _fused_deform_rows(pc, d_xyz, d_rotation, d_scaling):
     """The (N, 10) deformation output the three deltas are column views of, 0 for no deformation,
@@ -138,6 +157,8 @@ def _fused_ok(pc):
 def render(viewpoint_camera, pc, pipe, bg_color, d_xyz, d_rotation, d_scaling, is_6dof=False,
            scaling_modifier=1.0, override_color=None, direct_compute=False):
     dev = pc.get_xyz.device
+    if not _HONOR_OVERRIDE["on"]:
+        override_color = None  # the reference's behaviour (see _HONOR_OVERRIDE)
     # gaussian_renderer/__init__.py:41-47 builds these as zeros + 0 with retain_grad; the rasterizer never
     # reads their values (only .grad is delivered), so uninitialised leaf tensors serve: their .grad is
     # populated directly and no fill / add kernels run per render
@@ -153,7 +174,7 @@ def render(viewpoint_camera, pc, pipe, bg_color, d_xyz, d_rotation, d_scaling, i
         debug=getattr(pipe, "debug", False))
     rasterizer = GaussianRasterizer(raster_settings=raster_settings)
     rows, se3 = None, False
-    if (not direct_compute and override_color is None and not getattr(pipe, "compute_cov3D_python", False)
+    if (_FUSED["on"] and not direct_compute and override_color is None and not getattr(pipe, "compute_cov3D_python", False)
             and not getattr(pipe, "convert_SHs_python", False) and _fused_ok(pc)):
         if not is_6dof:
             rows = _fused_deform_rows(pc, d_xyz, d_rotation, d_scaling)

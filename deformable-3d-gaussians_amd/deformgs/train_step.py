@@ -2,6 +2,7 @@
 harness): deform -> render -> 0.8*L1 + 0.2*(1-SSIM) -> backward [-> grad all-reduce] -> Adam.
 """
 import torch
+import torch.distributed as dist
 
 import diff_gaussian_rasterization as dgr
 
@@ -15,15 +16,19 @@ _DEFER = {"before": 0}
 
 
 def forward_backward(gaussians, deform, cam, gt_image, pipe, background, is_6dof=False, lambda_dssim=0.2,
-                     warm=True, ast_noise=0.0, deferred_count=False):
+                     warm=True, ast_noise=0.0, deferred_count=False, rank_agreed=False):
     """train_baseline.py:104-128 (timed span of the reference's iter_start/iter_end events).
 
     deferred_count: the rasterizer does not wait for num_rendered in the forward nor in the backward
     (the host keeps issuing the loss and the whole backward; the count is read once that is queued);
     if the speculative pair capacity overflowed, `deferred_overflowed()`
     is True afterwards and the caller must redo the step with deferred_count=False after dropping
-    the gradients (`drop_grads`; bench.py). Single-rank only: with several ranks a redo must be
-    agreed on by every rank before the gradients are all-reduced."""
+    the gradients (`drop_grads`). With several ranks the redo must be agreed on by every rank before
+    the gradients are used (`train_step` does it with dist.OverflowAgreement): a multi-rank caller
+    must pass rank_agreed=True to promise that, else this raises."""
+    if deferred_count and not rank_agreed and dist.is_initialized() and dist.get_world_size() > 1:
+        raise RuntimeError("forward_backward(deferred_count=True) with several ranks needs a rank agreement on "
+                           "overflow redos (use train_step(), or pass rank_agreed=True after arranging one)")
     if not deferred_count:
         return _forward_backward(gaussians, deform, cam, gt_image, pipe, background, is_6dof, lambda_dssim, warm,
                                  ast_noise)
@@ -43,6 +48,39 @@ def forward_backward(gaussians, deform, cam, gt_image, pipe, background, is_6dof
         if pkg is not None:
             dgr.release_context(pkg["render"])
         lib.dgs_raster_set_deferred_count(0)
+
+
+def train_step(gaussians, deform, cam, gt_image, pipe, background, is_6dof=False, lambda_dssim=0.2, warm=True,
+               ast_noise=0.0, deferred_count=True, allreduce=None, agreement=None):
+    """One iteration's compute up to the optimizer: forward_backward (deferred pair count unless
+    deferred_count=False), the synchronous redo of a step whose speculative pair capacity overflowed
+    (agreed across ranks by `agreement`, a dist.OverflowAgreement, when world > 1), and the gradient
+    all-reduce (`allreduce`, an armed dist.OverlappedGradAllReduce, when world > 1).
+    Returns (loss, render package, redone)."""
+    multi = allreduce is not None and allreduce.world() > 1
+    if multi and deferred_count and agreement is None:
+        raise RuntimeError("train_step: several ranks with the deferred pair count need an OverflowAgreement")
+    if multi:
+        allreduce.arm()
+    loss, pkg = forward_backward(gaussians, deform, cam, gt_image, pipe, background, is_6dof, lambda_dssim, warm,
+                                 ast_noise, deferred_count=deferred_count, rank_agreed=multi)
+    redone = False
+    if deferred_count:
+        over = deferred_overflowed()
+        if multi:
+            over = agreement(over)
+        if over:
+            redone = True
+            if multi:
+                allreduce.discard()
+            drop_grads(gaussians, deform)
+            if multi:
+                allreduce.arm()
+            loss, pkg = forward_backward(gaussians, deform, cam, gt_image, pipe, background, is_6dof, lambda_dssim,
+                                         warm, ast_noise, deferred_count=False)
+    if multi:
+        allreduce()
+    return loss, pkg, redone
 
 
 def deferred_overflowed():

@@ -68,6 +68,13 @@ class _Ctx:
             pass
 
 
+def _require_ctx(ctx):
+    if ctx.raster.handle is None:
+        raise RuntimeError("rasterize_gaussians: a second backward through the same render needs its rasterizer "
+                           "context, which the first backward released; keep it with "
+                           "diff_gaussian_rasterization._KEEP_CTX['on'] = True (the accumulators are re-zeroed)")
+
+
 def _f32(t):
     if t is None:
         return None
@@ -156,6 +163,7 @@ class _RasterizeGaussians(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_color, grad_radii, grad_depth):
         lib = _lib.load()
+        _require_ctx(ctx)
         means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp, radii = ctx.saved_tensors
         P = means3D.shape[0]
         dev = means3D.device
@@ -223,6 +231,7 @@ class _RasterizeGaussiansSplitSH(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_color, grad_radii, grad_depth, grad_visible):
         lib = _lib.load()
+        _require_ctx(ctx)
         radii = ctx.saved_tensors[0]
         P, dev = ctx.P, radii.device
         e = lambda *shape: torch.empty(shape, dtype=torch.float32, device=dev)  # noqa: E731

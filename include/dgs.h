@@ -131,6 +131,14 @@ void dgs_debug_set_binning(int mode);
 long long dgs_debug_binning_redos(void);
 /* host nanoseconds spent waiting for num_rendered (and the number of waits) since process start */
 long long dgs_debug_count_wait_ns(long long *waits);
+/* dL/dscales convention. 0 (default) = the upstream CUDA op's: the gradient w.r.t. the modified scale
+ * scale_modifier * s (its computeCov3D backward omits the factor); 1 = the chain rule through the
+ * modifier (dL/ds). Identical when scale_modifier == 1 (every training call: render() default). */
+void dgs_raster_set_exact_scale_grad(int on);
+/* Times the deformation MLP's barrier-free LDS hand-off gave up waiting (bounded spin expired) on the
+ * current device since process start: must be 0; a non-zero count means MLP outputs / gradients of
+ * some launch are invalid (GPU tests assert it stays 0). -1 if the counter could not be read. */
+long long dgs_debug_guard_expiries(void);
 
 /* ---- timing hooks (bench.py): per-kernel-class HIP event accumulation on the launch stream ---- */
 void dgs_timing_enable(int on);

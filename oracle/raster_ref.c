@@ -663,7 +663,9 @@ int or_backward(void *p, const float *dL_dpix, const float *dL_ddepth, float *dL
                     ds += dLm[r * 3 + k] * R[r * 3 + k];
                     dRm[r * 3 + k] = dLm[r * 3 + k] * sp[k];
                 }
-                dL_dscales[3 * i + k] = ds * mod;
+                /* upstream 3DGS computeCov3D backward returns the gradient w.r.t. the modified scale
+                 * (mod * s): no factor mod here (libdgs_hip: dgs_raster_set_exact_scale_grad(0)) */
+                dL_dscales[3 * i + k] = ds;
             }
             dR_dq(q, dRm, dL_drots + 4 * i);
         }

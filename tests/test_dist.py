@@ -189,3 +189,49 @@ def test_overlapped_grad_allreduce():
         torch.testing.assert_close(a1, 1.5 * torch.arange(7.0))
         torch.testing.assert_close(b1, torch.full((3, 2), 1.5))  # (3 * 1 + 0) / 2
         torch.testing.assert_close(c1, torch.full((5,), 3.0))
+
+
+def _agreement_case(rank, world):
+    """OverflowAgreement: any rank's overflow makes every rank redo; an early collective of the
+    discarded step completes on every rank and the redone step's reduction is the one kept."""
+    from deformgs.dist import OverflowAgreement
+    agree = OverflowAgreement()
+    votes = [agree(False), agree(rank == 1), agree(rank == 0), agree(True)]
+    a = torch.nn.Parameter(torch.zeros(4))
+    c = torch.nn.Parameter(torch.zeros(2))
+    ar = OverlappedGradAllReduce(lambda: [a], lambda: [c])
+    ar.arm()
+    ((rank + 1.0) * 100 * a).sum().backward()  # the overflowed step's gradients: discarded
+    started = ar._pending is not None
+    if agree(rank == 1):
+        ar.discard()
+        a.grad = None
+        ar.arm()
+        ((rank + 1.0) * a).sum().backward()
+    (c * (rank + 1.0)).sum().backward()
+    ar()
+    return votes, started, a.grad.clone(), c.grad.clone()
+
+
+def test_overflow_agreement_and_discard():
+    out = _run(_agreement_case)
+    for rank in (0, 1):
+        votes, started, ag, cg = out[rank]
+        assert votes == [False, True, True, True]
+        assert started
+        torch.testing.assert_close(ag, torch.full((4,), 1.5))
+        torch.testing.assert_close(cg, torch.full((2,), 1.5))
+
+
+def test_viewpoint_stack_matches_reference_formula():
+    """train_baseline.py:80-89: sorted by fid, int(round(i * (total - 1) / (sequence_length - 1)))."""
+    from deformgs.train import build_viewpoint_stack
+    cams = [types.SimpleNamespace(fid=torch.tensor([f])) for f in torch.rand(47, generator=torch.Generator().manual_seed(1))]
+    st = build_viewpoint_stack(cams, 30)
+    srt = sorted(cams, key=lambda c: float(c.fid))
+    step = (47 - 1) / (30 - 1)
+    assert [id(c) for c in st] == [id(srt[int(round(i * step))]) for i in range(30)]
+    assert [float(c.fid) for c in st] == sorted(float(c.fid) for c in st)
+    # more frames asked for than exist: indices repeat, as upstream
+    st2 = build_viewpoint_stack(cams[:5], 9)
+    assert len(st2) == 9 and len({id(c) for c in st2}) == 5

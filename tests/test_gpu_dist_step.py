@@ -1,0 +1,77 @@
+"""Frame-parallel training step with 2 ranks on the one GPU of the box: two fresh
+child processes (DGS_DEVICE=0, DGS_DIST_BACKEND=gloo) each render their own camera through
+train_step (deferred pair count, overlapped gradient all-reduce, rank-agreed overflow redo), then
+Adam. Checks: the averaged gradients equal the mean of the two single-rank steps computed here (the
+blend backward sums float atomics in arrival order: 1e-4 relative + 1e-6 of the tensor's max), and the
+post-Adam parameters are bitwise identical on both ranks. "overflow": rank 1's speculative pair
+capacity is forced to overflow, so BOTH ranks must redo (the agreement) and the result is unchanged.
+RCCL itself is unmeasured on hardware here (one GPU); gloo carries the same collectives.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from conftest import ROOT, gpu_available
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _single_rank_grads():
+    sys.path.insert(0, HERE)
+    from dist_step_worker import build, params_of
+    from deformgs.arguments import PipelineParams
+    from deformgs.train_step import train_step
+    dev = torch.device("cuda", 0)
+    out = []
+    for k in range(2):
+        gs, deform, cams, gts = build(dev)
+        train_step(gs, deform, cams[k], gts[k], PipelineParams(), torch.zeros(3, device=dev), deferred_count=False)
+        out.append([p.grad.detach().clone().cpu() for p in params_of(gs, deform)])
+    return out
+
+
+@pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")
+@pytest.mark.parametrize("mode", ["plain", "overflow"])
+def test_two_rank_step_averages_gradients(tmp_path, mode):
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), DGS_DEVICE="0", DGS_DIST_BACKEND="gloo")
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "dist_step_worker.py"), str(tmp_path),
+                                       mode], env=env, cwd=ROOT))
+    rcs = []
+    for p in procs:
+        try:
+            rcs.append(p.wait(timeout=100))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            rcs.append(-9)
+    assert rcs == [0, 0], rcs
+    r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
+    if mode == "overflow":
+        assert r0["redone"] and r1["redone"], "an overflow on one rank must be redone on every rank"
+    else:
+        assert not r0["redone"] and not r1["redone"]
+    single = _single_rank_grads()
+    for i, (a, b, s0, s1) in enumerate(zip(r0["grads"], r1["grads"], *single)):
+        assert torch.equal(a, b), f"reduced gradient {i} differs between ranks"
+        want = (s0 + s1) / 2
+        tol = 1e-6 * float(want.abs().max()) + 1e-4 * want.abs()
+        assert bool(((a - want).abs() <= tol).all()), (i, float((a - want).abs().max()))
+    for i, (a, b) in enumerate(zip(r0["params"], r1["params"])):
+        assert torch.equal(a, b), f"parameter {i} differs between ranks after Adam"

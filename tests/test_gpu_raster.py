@@ -316,3 +316,96 @@ def test_deferred_count_redo_matches_sync(binning):
     assert redo[0] == ref[0] and torch.equal(redo[1], ref[1])
     for a, b in zip(redo[2], ref[2]):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6 * max(1.0, b.abs().max().item()))
+
+
+def test_two_streams_at_once_match_sequential():
+    """Two renders in flight on two HIP streams (two rasterizer contexts, both sorting at once) equal
+    the same renders run one after the other: the radix / compaction scratch is per stream."""
+    a_in, rs_a, _ = scene(20000, 320, 240, seed=21, cam_index=1)
+    b_in, rs_b, _ = scene(15000, 200, 280, seed=22, cam_index=4, scale_boost=0.5)
+    for binning_mode in (0, 1):
+        from deformgs import _lib
+        lib = _lib.load()
+        lib.dgs_debug_set_binning(binning_mode)
+        try:
+            ref_a = _forward_only(a_in, rs_a, debug=False)
+            ref_b = _forward_only(b_in, rs_b, debug=False)
+            s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+            torch.cuda.synchronize()
+            for _ in range(3):
+                with torch.cuda.stream(s1):
+                    got_a = _forward_only(a_in, rs_a, debug=False)
+                with torch.cuda.stream(s2):
+                    got_b = _forward_only(b_in, rs_b, debug=False)
+                torch.cuda.synchronize()
+                for x, y in zip(got_a + got_b, ref_a + ref_b):
+                    np.testing.assert_array_equal(x, y)
+        finally:
+            lib.dgs_debug_set_binning(0)
+
+
+def test_shrinking_point_sets_reuse_contexts_exactly():
+    """Frames whose Gaussian count shrinks (prune) and grows again reuse pooled contexts with
+    smaller / larger count matrices; every frame equals the synchronous exact (debug) path, which
+    runs no speculative binning. (The rect binning's tagged tile totals live in their own zeroed
+    buffer: a stale count-matrix word can never carry the current generation tag.)"""
+    sizes = [150000, 40000, 3000, 90000, 500, 150000]
+    for n in sizes:
+        inp, rs, _ = scene(n, 256, 256, seed=n % 97, cam_index=n % 5)
+        a = _forward_only(inp, rs, debug=False)
+        b = _forward_only(inp, rs, debug=True)
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
+
+
+def test_second_backward_recomputes_not_doubles():
+    """A kept context (retain_graph + _KEEP_CTX) backpropagated twice gives the same gradients twice
+    (the accumulators are re-zeroed, not added onto); without the kept context the second backward
+    raises instead of reading a released context."""
+    import diff_gaussian_rasterization as dgr
+    inputs, rs, _ = scene(3000, 96, 96, seed=5, cam_index=2)
+    t = {k: v.cuda().requires_grad_(True) for k, v in inputs.items()}
+    N = t["means3D"].shape[0]
+    from diff_gaussian_rasterization import GaussianRasterizer
+    dgr._KEEP_CTX["on"] = True
+    try:
+        color, _, _ = GaussianRasterizer(settings_for_gpu(rs))(
+            means3D=t["means3D"], means2D=torch.zeros((N, 3), device="cuda"), shs=t["shs"],
+            opacities=t["opacities"], scales=t["scales"], rotations=t["rotations"])
+        w = torch.linspace(-1, 1, color.numel(), device="cuda").reshape(color.shape)
+        (color * w).sum().backward(retain_graph=True)
+        g1 = t["means3D"].grad.clone()
+        t["means3D"].grad = None
+        (color * w).sum().backward(retain_graph=True)
+        torch.testing.assert_close(t["means3D"].grad, g1, rtol=1e-5, atol=1e-7 * float(g1.abs().max()))
+        dgr.release_context(color)
+    finally:
+        dgr._KEEP_CTX["on"] = False
+    color, _, _ = GaussianRasterizer(settings_for_gpu(rs))(
+        means3D=t["means3D"], means2D=torch.zeros((N, 3), device="cuda"), shs=t["shs"],
+        opacities=t["opacities"], scales=t["scales"], rotations=t["rotations"])
+    color.sum().backward(retain_graph=True)
+    with pytest.raises(RuntimeError, match="second backward"):
+        color.sum().backward()
+
+
+def test_scale_gradient_conventions():
+    """dL/dscales with scale_modifier != 1: the upstream convention (default; the oracle's) is the
+    gradient w.r.t. the modified scale; dgs_raster_set_exact_scale_grad(1) multiplies it by the
+    modifier (the chain rule). scale_modifier = 1.3 here."""
+    from deformgs import _lib
+    lib = _lib.load()
+    inputs, rs, _ = scene(2000, 80, 96, seed=8, cam_index=3)
+    rs = dict(rs, scale_modifier=1.3)
+    rng = np.random.default_rng(4)
+    dcolor = rng.standard_normal((3, 80, 96)).astype(np.float32)
+    o, g = oracle_run(inputs, rs, dcolor, None)
+    _, _, _, up = _run_gpu(inputs, rs, dcolor, None)
+    assert frac_close(up["scales"], g["scales"], atol=2e-3 * np.abs(g["scales"]).max(), rtol=1e-3) >= 0.995
+    lib.dgs_raster_set_exact_scale_grad(1)
+    try:
+        _, _, _, ex = _run_gpu(inputs, rs, dcolor, None)
+    finally:
+        lib.dgs_raster_set_exact_scale_grad(0)
+    np.testing.assert_allclose(ex["scales"], up["scales"] * np.float32(1.3), rtol=1e-4,
+                               atol=1e-6 * np.abs(up["scales"]).max())
