@@ -518,6 +518,19 @@ __device__ __forceinline__ int2 compact_slot(bool keep, int tid, uint32_t *s_wcn
     return make_int2(base + below, tot);
 }
 
+// Pixel of thread tid within its 16x16 tile: wave w takes the 8x8 quadrant (w & 1, w >> 1), not a
+// 16x4 row strip, so a Gaussian covering part of the tile touches fewer waves (each (wave, Gaussian)
+// pair costs the wave's whole gradient reduction in the backward): blend_bwd 0.336 -> 0.319 ms at
+// P = 1.0 M pairs (3 A/B pairs, tools/variant_session.sh), forward unchanged. DGS_BLEND_STRIP: strips.
+__device__ __forceinline__ int2 tile_pixel(int tid) {
+#ifdef DGS_BLEND_STRIP
+    return make_int2(tid % TILE_X, tid / TILE_X);
+#else
+    const int w = tid >> 6, l = tid & 63;
+    return make_int2((w & 1) * 8 + (l & 7), (w >> 1) * 8 + (l >> 3));
+#endif
+}
+
 __global__ __launch_bounds__(256) void k_blend_fwd(const uint2 *__restrict__ ranges, const uint32_t *__restrict__ vals,
                                                    uint32_t cap, int W, int H, int gx, const float2 *__restrict__ xy,
                                                    const float4 *__restrict__ conic_o, const float4 *__restrict__ rgbd,
@@ -532,8 +545,9 @@ __global__ __launch_bounds__(256) void k_blend_fwd(const uint2 *__restrict__ ran
     const int tile = blockIdx.x;
     const int tid = threadIdx.x;
     const float tx0 = (float)((tile % gx) * TILE_X), ty0 = (float)((tile / gx) * TILE_Y);
-    const int px = (tile % gx) * TILE_X + (tid % TILE_X);
-    const int py = (tile / gx) * TILE_Y + (tid / TILE_X);
+    const int2 tp = tile_pixel(tid);
+    const int px = (tile % gx) * TILE_X + tp.x;
+    const int py = (tile / gx) * TILE_Y + tp.y;
     const bool inside = px < W && py < H;
     const float pfx = (float)px, pfy = (float)py;
     uint2 range = ranges[tile];
@@ -651,8 +665,9 @@ __global__ __launch_bounds__(256) void k_blend_bwd(const uint2 *__restrict__ ran
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const float tx0 = (float)((tile % gx) * TILE_X), ty0 = (float)((tile / gx) * TILE_Y);
-    const int px = (tile % gx) * TILE_X + (tid % TILE_X);
-    const int py = (tile / gx) * TILE_Y + (tid / TILE_X);
+    const int2 tp = tile_pixel(tid);
+    const int px = (tile % gx) * TILE_X + tp.x;
+    const int py = (tile / gx) * TILE_Y + tp.y;
     const bool inside = px < W && py < H;
     const float pfx = (float)px, pfy = (float)py;
     uint2 range = ranges[tile];
