@@ -1,8 +1,9 @@
 """One rank of the 2-rank training-step test (tests/test_gpu_dist_step.py); not collected by pytest.
 
 Env: torchrun-style RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT, DGS_DEVICE=0 (both ranks on the
-one GPU) and DGS_DIST_BACKEND=gloo (RCCL refuses two ranks on one device). argv: out_dir mode, mode
-"plain" or "overflow" (rank 1 forces its deferred pair count to overflow: every rank must redo).
+one GPU) and DGS_DIST_BACKEND=gloo (RCCL refuses two ranks on one device). argv: out_dir mode [6dof], mode
+"plain" or "overflow" (rank 1 forces its deferred pair count to overflow: every rank must redo);
+"6dof": the screw deformation head of config 4 (trex --is_6dof) instead of d_xyz.
 Writes out_dir/rank{r}.pt = {"grads", "params", "redone"}.
 """
 import os
@@ -15,7 +16,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "deformable-3d-gaussians_amd"), HERE]
 import torch  # noqa: E402
 
 
-def build(dev, n=4000, res=128):
+def build(dev, n=4000, res=128, six=False):
     """The test's model / cameras / targets (identical on every rank and in the parent)."""
     from deformgs.arguments import OptimizationParams
     from deformgs.deform_model import DeformModelBaseline
@@ -26,9 +27,11 @@ def build(dev, n=4000, res=128):
     gs = GaussianModel(3)
     gs.from_tensors(g["xyz"], g["features_dc"], g["features_rest"], g["scaling"], g["rotation"], g["opacity"])
     gs.training_setup(OptimizationParams())
-    deform = DeformModelBaseline(is_blender=True, is_6dof=False, device=dev)
+    deform = DeformModelBaseline(is_blender=True, is_6dof=six, device=dev)
+    net = deform.deform
+    heads = (net.branch_w, net.branch_v) if six else (net.gaussian_warp,)
     with torch.no_grad():
-        for h in (deform.deform.gaussian_warp, deform.deform.gaussian_rotation, deform.deform.gaussian_scaling):
+        for h in heads + (net.gaussian_rotation, net.gaussian_scaling):
             h.weight.mul_(0.01)
             h.bias.mul_(0.01)
     deform.train_setting(OptimizationParams())
@@ -45,6 +48,7 @@ def params_of(gs, deform):
 
 def main():
     out_dir, mode = sys.argv[1], sys.argv[2]
+    six = len(sys.argv) > 3 and sys.argv[3] == "6dof"
     from deformgs import _lib
     from deformgs.arguments import PipelineParams
     from deformgs.dist import OverflowAgreement, OverlappedGradAllReduce, init_from_env
@@ -53,20 +57,20 @@ def main():
     rank, world, local = init_from_env()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    gs, deform, cams, gts = build(dev)
+    gs, deform, cams, gts = build(dev, six=six)
     bg = torch.zeros(3, device=dev)
     allreduce = OverlappedGradAllReduce(lambda: params_of(gs, deform)[:6], lambda: list(deform.deform.parameters()))
     agreement = OverflowAgreement()
     lib = _lib.load()
     # learn the pair capacity on a synchronous render of this rank's frame, then (overflow mode)
     # shrink rank 1's so its deferred count overflows
-    train_step(gs, deform, cams[rank], gts[rank], PipelineParams(), bg, deferred_count=False, allreduce=allreduce,
+    train_step(gs, deform, cams[rank], gts[rank], PipelineParams(), bg, six, deferred_count=False, allreduce=allreduce,
                agreement=agreement)
     gs.optimizer.zero_grad(set_to_none=True)
     deform.optimizer.zero_grad(set_to_none=True)
     if mode == "overflow" and rank == 1:
         lib.dgs_debug_set_pair_cap(local, 100)
-    loss, pkg, redone = train_step(gs, deform, cams[rank], gts[rank], PipelineParams(), bg, deferred_count=True,
+    loss, pkg, redone = train_step(gs, deform, cams[rank], gts[rank], PipelineParams(), bg, six, deferred_count=True,
                                    allreduce=allreduce, agreement=agreement)
     grads = [p.grad.detach().clone().cpu() for p in params_of(gs, deform)]
     optimizer_step(gs, deform, 3000)

@@ -29,7 +29,7 @@ def _free_port():
     return p
 
 
-def _single_rank_grads():
+def _single_rank_grads(six=False):
     sys.path.insert(0, HERE)
     from dist_step_worker import build, params_of
     from deformgs.arguments import PipelineParams
@@ -37,22 +37,24 @@ def _single_rank_grads():
     dev = torch.device("cuda", 0)
     out = []
     for k in range(2):
-        gs, deform, cams, gts = build(dev)
-        train_step(gs, deform, cams[k], gts[k], PipelineParams(), torch.zeros(3, device=dev), deferred_count=False)
+        gs, deform, cams, gts = build(dev, six=six)
+        train_step(gs, deform, cams[k], gts[k], PipelineParams(), torch.zeros(3, device=dev), six, deferred_count=False)
         out.append([p.grad.detach().clone().cpu() for p in params_of(gs, deform)])
     return out
 
 
 @pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")
-@pytest.mark.parametrize("mode", ["plain", "overflow"])
+@pytest.mark.parametrize("mode", ["plain", "overflow", "6dof"])
 def test_two_rank_step_averages_gradients(tmp_path, mode):
+    """mode 6dof: config 4's screw deformation head (trex --is_6dof), plain deferred step."""
+    six = mode == "6dof"
     port = _free_port()
     procs = []
     for r in range(2):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), DGS_DEVICE="0", DGS_DIST_BACKEND="gloo")
         procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "dist_step_worker.py"), str(tmp_path),
-                                       mode], env=env, cwd=ROOT))
+                                       "plain" if six else mode] + (["6dof"] if six else []), env=env, cwd=ROOT))
     rcs = []
     for p in procs:
         try:
@@ -67,7 +69,7 @@ def test_two_rank_step_averages_gradients(tmp_path, mode):
         assert r0["redone"] and r1["redone"], "an overflow on one rank must be redone on every rank"
     else:
         assert not r0["redone"] and not r1["redone"]
-    single = _single_rank_grads()
+    single = _single_rank_grads(six)
     for i, (a, b, s0, s1) in enumerate(zip(r0["grads"], r1["grads"], *single)):
         assert torch.equal(a, b), f"reduced gradient {i} differs between ranks"
         want = (s0 + s1) / 2
