@@ -787,6 +787,187 @@ __global__ __launch_bounds__(256) void k_blend_bwd(const uint2 *__restrict__ ran
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Blend backward, two pixels per lane (the default): a 16x16 tile runs as ONE 128-thread workgroup of
+// two waves; wave w covers the 16x8 half (rows 8w..8w+7), lane l the pixel pair (l & 7, row) and
+// (8 + (l & 7), row): one dy, a packed dx, so the per-(pixel, Gaussian) arithmetic runs as packed fp32
+// (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: two pixels per instruction), and the per-(wave,
+// Gaussian) gradient reduction covers 128 pixels instead of 64 (half as many reductions and atomics
+// per Gaussian). Per-pixel activity that k_blend_bwd expresses with the exec mask becomes selects:
+// an inactive pixel of a pair keeps its state and contributes zero. 128 Gaussians staged per round
+// (6 KB of LDS: staging 256, two per thread, took 0.29 ms: 24 KB per workgroup capped the occupancy).
+// blend_bwd 0.315-0.322 -> 0.283 ms at P = 1.0 M pairs (A/B against DGS_BLEND1=1).
+// (The same packing in the forward was slower: 0.137 vs 0.127 ms; its per-Gaussian work is too small
+// to pay for half the waves per tile.)
+// ------------------------------------------------------------------------------------------------
+typedef float f2 __attribute__((ext_vector_type(2)));
+constexpr int B2 = 128;  // threads per tile (two waves), Gaussians staged per round
+
+// Block-wide stable compaction slot of a kept item over NW waves: (slot, kept count)
+template <int NW>
+__device__ __forceinline__ int2 compact_slot_n(bool keep, int tid, uint32_t *s_wcnt) {
+    const unsigned long long m = __ballot(keep);
+    const int lane = tid & 63, wave = tid >> 6;
+    const int below = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) s_wcnt[wave] = (uint32_t)__popcll(m);
+    __syncthreads();
+    int base = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+        const int c = (int)s_wcnt[w];
+        base += w < wave ? c : 0;
+        tot += c;
+    }
+    return make_int2(base + below, tot);
+}
+
+__device__ __forceinline__ f2 sel2(bool a, bool b, f2 x, f2 y) { return f2{a ? x.x : y.x, b ? x.y : y.y}; }
+
+#ifdef DGS_BWD2_WAVES  // experiment: occupancy target (registers capped accordingly)
+#define BWD2_OCC __attribute__((amdgpu_waves_per_eu(DGS_BWD2_WAVES)))
+#else
+#define BWD2_OCC
+#endif
+__global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restrict__ ranges, const uint32_t *__restrict__ vals,
+                                                   uint32_t cap, int W, int H, int gx, const float *bg,
+                                                   const float2 *__restrict__ xy, const float4 *__restrict__ conic_o,
+                                                   const float4 *__restrict__ rgbd, const float *__restrict__ final_T,
+                                                   const uint32_t *__restrict__ n_contrib,
+                                                   const float *__restrict__ dL_dpix, const float *__restrict__ dL_ddepth,
+                                                   float *__restrict__ acc) {
+    __shared__ float2 s_xy[B2];
+    __shared__ float4 s_co[B2];
+    __shared__ float4 s_cd[B2];
+    __shared__ uint32_t s_id[B2];
+    __shared__ int s_pos[B2];
+    __shared__ uint32_t s_wcnt[B2 / 64];
+    __shared__ uint32_t s_maxlast;
+    const int tile = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int tx0 = (tile % gx) * TILE_X, ty0 = (tile / gx) * TILE_Y;
+    const int px0 = tx0 + (lane & 7), px1 = px0 + 8, py = ty0 + 8 * (tid >> 6) + (lane >> 3);
+    const bool in0 = px0 < W && py < H, in1 = px1 < W && py < H;
+    const f2 pfx = f2{(float)px0, (float)px1};
+    const float pfy = (float)py;
+    uint2 range = ranges[tile];
+    range.x = min(range.x, cap);  // a deferred count not resolved yet: the launched capacity bounds the list
+    range.y = min(range.y, cap);
+    const int HW = H * W;
+    const int pid0 = py * W + px0, pid1 = py * W + px1;
+    f2 Tfinal = f2{1.f, 1.f}, dp0 = f2{0.f, 0.f}, dp1 = dp0, dp2 = dp0, ddep = dp0;
+    uint32_t last0 = 0, last1 = 0;
+    if (in0) {
+        Tfinal.x = final_T[pid0];
+        last0 = n_contrib[pid0];
+        dp0.x = dL_dpix[pid0];
+        dp1.x = dL_dpix[HW + pid0];
+        dp2.x = dL_dpix[2 * HW + pid0];
+        ddep.x = dL_ddepth ? dL_ddepth[pid0] : 0.f;
+    }
+    if (in1) {
+        Tfinal.y = final_T[pid1];
+        last1 = n_contrib[pid1];
+        dp0.y = dL_dpix[pid1];
+        dp1.y = dL_dpix[HW + pid1];
+        dp2.y = dL_dpix[2 * HW + pid1];
+        ddep.y = dL_ddepth ? dL_ddepth[pid1] : 0.f;
+    }
+    if (tid == 0) s_maxlast = 0;
+    __syncthreads();
+    atomicMax(&s_maxlast, max(last0, last1));
+    __syncthreads();
+    const int todo_total = (int)s_maxlast;  // Gaussians past every pixel's last contributor are skipped
+    const float b0 = bg[0], b1 = bg[1], b2 = bg[2];
+    const f2 bgdot = b0 * dp0 + b1 * dp1 + b2 * dp2;
+    const float hx = 0.5f * W, hy = 0.5f * H;
+    f2 T = Tfinal;
+    const f2 zero = f2{0.f, 0.f};
+    f2 acc0 = zero, acc1 = zero, acc2 = zero, accd = zero;
+    f2 lc0 = zero, lc1 = zero, lc2 = zero, lcd = zero, last_alpha = zero;
+    const int rounds = div_up(todo_total, B2);
+    const int end = (int)range.x + todo_total;
+    for (int r = 0; r < rounds; r++) {
+        __syncthreads();
+        const int prog = r * B2 + tid;
+        bool keep = false;
+        uint32_t id = 0;
+        float2 gl;
+        float4 cl;
+        if (prog < todo_total) {
+            id = vals[end - prog - 1];
+            gl = xy[id];
+            cl = conic_o[id];
+            keep = tile_reach(gl, cl, (float)tx0, (float)ty0);
+        }
+        const int2 sl = compact_slot_n<B2 / 64>(keep, tid, s_wcnt);
+        if (keep) {
+            s_id[sl.x] = id;
+            s_xy[sl.x] = gl;
+            s_co[sl.x] = cl;
+            s_cd[sl.x] = rgbd[id];
+            s_pos[sl.x] = prog;
+        }
+        __syncthreads();
+        const int n = sl.y;
+        for (int j = 0; j < n; j++) {
+            const uint32_t contributor = (uint32_t)(todo_total - 1 - s_pos[j]);  // position in the full list
+            const float2 g = s_xy[j];
+            const float4 co = s_co[j];
+            const f2 dx = g.x - pfx;
+            const float dy = g.y - pfy;
+            const f2 power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+            const f2 G = f2{__expf(power.x), __expf(power.y)};
+            const f2 alpha = f2{fminf(0.99f, co.w * G.x), fminf(0.99f, co.w * G.y)};
+            const bool act0 = in0 && contributor < last0 && power.x <= 0.f && alpha.x >= 1.f / 255.f;
+            const bool act1 = in1 && contributor < last1 && power.y <= 0.f && alpha.y >= 1.f / 255.f;
+            if (__ballot(act0 || act1) == 0ull) continue;  // wave-uniform
+            const float4 cd = s_cd[j];
+            // 1 / (1 - alpha): hardware reciprocal + one Newton step (<= 1 ulp)
+            const f2 om = 1.f - alpha;
+            f2 inv = f2{__builtin_amdgcn_rcpf(om.x), __builtin_amdgcn_rcpf(om.y)};
+            inv = inv * (1.f - om * inv) + inv;
+            const f2 Tn = T * inv;
+            // the pending contribution of the previous active Gaussian of each pixel; an inactive
+            // pixel of the pair takes none (la = 0) and keeps its state below
+            const f2 la = sel2(act0, act1, last_alpha, zero);
+            acc0 = la * lc0 + (1.f - la) * acc0;
+            acc1 = la * lc1 + (1.f - la) * acc1;
+            acc2 = la * lc2 + (1.f - la) * acc2;
+            accd = la * lcd + (1.f - la) * accd;
+            const f2 w = sel2(act0, act1, alpha * Tn, zero);
+            f2 dLda = (cd.x - acc0) * dp0 + (cd.y - acc1) * dp1 + (cd.z - acc2) * dp2 + (cd.w - accd) * ddep;
+            dLda = dLda * Tn + (-Tfinal * inv) * bgdot;
+            dLda = sel2(act0, act1, dLda, zero);
+            lc0 = sel2(act0, act1, f2{cd.x, cd.x}, lc0);
+            lc1 = sel2(act0, act1, f2{cd.y, cd.y}, lc1);
+            lc2 = sel2(act0, act1, f2{cd.z, cd.z}, lc2);
+            lcd = sel2(act0, act1, f2{cd.w, cd.w}, lcd);
+            last_alpha = sel2(act0, act1, alpha, last_alpha);
+            T = sel2(act0, act1, Tn, T);
+            const f2 dLdG = co.w * dLda;
+            const f2 gdx = G * dx, gdy = G * dy;
+            const f2 dGdx = -gdx * co.x - gdy * co.y;
+            const f2 dGdy = -gdy * co.z - gdx * co.y;
+            const f2 vmx = dLdG * dGdx * hx, vmy = dLdG * dGdy * hy;
+            const f2 vcx = -0.5f * gdx * dx * dLdG, vcy = -0.5f * gdx * dy * dLdG, vcz = -0.5f * gdy * dy * dLdG;
+            const f2 vop = G * dLda;
+            const f2 vr = w * dp0, vg = w * dp1, vb = w * dp2, vd = w * ddep;
+            // the pair's sums, then the reduce-scatter over the wave (as k_blend_bwd)
+            const float w0 = row_sum15(fold16(fold32(vmx.x + vmx.y, vmy.x + vmy.y), fold32(vcx.x + vcx.y, vcy.x + vcy.y)));
+            const float w1 = row_sum15(fold16(fold32(vcz.x + vcz.y, vop.x + vop.y), fold32(vr.x + vr.y, vg.x + vg.y)));
+            const float w2 = row_sum15(fold16(fold32(vb.x + vb.y, vd.x + vd.y),
+                                              fold32(fabsf(vmx.x) + fabsf(vmx.y), fabsf(vmy.x) + fabsf(vmy.y))));
+            if ((lane & 15) == 15) {
+                const int row = lane >> 4;
+                float *dst = acc + (size_t)s_id[j] * ACC_STRIDE + ((row & 1) << 1) + (row >> 1);
+                atomicAdd(dst, w0);
+                atomicAdd(dst + 4, w1);
+                atomicAdd(dst + 8, w2);
+            }
+        }
+    }
+}
+
 __device__ inline void dR_dq(float4 q, const float dR[9], float4 &dq) {
     float r = q.x, x = q.y, y = q.z, z = q.w;
     dq.x = 2.f * (-z * dR[1] + y * dR[2] + z * dR[3] - x * dR[5] - y * dR[6] + x * dR[7]);
@@ -1141,6 +1322,16 @@ std::mutex g_pool_mu;
 std::vector<dgs_raster_ctx *> g_pool;
 
 size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
+
+// DGS_BLEND1=1: the one-pixel-per-lane blend backward (k_blend_bwd, 4 waves per tile) instead of the
+// packed two-pixel one (k_blend_bwd2, the default)
+bool blend_one_pixel() {
+    static const bool v = [] {
+        const char *e = getenv("DGS_BLEND1");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
 
 // DGS_HIPCUB_SORT=1: hipcub::DeviceRadixSort for the depth and tile sorts instead of radix.hip
 bool hipcub_sort() {
@@ -1697,8 +1888,12 @@ static int raster_backward(dgs_raster_ctx *c, const float *dL_dcolor, const floa
     c->bwd_done = true;
     if (cap > 0) {
         ScopedTimer tm("blend_bwd", stream);
-        hipLaunchKernelGGL(k_blend_bwd, dim3(T), dim3(TILE_PIX), 0, stream, c->ranges, c->vals, cap, c->W, c->H, c->gx,
-                           c->s.bg, c->xy, c->conic_o, c->rgbd, c->final_T, c->n_contrib, dL_dcolor, dL_ddepth, acc);
+        if (blend_one_pixel())
+            hipLaunchKernelGGL(k_blend_bwd, dim3(T), dim3(TILE_PIX), 0, stream, c->ranges, c->vals, cap, c->W, c->H, c->gx,
+                               c->s.bg, c->xy, c->conic_o, c->rgbd, c->final_T, c->n_contrib, dL_dcolor, dL_ddepth, acc);
+        else
+            hipLaunchKernelGGL(k_blend_bwd2, dim3(T), dim3(B2), 0, stream, c->ranges, c->vals, cap, c->W, c->H, c->gx,
+                               c->s.bg, c->xy, c->conic_o, c->rgbd, c->final_T, c->n_contrib, dL_dcolor, dL_ddepth, acc);
     }
     DGS_LAUNCH_CHECK("k_blend_bwd", dbg, stream);
     const float fx = c->W / (2.f * c->s.tanfovx), fy = c->H / (2.f * c->s.tanfovy);
