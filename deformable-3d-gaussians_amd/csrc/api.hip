@@ -23,6 +23,8 @@ struct Pending {
 std::vector<Pending> g_pending;
 std::vector<hipEvent_t> g_free_events;
 std::map<std::string, std::pair<double, int>> g_acc;
+int g_period = 1;                      // time every g_period-th launch of a class (dgs_timing_sample)
+std::map<std::string, long long> g_seen;  // launches of each selected class since the last reset
 
 hipEvent_t take_event() {
     if (!g_free_events.empty()) {
@@ -69,6 +71,8 @@ ScopedTimer::ScopedTimer(const char *n, hipStream_t s) : name(n), stream(s), ev0
     if (!g_timing) return;
     std::lock_guard<std::mutex> lk(g_tmu);
     if (!g_timing_sel.empty() && !g_timing_sel.count(n)) return;
+    // each event record is a stream marker (~6 us of GPU idle): sampled launches only
+    if (g_period > 1 && (g_seen[n]++ % g_period) != 0) return;
     hipEvent_t e = take_event();
     (void)hipEventRecord(e, stream);
     ev0 = (void *)e;
@@ -125,4 +129,10 @@ extern "C" void dgs_timing_reset(void) {
     std::lock_guard<std::mutex> lk(dgs::g_tmu);
     dgs::drain_locked();
     dgs::g_acc.clear();
+    dgs::g_seen.clear();
+}
+
+extern "C" void dgs_timing_sample(int period) {
+    std::lock_guard<std::mutex> lk(dgs::g_tmu);
+    dgs::g_period = period < 1 ? 1 : period;
 }

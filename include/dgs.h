@@ -147,6 +147,9 @@ void dgs_timing_select(const char *csv);
 /* Returns accumulated ms for kernel class `name` and its launch count (host); syncs those events. */
 double dgs_timing_query(const char *name, int *launches);
 void dgs_timing_reset(void);
+/* Time only every `period`-th launch of each selected class (1 = every launch, the default): each
+ * timed launch costs two stream markers, ~6 us of GPU idle each. */
+void dgs_timing_sample(int period);
 
 /* ---- deformation MLP (utils/time_utils.py:56-201), fused PE + 8x256 MLP ----
  * Default: fp32 GEMMs on bf16 MFMA over an exact hi/mid/lo operand split (six products per fp32
