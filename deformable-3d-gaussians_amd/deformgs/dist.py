@@ -180,7 +180,20 @@ class OverflowAgreement:
         if not dist.is_initialized() or dist.get_world_size(self.group) == 1:
             return bool(local_overflow)
         if self._gloo is None:
-            self._gloo = self.group if dist.get_backend(self.group) == "gloo" else dist.new_group(backend="gloo")
+            if dist.get_backend(self.group) == "gloo":
+                self._gloo = self.group
+            else:
+                try:  # a host group beside RCCL; DGS_AGREE_BACKEND=default keeps the flag on the main group
+                    if os.environ.get("DGS_AGREE_BACKEND", "gloo") != "gloo":
+                        raise RuntimeError("host group disabled")
+                    self._gloo = dist.new_group(backend="gloo")
+                except Exception:  # (same outcome on every rank: the group is created collectively)
+                    self._gloo = False
+        if self._gloo is False:  # a device flag on the main group (queues behind its collectives)
+            dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
+            flag = torch.tensor([1 if local_overflow else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+            return bool(flag.item())
         flag = torch.tensor([1 if local_overflow else 0], dtype=torch.int32)
         dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self._gloo)
         return bool(flag.item())
