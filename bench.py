@@ -354,7 +354,8 @@ def main():
                    + (" (raw-init heads)" if args.raw_init else " (heads at 1/100 init: steady-state deltas)"),
                    "global_batch": world, "includes_adam": not args.no_adam, "pairs_per_render": P_pairs,
                    "pair_capacity": pair_cap, "redone_steps": state["redos"],
-                   "parallelism": f"dp{world} (frame-parallel, RCCL grad all-reduce)"},
+                   "parallelism": f"dp{world} (frame-parallel, "
+                   + ("RCCL" if world == 1 or dist.get_backend() == "nccl" else dist.get_backend()) + " grad all-reduce)"},
         "roofline": roofline,
         "kernels_ms_per_step": {k: v[0] / args.steps for k, v in kernels.items()},
         # host time per step: issuing forward + backward (including the wait for the pair count
