@@ -165,7 +165,12 @@ struct WPlan {
 // Splits: per-chunk cost = the busiest SIMD's MFMA tiles (waves w and w + 4 share SIMD w % 4) plus a
 // per-chunk staging/barrier cost (`fixed`), floored at `floor_`; the smallest per-workgroup time whose
 // ceil(cost * nch / T) fit `target` workgroups (whole jobs never straddle).
-inline WPlan make_wplan(const Flags &F, int target, double fixed, double floor_) {
+// shape_cost (optional, the split k_dws): measured per-chunk cost of the four job shapes instead of
+// the MFMA-tile model, indexed by dw_shape().
+inline int dw_shape(int nrows, int krows) {
+    return krows == 256 ? (nrows == 256 ? 0 : 1) : (krows > 32 ? 2 : 3);
+}
+inline WPlan make_wplan(const Flags &F, int target, double fixed, double floor_, const double *shape_cost = nullptr) {
     WPlan W{};
     struct Raw {
         int zrow, nrows, xrow, krows, layer, kt;
@@ -205,6 +210,7 @@ inline WPlan make_wplan(const Flags &F, int target, double fixed, double floor_)
         int crit = simd[0];
         for (int s = 1; s < 4; s++) crit = simd[s] > crit ? simd[s] : crit;
         cost[q] = crit + fixed > floor_ ? crit + fixed : floor_;
+        if (shape_cost) cost[q] = shape_cost[dw_shape(raw[q].nrows, raw[q].krows)];
         total += cost[q];
     }
     const int nch = 1 << 20;  // relative scale only (the chunk count cancels)

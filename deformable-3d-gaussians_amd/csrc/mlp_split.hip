@@ -186,6 +186,30 @@ struct NoPre {
 // counts into dgs_mlps_guard_expired (a global atomic from one lane), which the host reads with
 // dgs_debug_guard_expiries() and every GPU test checks to be 0 (outputs after an expiry are invalid).
 __device__ uint32_t dgs_mlps_guard_expired;
+
+#ifdef DGS_CLOCK_STAMPS
+// Diagnostic build only (tools/mlp_clock.py): per-workgroup in-kernel clock of k_fwd / k_bwd / k_dws
+// (MI355X_MICROARCH 'DVFS give-back' item 6): shader-clock and 100 MHz real-time stamps of wave 0 at
+// block start and end, into a buffer no kernel reads. The product build has no stamps.
+constexpr int CLK_BLOCKS = 2048;
+__device__ unsigned long long dgs_clk[3][CLK_BLOCKS][4];
+struct ClkStamp {
+    unsigned long long t, r;
+    __device__ ClkStamp() : t(__builtin_amdgcn_s_memtime()), r(__builtin_amdgcn_s_memrealtime()) {}
+    __device__ void end(int k) const {
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        if (threadIdx.x == 0 && blockIdx.x < CLK_BLOCKS) {
+            unsigned long long *p = dgs_clk[k][blockIdx.x];
+            p[0] = t; p[1] = t1; p[2] = r; p[3] = r1;
+        }
+    }
+};
+#define CLK_BEGIN() const ClkStamp clk_
+#define CLK_END(k) clk_.end(k)
+#else
+#define CLK_BEGIN()
+#define CLK_END(k)
+#endif
 __device__ __forceinline__ uint32_t lds_peek(const uint32_t *f) {
     return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -653,8 +677,10 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
     __shared__ bf16x8 lds[G_FWD * UG];
     __shared__ uint32_t hwr[8], hrd[8];  // trunk hand-off counters (HGate)
     const int b = blockIdx.x;
+    CLK_BEGIN();
     if (b < a.nfull) fwd_block<SAVE, NQ>(a, lds, hwr, hrd, b * BM, b);
     else fwd_block<SAVE, 1>(a, lds, hwr, hrd, a.nfull * BM + (b - a.nfull) * 16, b);
+    CLK_END(0);
 }
 
 
@@ -777,8 +803,10 @@ __global__ __launch_bounds__(NTHR) void k_bwd(BwdArgs a) {
     __shared__ bf16x8 lds[G_BWD * UG];
     __shared__ uint32_t hwr[8], hrd[8];  // dZ hand-off counters (HGate), as in k_fwd's trunk
     const int b = blockIdx.x;
+    CLK_BEGIN();
     if (b < a.nfull) bwd_block<TE_ROWS, NQ>(a, lds, hwr, hrd, b * BM, b);
     else bwd_block<TE_ROWS, 1>(a, lds, hwr, hrd, a.nfull * BM + (b - a.nfull) * 16, b);
+    CLK_END(1);
 }
 
 // Timenet gradients for a frame-uniform t (DGS_MLP_UNIFORM_T). With one TIN / TH for every point,
@@ -1425,6 +1453,7 @@ __global__ __launch_bounds__(DW_THREADS) void k_dws(WJobs JT, size_t Ns, const f
         if (q < JT.n && (int)blockIdx.x >= JT.j[q].block0) J = JT.j[q];
     // job shapes (host-checked in dw_split_once): krows = 256 with nrows 256 or 32 -> COL; nrows =
     // 256 with krows 96 or 16 -> ROW
+    CLK_BEGIN();
     if (J.krows == 256) {
         if (J.nrows == 256)
             dws_run<true, 8>(J, Ns, dz, saved, slabs, dws_lds);
@@ -1435,6 +1464,7 @@ __global__ __launch_bounds__(DW_THREADS) void k_dws(WJobs JT, size_t Ns, const f
     } else {
         dws_run<false, 1>(J, Ns, dz, saved, slabs, dws_lds);
     }
+    CLK_END(2);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1621,7 +1651,19 @@ static int *pack_map_for(const Plan &P, int flags) {
 }
 
 // dW split plan: one 8-wave workgroup per CU (LDS 144 KiB); per-chunk cost in MFMA tiles + staging
-static WPlan split_wplan(const Flags &F) { return make_wplan(F, 256, 1.5, 4.0); }
+// k_dws per-chunk cost by job shape (dw_shape: COL 256x256, COL 32-row head, ROW 96-col, ROW 16-col),
+// relative to the full tile, from the per-workgroup durations of tools/mlp_clock.py at 100k points
+// (profiles/r3p_mlp_clock_before.json: a full-tile chunk 4.5 us, a 96-col chunk 2.6 us, a head chunk
+// 1.5 us; the MFMA-tile model gave the narrow jobs too few workgroups, which then finished 25 % after
+// the rest. With these costs every job's workgroups end within 4 %: profiles/r3p_mlp_clock.json)
+static const double kDwsShapeCost[4] = {1.0, 0.33, 0.58, 0.30};
+static WPlan split_wplan(const Flags &F) {
+    static const bool model = [] {  // A/B only: the MFMA-tile cost model
+        const char *e = getenv("DGS_DWS_TILE_MODEL");
+        return e && *e == '1';
+    }();
+    return make_wplan(F, 256, 1.5, 4.0, model ? nullptr : kDwsShapeCost);
+}
 static int dw_split(const Flags &F, size_t Ns, const float *dz, const float *saved, float *slabs, float *const *grads,
                     hipStream_t stream);
 
@@ -1869,6 +1911,21 @@ static int net_flags(int flags) {
     return exact_fp32(flags) ? flags & (DGS_MLP_BLENDER | DGS_MLP_6DOF | DGS_MLP_NO_ROTSCALE)
                              : flags & (DGS_MLP_BLENDER | DGS_MLP_6DOF | DGS_MLP_NO_ROTSCALE | DGS_MLP_UNIFORM_T);
 }
+
+#ifdef DGS_CLOCK_STAMPS
+// kernel k (0 k_fwd, 1 k_bwd, 2 k_dws): the last launch's per-workgroup stamps, out[b] = (shader
+// cycles, real-time ticks at 100 MHz) for b < n (diagnostic builds only)
+extern "C" int dgs_debug_clock(int k, int n, unsigned long long *out) {
+    static unsigned long long h[mlps::CLK_BLOCKS][4];
+    if (k < 0 || k > 2 || n > mlps::CLK_BLOCKS) return -1;
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(dgs::mlps::dgs_clk), sizeof(h), sizeof(h) * k) != hipSuccess) return -1;
+    for (int b = 0; b < n; b++) {
+        out[2 * b] = h[b][1] - h[b][0];
+        out[2 * b + 1] = h[b][3] - h[b][2];
+    }
+    return 0;
+}
+#endif
 
 extern "C" long long dgs_debug_guard_expiries(void) {
     uint32_t v = 0;
