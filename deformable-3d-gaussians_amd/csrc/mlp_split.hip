@@ -192,7 +192,7 @@ __device__ uint32_t dgs_mlps_guard_expired;
 // (MI355X_MICROARCH 'DVFS give-back' item 6): shader-clock and 100 MHz real-time stamps of wave 0 at
 // block start and end, into a buffer no kernel reads. The product build has no stamps.
 constexpr int CLK_BLOCKS = 2048;
-__device__ unsigned long long dgs_clk[3][CLK_BLOCKS][4];
+__device__ unsigned long long dgs_clk[3][CLK_BLOCKS][6];
 struct ClkStamp {
     unsigned long long t, r;
     __device__ ClkStamp() : t(__builtin_amdgcn_s_memtime()), r(__builtin_amdgcn_s_memrealtime()) {}
@@ -201,6 +201,9 @@ struct ClkStamp {
         if (threadIdx.x == 0 && blockIdx.x < CLK_BLOCKS) {
             unsigned long long *p = dgs_clk[k][blockIdx.x];
             p[0] = t; p[1] = t1; p[2] = r; p[3] = r1;
+            // HW_ID (CU / SH / SE fields) and XCC_ID: which CU ran the workgroup
+            p[4] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+                   ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);
         }
     }
 };
@@ -392,6 +395,22 @@ __device__ inline void zero_tiles(f32x4 (&v)[NQ_]) {
 // ------------------------------------------------------------------------------------------------
 // forward
 // ------------------------------------------------------------------------------------------------
+// Persistent launches (round 3): one workgroup per CU runs block after block, taking the next block
+// index from a device counter, so faster XCDs take more blocks. The eight XCDs hold different clocks
+// under this load (1.80-2.04 GHz measured, tools/mlp_clock.py) and the hardware hands workgroups to
+// XCDs round-robin, so with one launch block per block the slowest XCD set the kernel time. Block b
+// computes exactly what it computed before (same points, same mask slot): outputs are bitwise
+// unchanged. The index of the next block is fetched at the start of the current one (latency hidden
+// by the block); the last workgroup to finish zeroes the counter pair for the next launch.
+__device__ __forceinline__ int queue_take(uint32_t *q) { return (int)gridDim.x + (int)atomicAdd(q, 1u); }
+__device__ __forceinline__ void queue_release(uint32_t *q) {
+    // every workgroup's final take has returned before its increment of q[1]
+    if (threadIdx.x == 0 && atomicAdd(q + 1, 1u) == gridDim.x - 1) {
+        atomicExch(q, 0u);
+        atomicExch(q + 1, 0u);
+    }
+}
+
 struct FwdArgs {
     int N;
     size_t Ns;
@@ -407,6 +426,8 @@ struct FwdArgs {
     int bT1, bT2, bL[8], bHd;      // fp32 offsets
     int wT1, wT2;                  // fp32 timenet weights [256][16], [32][256]
     int flags;
+    uint32_t *queue;  // block queue (persistent launch, BlockQueue) or nullptr: one launch block per block
+    int nblk;         // blocks (64-point + 16-point)
 };
 
 // The reference feeds every Gaussian the same frame time (train_baseline.py:107-110), so the
@@ -469,7 +490,11 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
     constexpr int BMB = 16 * NQB;  // points of this block (the LDS images keep the BM-point stride)
     float *lf = reinterpret_cast<float *>(lds);
     float *stage = lf + G_H * UG * 4;  // fp32 [112][BM] feature staging (H region, before the trunk)
-    const int tid = threadIdx.x, lane = tid & 63;
+    // re-derived per block (opaque to loop-invariant hoisting): in the persistent loop, lane
+    // addresses hoisted out of it would stay live across the whole block and spill
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63;
     const int r = __builtin_amdgcn_readfirstlane(tid >> 6);  // n-tile of this wave (provably uniform)
     const int kq = lane >> 4, col = lane & 15;
     const int pend = min(a.N, p0 + BMB);  // real points of the block: [p0, pend)
@@ -676,10 +701,20 @@ template <bool SAVE>
 __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
     __shared__ bf16x8 lds[G_FWD * UG];
     __shared__ uint32_t hwr[8], hrd[8];  // trunk hand-off counters (HGate)
-    const int b = blockIdx.x;
+    __shared__ int s_next;
     CLK_BEGIN();
-    if (b < a.nfull) fwd_block<SAVE, NQ>(a, lds, hwr, hrd, b * BM, b);
-    else fwd_block<SAVE, 1>(a, lds, hwr, hrd, a.nfull * BM + (b - a.nfull) * 16, b);
+    for (int b = blockIdx.x;;) {
+        int nx = 0;
+        if (a.queue && threadIdx.x == 0) nx = queue_take(a.queue);
+        if (b < a.nfull) fwd_block<SAVE, NQ>(a, lds, hwr, hrd, b * BM, b);
+        else fwd_block<SAVE, 1>(a, lds, hwr, hrd, a.nfull * BM + (b - a.nfull) * 16, b);
+        if (!a.queue) break;
+        if (threadIdx.x == 0) s_next = nx;
+        __syncthreads();  // also: the next block's staging overwrites LDS this one's heads read
+        b = s_next;
+        if (b >= a.nblk) break;
+    }
+    if (a.queue) queue_release(a.queue);
     CLK_END(0);
 }
 
@@ -697,6 +732,8 @@ struct BwdArgs {
     int nfull;            // as FwdArgs::nfull
     int tHd, tL[8], tT2;  // image k-slots
     int flags;
+    uint32_t *queue;      // as FwdArgs
+    int nblk;
 };
 
 // relu' bits of the layer input for this wave's 16 x 64 tile, loaded ahead of the GEMM
@@ -714,7 +751,11 @@ __device__ __forceinline__ void bwd_block(const BwdArgs &a, bf16x8 *lds, uint32_
     constexpr int BMB = 16 * NQB;  // points of this block (fwd_block)
     float *lf = reinterpret_cast<float *>(lds);
     float *stage = lf + G_BH * UG * 4;  // fp32 [32][BM] (H region, before the first dZ)
-    const int tid = threadIdx.x, lane = tid & 63;
+    // re-derived per block (opaque to loop-invariant hoisting): in the persistent loop, lane
+    // addresses hoisted out of it would stay live across the whole block and spill
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63;
     const int r = __builtin_amdgcn_readfirstlane(tid >> 6);
     const Flags F = make_flags(a.flags);
     const size_t Ns = a.Ns;
@@ -802,10 +843,20 @@ template <bool TE_ROWS>
 __global__ __launch_bounds__(NTHR) void k_bwd(BwdArgs a) {
     __shared__ bf16x8 lds[G_BWD * UG];
     __shared__ uint32_t hwr[8], hrd[8];  // dZ hand-off counters (HGate), as in k_fwd's trunk
-    const int b = blockIdx.x;
+    __shared__ int s_next;
     CLK_BEGIN();
-    if (b < a.nfull) bwd_block<TE_ROWS, NQ>(a, lds, hwr, hrd, b * BM, b);
-    else bwd_block<TE_ROWS, 1>(a, lds, hwr, hrd, a.nfull * BM + (b - a.nfull) * 16, b);
+    for (int b = blockIdx.x;;) {  // persistent: as k_fwd
+        int nx = 0;
+        if (a.queue && threadIdx.x == 0) nx = queue_take(a.queue);
+        if (b < a.nfull) bwd_block<TE_ROWS, NQ>(a, lds, hwr, hrd, b * BM, b);
+        else bwd_block<TE_ROWS, 1>(a, lds, hwr, hrd, a.nfull * BM + (b - a.nfull) * 16, b);
+        if (!a.queue) break;
+        if (threadIdx.x == 0) s_next = nx;
+        __syncthreads();
+        b = s_next;
+        if (b >= a.nblk) break;
+    }
+    if (a.queue) queue_release(a.queue);
     CLK_END(1);
 }
 
@@ -1703,6 +1754,32 @@ static Blocks block_split(int N) {
     if (rounds < 2 || last > TAIL_MAX_LAST || 4 * last > ncu) return {nb, 0};
     return {nb - last, 4 * last};
 }
+// Block-queue counters of the persistent k_fwd / k_bwd, one zeroed pair per (device, stream, kernel)
+// (two launches in flight on two streams must not share one). DGS_MLP_STATIC=1: one launch block per
+// block, no queue (A/B).
+static uint32_t *block_queue(hipStream_t stream, int kernel) {
+    static const bool off = [] {
+        const char *e = getenv("DGS_MLP_STATIC");
+        return e && e[0] == '1';
+    }();
+    if (off) return nullptr;
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, uint32_t *> words;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    uint32_t *&w = words[{dev, stream}];
+    if (!w) {
+        if (hipMalloc(&w, 4 * sizeof(uint32_t)) != hipSuccess) {
+            w = nullptr;
+            return nullptr;
+        }
+        if (hipMemset(w, 0, 4 * sizeof(uint32_t)) != hipSuccess) return nullptr;
+    }
+    return w + 2 * kernel;
+}
+static int persistent_grid(int nblk, const uint32_t *queue) { return queue ? std::min(nblk, cu_count()) : nblk; }
+
 static size_t mask_words(const Flags &F, size_t Ns) {
     const size_t nb = Ns / BM;
     return (size_t)F.nmask * 2 * (nb + 3 * std::min<size_t>(nb, TAIL_MAX_LAST));
@@ -1779,6 +1856,9 @@ int forward(int flags, int N, const float *xyz, const float *t, const float *pac
     const Blocks bs = block_split(N);
     a.nfull = bs.nfull;
     const int nblk = bs.nfull + bs.ntail;
+    a.nblk = nblk;
+    a.queue = nblk > 0 ? block_queue(stream, 0) : nullptr;
+    const int grid = persistent_grid(nblk, a.queue);
     {
         ScopedTimer tm("mlp_fwd", stream);
         if (saved && P.F.blender) {
@@ -1786,9 +1866,9 @@ int forward(int flags, int N, const float *xyz, const float *t, const float *pac
             hipLaunchKernelGGL(k_timenet, dim3(1), dim3(256), 0, stream, a);
         }
         if (saved)
-            hipLaunchKernelGGL(k_fwd<true>, dim3(nblk), dim3(NTHR), 0, stream, a);
+            hipLaunchKernelGGL(k_fwd<true>, dim3(grid), dim3(NTHR), 0, stream, a);
         else
-            hipLaunchKernelGGL(k_fwd<false>, dim3(nblk), dim3(NTHR), 0, stream, a);
+            hipLaunchKernelGGL(k_fwd<false>, dim3(grid), dim3(NTHR), 0, stream, a);
     }
     DGS_LAUNCH_CHECK("k_fwd", false, stream);
     return DGS_OK;
@@ -1811,12 +1891,15 @@ int backward(int flags, int N, const float *packed, const float *saved, const fl
     const Blocks bs = block_split(N);
     b.nfull = bs.nfull;
     const int nblk = bs.nfull + bs.ntail;
+    b.nblk = nblk;
+    b.queue = nblk > 0 ? block_queue(stream, 1) : nullptr;
+    const int grid = persistent_grid(nblk, b.queue);
     {
         ScopedTimer tm("mlp_bwd", stream);
         if (F.blender && !F.uniform_t)
-            hipLaunchKernelGGL(k_bwd<true>, dim3(nblk), dim3(NTHR), 0, stream, b);
+            hipLaunchKernelGGL(k_bwd<true>, dim3(grid), dim3(NTHR), 0, stream, b);
         else
-            hipLaunchKernelGGL(k_bwd<false>, dim3(nblk), dim3(NTHR), 0, stream, b);
+            hipLaunchKernelGGL(k_bwd<false>, dim3(grid), dim3(NTHR), 0, stream, b);
     }
     DGS_LAUNCH_CHECK("k_bwd", false, stream);
     int rc;
@@ -1913,16 +1996,15 @@ static int net_flags(int flags) {
 }
 
 #ifdef DGS_CLOCK_STAMPS
-// kernel k (0 k_fwd, 1 k_bwd, 2 k_dws): the last launch's per-workgroup stamps, out[b] = (shader
-// cycles, real-time ticks at 100 MHz) for b < n (diagnostic builds only)
+// kernel k (0 k_fwd, 1 k_bwd, 2 k_dws): the last launch's per-workgroup stamps, out[6 b ..] =
+// (shader clock start, end, 100 MHz real time start, end, HW_ID | XCC_ID << 32, 0) for b < n
+// (diagnostic builds only)
 extern "C" int dgs_debug_clock(int k, int n, unsigned long long *out) {
-    static unsigned long long h[mlps::CLK_BLOCKS][4];
+    static unsigned long long h[mlps::CLK_BLOCKS][6];
     if (k < 0 || k > 2 || n > mlps::CLK_BLOCKS) return -1;
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(dgs::mlps::dgs_clk), sizeof(h), sizeof(h) * k) != hipSuccess) return -1;
-    for (int b = 0; b < n; b++) {
-        out[2 * b] = h[b][1] - h[b][0];
-        out[2 * b + 1] = h[b][3] - h[b][2];
-    }
+    for (int b = 0; b < n; b++)
+        for (int q = 0; q < 6; q++) out[6 * b + q] = h[b][q];
     return 0;
 }
 #endif

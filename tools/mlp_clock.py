@@ -53,20 +53,40 @@ def main():
         iters += 10
     lib.dgs_timing_enable(0)
     out = {"n": a.n, "iters": iters}
-    buf = (ctypes.c_ulonglong * (2 * CLK_BLOCKS))()
+    buf = (ctypes.c_ulonglong * (6 * CLK_BLOCKS))()
     for k, name, tname in ((0, "k_fwd", "mlp_fwd"), (1, "k_bwd", "mlp_bwd"), (2, "k_dws", "mlp_dw")):
         assert fn(k, CLK_BLOCKS, buf) == 0
-        v = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 2).astype(np.float64)
-        v = v[(v[:, 1] > 0) & (v[:, 1] < 1e9)]
-        ghz = v[:, 0] / v[:, 1] * 0.1
+        raw = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 6)
+        # the last launch's workgroups: real-time start within 10 ms of the latest start
+        ok = (raw[:, 3] > raw[:, 2]) & (raw[:, 2] + 1_000_000 > raw[:, 2].max())
+        v = raw[ok].astype(np.float64)
+        cyc, tick = v[:, 1] - v[:, 0], v[:, 3] - v[:, 2]
+        ghz = cyc / tick * 0.1
         n = _lib.I(0)
         ms = lib.dgs_timing_query(tname.encode(), n) / max(n.value, 1)
-        out[name] = {"blocks": int(len(v)), "ghz_median": float(np.median(ghz)), "ghz_min": float(ghz.min()),
-                     "ghz_max": float(ghz.max()), "block_us_median": float(np.median(v[:, 1]) / 100.0),
-                     "kernel_ms": ms, "clock_frac_of_nominal": float(np.median(ghz)) / NOMINAL_GHZ,
-                     "block_us_pct": [float(np.percentile(v[:, 1], q)) / 100.0 for q in (0, 10, 50, 90, 100)]}
-        if k == 2:  # per workgroup, in launch order (jobs own contiguous block ranges)
-            out[name]["block_us"] = [round(float(u) / 100.0, 1) for u in v[:, 1]]
+        span = (v[:, 3].max() - v[:, 2].min()) / 100.0
+        # CU key: XCC id, SE / SH / CU fields of HW_ID (bits 8..15)
+        hw = raw[ok][:, 4]
+        cu = ((hw >> np.uint64(32)) << np.uint64(8)) | ((hw >> np.uint64(8)) & np.uint64(0xFF))
+        keys, inv = np.unique(cu, return_inverse=True)
+        busy = np.bincount(inv, weights=tick) / 100.0
+        nblk = np.bincount(inv)
+        start0 = v[:, 2].min()
+        first = np.array([v[inv == c, 2].min() for c in range(len(keys))]) - start0
+        last = np.array([v[inv == c, 3].max() for c in range(len(keys))]) - start0
+        out[name] = {"blocks": int(len(v)), "ghz_median": float(np.median(ghz)),
+                     "kernel_ms": ms, "span_us": span, "clock_frac_of_nominal": float(np.median(ghz)) / NOMINAL_GHZ,
+                     "block_us_pct": [float(np.percentile(tick, q)) / 100.0 for q in (0, 10, 50, 90, 100)],
+                     "cus": int(len(keys)), "blocks_per_cu": np.bincount(nblk).tolist(),
+                     "cu_busy_us_pct": [float(np.percentile(busy, q)) for q in (0, 10, 50, 90, 100)],
+                     "cu_first_start_us_pct": [float(np.percentile(first, q)) / 100.0 for q in (0, 50, 100)],
+                     "cu_last_end_us_pct": [float(np.percentile(last, q)) / 100.0 for q in (0, 50, 100)],
+                     "busy_frac": float(busy.sum() / (len(keys) * span))}
+        xcc = (hw >> np.uint64(32)).astype(np.int64)
+        out[name]["per_xcc"] = {int(x): {"blocks": int((xcc == x).sum()), "block_us_median": float(np.median(tick[xcc == x])) / 100.0,
+                                         "ghz_median": float(np.median(ghz[xcc == x])),
+                                         "last_end_us": float(v[xcc == x, 3].max() - start0) / 100.0}
+                                for x in np.unique(xcc)}
     print(json.dumps(out), flush=True)
 
 
