@@ -32,12 +32,15 @@ SPLIT_MFMA_PEAK_TFLOPS = 2500.0 / 6
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")  # tools/pmc_traffic.py output
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak (spec)
 
-# algorithmic multiply-accumulates per point of the blender network with one frame time per step
+# multiply-accumulates per point of the blender network with one frame time per step
 # (train_baseline.py:107-110): the timenet (13*256 + 256*30 = 11,008 MACs) is evaluated
-# once per launch, and its gradients come from the layer-0/5 bias gradients (DGS_MLP_UNIFORM_T)
-MLP_FWD_MAC = 508928            # every trunk + head weight once
+# once per launch, and its gradients come from the layer-0/5 bias gradients (DGS_MLP_UNIFORM_T). The
+# reference network has 508,928 trunk + head weights; with one frame time t_emb is a constant whose
+# 2 x 256 x 30 linear.0 / linear.5 columns fold into the biases (once per launch), so the per-point
+# work the kernels do, and are credited with, is 508,928 - 15,360 = 493,568 MACs forward and for dW
+MLP_FWD_MAC = 493568            # every trunk + head weight once, t_emb columns folded
 MLP_DX_MAC = 461312             # W^T products whose input gradient is needed (heads, L7..L1 hidden rows)
-MLP_DW_MAC = 508928             # every trunk + head weight once
+MLP_DW_MAC = 493568             # every trunk + head weight once, t_emb columns from gb (x) te
 
 
 def parse():

@@ -978,8 +978,9 @@ struct RJob {
     int rowpad0;       // padded output row of source row 0 (head stacking)
     int nseg;
     Seg seg[3];        // source col <-> padded feature
-    int block0[2];     // first slab of the layer's k-tile 0 / 1 (features [0,256) / [256,512))
+    int block0[2];     // first slab of the layer's k-tile 0 / 1 (padded features [0,k1) / [k1,..))
     int nsplit[2];
+    int k1;            // padded feature where k-tile 1 starts (WPlan::layer_k1)
 };
 
 constexpr int MAXR = 28;
@@ -1005,7 +1006,8 @@ __global__ __launch_bounds__(256) void k_dw_reduce(RJobs R, const float *__restr
         int f = -1;
         for (int k = 0; k < J.nseg; k++)
             if (c >= J.seg[k].s0 && c < J.seg[k].s0 + J.seg[k].len) f = J.seg[k].p0 + (c - J.seg[k].s0);
-        int kt = f / WT, kl = f % WT;
+        if (f < 0) return;  // a folded t_emb column: written by k_tgrad
+        const int kt = f >= J.k1 ? 1 : 0, kl = f - (kt ? J.k1 : 0);
         const float *sl = slabs + (size_t)J.block0[kt] * SLAB + n * WT + kl;
         // unrolled: the slab loads are issued together, the adds stay in slab order (deterministic)
 #pragma unroll 8
@@ -1213,6 +1215,7 @@ int launch_dw_reduce(const Flags &F, const WPlan &W, const float *slabs, float *
             J.block0[kt] = jq >= 0 ? W.jobs.j[jq].block0 : 0;
             J.nsplit[kt] = jq >= 0 ? W.jobs.j[jq].nsplit : 0;
         }
+        J.k1 = W.layer_k1[layer];
         R.begin[R.n] = total;
         total += bias ? r : r * c;
         R.n++;

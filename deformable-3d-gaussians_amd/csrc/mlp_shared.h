@@ -20,8 +20,9 @@ constexpr int F_XE = 0, F_TE = 64, F_H = 96;
 constexpr int S_H0 = 0, S_XE = 1024, S_TE = 1088, S_H4 = 1120, S_TIN = 2144, S_TH = 2160;
 __host__ __device__ constexpr int s_h(int i) { return i < 4 ? S_H0 + 256 * i : S_H4 + 256 * (i - 4); }
 // timenet of a frame-uniform t (blender), evaluated once per launch by k_timenet into the tail of
-// the saved buffer: [t0 | TIN (16) | TE (32) | TH (256)]
-constexpr int TC_T = 0, TC_TIN = 16, TC_TE = 32, TC_TH = 64, TC_FLOATS = 512;
+// the saved buffer: [t0 | TIN (16) | TE (32) | TH (256) | C0 (256) | C5 (256)], C0 / C5 = the biases of
+// linear.0 / linear.5 with the t_emb columns folded in (split path, uniform t)
+constexpr int TC_T = 0, TC_TIN = 16, TC_TE = 32, TC_TH = 64, TC_C0 = 320, TC_C5 = 576, TC_FLOATS = 1024;
 // relu' bit-mask rows: H0..H7 then TH (blender)
 __host__ __device__ constexpr int m_h(int i) { return 256 * i; }
 constexpr int M_TH = 2048;
@@ -64,9 +65,19 @@ __host__ __device__ inline int seg_lookup(const Seg *s, int ns, int p) {
     return -1;
 }
 
-// input-feature segments of the concatenated trunk inputs
-inline int layer_in_segs(const Flags &F, int layer, Seg *s) {
+// input-feature segments of the concatenated trunk inputs. With a frame-uniform t (F.uniform_t, the
+// split path only) linear.0 / linear.5 see t_emb as a constant: its columns are folded into the bias
+// (k_timenet: C0 = b0 + W0,te te, C5 likewise), so the forward GEMMs and dW cover x_emb (and h) only,
+// and the t_emb columns' dW is gb (x) te (k_tgrad). fold = false: the full layout (the backward's
+// transposed images, whose x_emb / t_emb rows are never read with a uniform t).
+inline int layer_in_segs(const Flags &F, int layer, Seg *s, bool fold = true) {
     const int te = F.blender ? 30 : F.tin;
+    if (fold && F.uniform_t && (layer == 0 || layer == 5)) {
+        s[0] = seg(F_XE, 63, 0);
+        if (layer == 0) return 1;
+        s[1] = seg(64, 256, 63 + te);  // h right after x_emb
+        return 2;
+    }
     if (layer == 0) {
         s[0] = seg(F_XE, 63, 0);
         s[1] = seg(F_TE, te, 63);
@@ -83,6 +94,10 @@ inline int layer_in_segs(const Flags &F, int layer, Seg *s) {
 }
 
 __host__ __device__ inline int layer_kpad(int layer) { return layer == 0 ? 96 : layer == 5 ? 352 : 256; }
+// padded K of the forward GEMM / dW (t_emb folded with a uniform t)
+__host__ __device__ inline int layer_kpad_f(const Flags &F, int layer) {
+    return F.uniform_t && layer == 0 ? 64 : F.uniform_t && layer == 5 ? 320 : layer_kpad(layer);
+}
 
 // parameter indices in state_dict order (include/dgs.h)
 struct Params {
@@ -159,6 +174,7 @@ struct WJobs {
 struct WPlan {
     WJobs jobs;
     int layer_job[11][2];  // job index of k-tile 0/1 per layer (-1 if none)
+    int layer_k1[11];      // padded feature where k-tile 1 starts (256; 64 for a folded linear.5)
     int nblocks;
 };
 
@@ -168,7 +184,7 @@ struct WPlan {
 // shape_cost (optional, the split k_dws): measured per-chunk cost of the four job shapes instead of
 // the MFMA-tile model, indexed by dw_shape().
 inline int dw_shape(int nrows, int krows) {
-    return krows == 256 ? (nrows == 256 ? 0 : 1) : (krows > 32 ? 2 : 3);
+    return krows == 256 ? (nrows == 256 ? 0 : 1) : (krows > 64 ? 2 : krows > 32 ? 4 : 3);
 }
 inline WPlan make_wplan(const Flags &F, int target, double fixed, double floor_, const double *shape_cost = nullptr) {
     WPlan W{};
@@ -177,7 +193,16 @@ inline WPlan make_wplan(const Flags &F, int target, double fixed, double floor_,
     };
     Raw raw[MAXJ];
     int nr = 0;
+    for (int l = 0; l < 11; l++) W.layer_k1[l] = WT;
     for (int i = 0; i < 8; i++) {
+        if (F.uniform_t && (i == 0 || i == 5)) {  // folded t_emb: x_emb rows (+ h rows for linear.5)
+            raw[nr++] = Raw{Z_L0 + 256 * i, 256, S_XE, 64, i, 0};
+            if (i == 5) {
+                raw[nr++] = Raw{Z_L0 + 256 * i, 256, S_H4, 256, i, 1};
+                W.layer_k1[i] = 64;
+            }
+            continue;
+        }
         int xrow = (i == 0 || i == 5) ? S_XE : s_h(i - 1);
         int kp = layer_kpad(i);
         for (int kt = 0; kt * WT < kp; kt++)

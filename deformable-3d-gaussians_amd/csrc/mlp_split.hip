@@ -260,8 +260,9 @@ struct HGate {
 // groups g0 + 4c + kq). Fully unrolled; per k-step: each column tile's six MFMAs followed by its B
 // fragment for the next k-step into the same registers, then the A fragment RING k-steps ahead
 // (register ring: the A stream comes from L2). sched_barrier keeps that order per k-step; the other
-// three waves of the SIMD cover the B reload latency. pre() runs after the A prologue.
-template <int NK, int NQ_, class Pre = NoPre, class Gate = NoGate>
+// three waves of the SIMD cover the B reload latency. pre() runs after the A prologue. SKIP: k-steps
+// >= SKIP read the LDS image one k-step further on (linear.5 with t_emb folded: x_emb | h, past t_emb).
+template <int NK, int NQ_, class Pre = NoPre, class Gate = NoGate, int SKIP = (1 << 20)>
 __device__ inline void gemm(const bf16x8 *__restrict__ Aw, const bf16x8 *lds, int g0, int q0, int lane,
                             f32x4 (&acc)[NQ_], Pre pre = Pre(), Gate gate = Gate()) {
     static_assert(NK >= 1, "empty GEMM");
@@ -274,6 +275,7 @@ __device__ inline void gemm(const bf16x8 *__restrict__ Aw, const bf16x8 *lds, in
     constexpr int AK = KSLOT;
 #endif
     constexpr int BK = KG * UG;
+    auto bofs = [](int k) { return (k + (k >= SKIP ? 1 : 0)) * BK; };  // compile-time per unrolled k
     constexpr int RING = 2;
     AFrag ring[RING];
 #pragma unroll
@@ -294,10 +296,10 @@ __device__ inline void gemm(const bf16x8 *__restrict__ Aw, const bf16x8 *lds, in
         for (int q = 0; q < NQ_; q++) {
             // the next tile's B fragment (or the next k-step's first) is in flight during this tile's MFMAs
             AFrag nb;
-            if (q + 1 < NQ_) nb = load_b(Bp + k * BK, q + 1);
+            if (q + 1 < NQ_) nb = load_b(Bp + bofs(k), q + 1);
             else if (k + 1 < NK) {
                 gate.need(k + 1, seen);
-                nb = load_b(Bp + (k + 1) * BK, 0);
+                nb = load_b(Bp + bofs(k + 1), 0);
             }
             mma6(ring[k % RING], b, acc[q], lo[q]);
             if (q + 1 < NQ_ || k + 1 < NK) b = nb;
@@ -425,6 +427,7 @@ struct FwdArgs {
     int fT1, fT2, fL[8], fHd;      // image k-slots
     int bT1, bT2, bL[8], bHd;      // fp32 offsets
     int wT1, wT2;                  // fp32 timenet weights [256][16], [32][256]
+    int w0te, w5te;                // fp32 t_emb columns of linear.0 / linear.5 [256][32] (C0 / C5)
     int flags;
     uint32_t *queue;  // block queue (persistent launch, BlockQueue) or nullptr: one launch block per block
     int nblk;         // blocks (64-point + 16-point)
@@ -434,7 +437,7 @@ struct FwdArgs {
 // timenet (time_utils.py:74-76, 13 -> 256 -> 30) has one value per launch: evaluated here once in
 // fp32 (one workgroup); a k_fwd block whose points all carry that t broadcasts TE / TH.
 __global__ __launch_bounds__(256) void k_timenet(FwdArgs a) {
-    __shared__ float tin[16], th[256];
+    __shared__ float tin[16], th[256], te[32];
     const int j = threadIdx.x;
     const float t0 = a.t[0];
     if (j < 16) {
@@ -470,7 +473,22 @@ __global__ __launch_bounds__(256) void k_timenet(FwdArgs a) {
         acc += __shfl_xor(acc, 1);
         acc += __shfl_xor(acc, 2);
         acc += __shfl_xor(acc, 4);
-        if (q == 0) a.tc[TC_TE + k] = acc + a.fp[a.bT2 + k];
+        if (q == 0) {
+            a.tc[TC_TE + k] = acc + a.fp[a.bT2 + k];
+            te[k] = k < 30 ? acc + a.fp[a.bT2 + k] : 0.f;
+        }
+    }
+    __syncthreads();
+    {  // C0 / C5: the biases of linear.0 / linear.5 with the t_emb columns folded in (k_fwd, uniform t)
+        const float *w0 = a.fp + a.w0te + j * 32, *w5 = a.fp + a.w5te + j * 32;
+        float c0 = a.fp[a.bL[0] + j], c5 = a.fp[a.bL[5] + j];
+#pragma unroll
+        for (int k = 0; k < 30; k++) {
+            c0 = fmaf(w0[k], te[k], c0);
+            c5 = fmaf(w5[k], te[k], c5);
+        }
+        a.tc[TC_C0 + j] = c0;
+        a.tc[TC_C5 + j] = c5;
     }
 }
 
@@ -485,7 +503,7 @@ struct BiasPre {
 // One block of NQB 16-point column tiles (NQB = 4: the 64-point blocks; NQB = 1: the 16-point tail
 // blocks that spread the last, sparse round of blocks over the idle CUs). p0: first point; slot: the
 // block's relu'-mask slot.
-template <bool SAVE, int NQB>
+template <bool SAVE, int NQB, bool FOLD>
 __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_t *hwr, uint32_t *hrd, int p0, int slot) {
     constexpr int BMB = 16 * NQB;  // points of this block (the LDS images keep the BM-point stride)
     float *lf = reinterpret_cast<float *>(lds);
@@ -516,13 +534,16 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
     DGS_STAMP(0);
     // frame-uniform t: all points of the block carry k_timenet's t0 (every wave checks the same
     // values, so the branch is block-uniform without a barrier)
-    bool uniform_t = F.uniform_t && a.tc;  // the caller's guarantee (DGS_MLP_UNIFORM_T), else checked
-    if (F.blender && a.tc && !uniform_t) {
+    bool uniform_t = FOLD || (F.uniform_t && a.tc);  // the caller's guarantee (DGS_MLP_UNIFORM_T), else checked
+    if (!FOLD && F.blender && a.tc && !uniform_t) {
         const float t0 = a.tc[TC_T];
         const int p = p0 + lane;
         const float tv = (lane < BMB && p < a.N) ? a.t[p] : t0;
         uniform_t = __ballot(tv != t0) == 0;
     }
+    // t_emb folded into the linear.0 / linear.5 biases (FOLD = DGS_MLP_UNIFORM_T; the host always
+    // provides tc then): no t_emb / TIN staging, the trunk GEMMs read x_emb (| h) only
+    constexpr bool fold = FOLD;
     if (tid < 8) {
         hwr[tid] = 0;
         hrd[tid] = 0;
@@ -544,7 +565,8 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
         }
     }
     if (tid < BMB) stage[63 * BM + tid] = 0.f;  // padding feature
-    if (uniform_t) {  // TE and TIN: k_timenet's values broadcast over the points
+    if (fold) {
+    } else if (uniform_t) {  // TE and TIN: k_timenet's values broadcast over the points
         for (int e = tid; e < 48 * BMB; e += NTHR) {
             const int f = e / BMB, m = e % BMB;
             stage[(ST_TE + f) * BM + m] = f < 32 ? a.tc[TC_TE + f] : a.tc[TC_TIN + f - 32];
@@ -572,19 +594,20 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
     // saved network inputs (fp32, coalesced) and their split LDS images
     const bool te_ready = uniform_t || !F.blender;
     if (SAVE) {
-        const int nrow = te_ready ? 96 : 64;  // XE | TE rows are adjacent in saved (S_TE = S_XE + 64)
+        // XE | TE rows are adjacent in saved (S_TE = S_XE + 64); folded: dW reads x_emb only
+        const int nrow = te_ready && !fold ? 96 : 64;
         for (int e = tid; e < nrow * BMB; e += NTHR) {
             const int f = e / BMB, m = e % BMB;
             a.saved[(size_t)(S_XE + f) * Ns + p0 + m] = stage[f * BM + m];
         }
-        if (F.blender)
+        if (F.blender && !fold)
             for (int e = tid; e < 16 * BMB; e += NTHR) {
                 const int f = e / BMB, m = e % BMB;
                 a.saved[(size_t)(S_TIN + f) * Ns + p0 + m] = stage[(ST_TIN + f) * BM + m];
             }
     }
     {
-        const int ngrp = F.blender ? 14 : 12;  // staging groups: XE 0-7 | TE 8-11 | TIN 12-13
+        const int ngrp = fold ? 8 : F.blender ? 14 : 12;  // staging groups: XE 0-7 | TE 8-11 | TIN 12-13
         for (int u = tid; u < ngrp * BMB; u += NTHR) {
             const int g = u / BMB, m = u % BMB;
             if (g >= G_TE && g < G_H && !te_ready) continue;  // TE comes from the per-point timenet
@@ -593,7 +616,7 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
             for (int j = 0; j < 8; j++) v[j] = stage[(8 * g + j) * BM + m];
             put_unit8(lds, g < 12 ? g : G_TIN + g - 12, m, v);
         }
-        if (F.blender)  // TIN k-step padding (features 16..31): zero, not stale LDS
+        if (F.blender && !fold)  // TIN k-step padding (features 16..31): zero, not stale LDS
             for (int u = tid; u < 2 * UG; u += NTHR) lds[(G_TIN + 2) * UG + u] = bf16x8{};
     }
     lds_barrier();
@@ -637,15 +660,22 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
 #pragma unroll 1
     for (int L = 0; L < 8; L++) {
         const int g0 = (L == 0 || L == 5) ? G_XE : G_H;
-        const int nk = layer_kpad(L) / 32;
+        const int nk = layer_kpad_f(F, L) / 32;
         zero_tiles(c);
         const bf16x8 *Aw = a.img + (size_t)(a.fL[L] + r * nk) * KSLOT;
         float4 bv;  // loaded behind the A prologue: its latency is covered by the GEMM
-        const BiasPre bp{&bv, a.fp + a.bL[L], r, lane};
-        const HGate hg{hwr, hrd, L == 5 ? 3 : 0, 2u * L, true, lane};
-        if (L == 0) gemm<3, NQB>(Aw, lds, g0, 0, lane, c, bp);  // XE | TE only
-        else if (L == 5) gemm<11, NQB>(Aw, lds, g0, 0, lane, c, bp, hg);
-        else gemm<8, NQB>(Aw, lds, g0, 0, lane, c, bp, hg);
+        const float *bias = fold && L == 0 ? a.tc + TC_C0 : fold && L == 5 ? a.tc + TC_C5 : a.fp + a.bL[L];
+        const BiasPre bp{&bv, bias, r, lane};
+        const HGate hg{hwr, hrd, L == 5 ? (fold ? 2 : 3) : 0, 2u * L, true, lane};
+        if (L == 0) {
+            if constexpr (FOLD) gemm<2, NQB>(Aw, lds, g0, 0, lane, c, bp);  // XE only
+            else gemm<3, NQB>(Aw, lds, g0, 0, lane, c, bp);                 // XE | TE
+        } else if (L == 5) {
+            if constexpr (FOLD) gemm<10, NQB, BiasPre, HGate, 2>(Aw, lds, g0, 0, lane, c, bp, hg);  // XE | H
+            else gemm<11, NQB>(Aw, lds, g0, 0, lane, c, bp, hg);                                    // XE | TE | H
+        } else {
+            gemm<8, NQB>(Aw, lds, g0, 0, lane, c, bp, hg);
+        }
         DGS_STAMP(4 + 2 * L);
         DGS_WSTAMP(22, L);  // per wave: GEMM end (layer 3)
 #ifdef DGS_DIAG_EPI_PRIO  // experiment: raised issue priority through the epilogue
@@ -697,7 +727,7 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
 #endif
 }
 
-template <bool SAVE>
+template <bool SAVE, bool FOLD>
 __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
     __shared__ bf16x8 lds[G_FWD * UG];
     __shared__ uint32_t hwr[8], hrd[8];  // trunk hand-off counters (HGate)
@@ -706,8 +736,8 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
     for (int b = blockIdx.x;;) {
         int nx = 0;
         if (a.queue && threadIdx.x == 0) nx = queue_take(a.queue);
-        if (b < a.nfull) fwd_block<SAVE, NQ>(a, lds, hwr, hrd, b * BM, b);
-        else fwd_block<SAVE, 1>(a, lds, hwr, hrd, a.nfull * BM + (b - a.nfull) * 16, b);
+        if (b < a.nfull) fwd_block<SAVE, NQ, FOLD>(a, lds, hwr, hrd, b * BM, b);
+        else fwd_block<SAVE, 1, FOLD>(a, lds, hwr, hrd, a.nfull * BM + (b - a.nfull) * 16, b);
         if (!a.queue) break;
         if (threadIdx.x == 0) s_next = nx;
         __syncthreads();  // also: the next block's staging overwrites LDS this one's heads read
@@ -871,6 +901,7 @@ struct TGradArgs {
     const float *tc;      // k_timenet's TIN / TH
     const float *gb0, *gb5;
     float *gT0w, *gT0b, *gT2w, *gT2b;
+    float *gW0, *gW5;     // linear.0 / linear.5 weight gradients: their folded t_emb columns
     int tin;
 };
 
@@ -891,6 +922,14 @@ __global__ __launch_bounds__(1024) void k_tgrad(TGradArgs a) {
 #pragma unroll
         for (int o = 1; o < 32; o <<= 1) s += __shfl_xor(s, o);
         if (part == 0) S[k] = s;
+    }
+    // the folded t_emb columns 63..92 of linear.0 / linear.5: dW = gb (x) te (the dW kernel covers
+    // x_emb and h only)
+    for (int e = j; e < 256 * 30; e += 1024) {
+        const int n = e / 30, k = e - n * 30;
+        const float te = a.tc[TC_TE + k];
+        a.gW0[n * 93 + 63 + k] = a.gb0[n] * te;
+        a.gW5[n * 349 + 63 + k] = a.gb5[n] * te;
     }
     __syncthreads();
     for (int e = j; e < 30 * 256; e += 1024) a.gT2w[e] = S[e >> 8] * th[e & 255];
@@ -1503,15 +1542,17 @@ __global__ __launch_bounds__(DW_THREADS) void k_dws(WJobs JT, size_t Ns, const f
     for (int q = 1; q < MAXJ; q++)
         if (q < JT.n && (int)blockIdx.x >= JT.j[q].block0) J = JT.j[q];
     // job shapes (host-checked in dw_split_once): krows = 256 with nrows 256 or 32 -> COL; nrows =
-    // 256 with krows 96 or 16 -> ROW
+    // 256 with krows 96, 64 (folded t_emb) or 16 -> ROW
     CLK_BEGIN();
     if (J.krows == 256) {
         if (J.nrows == 256)
             dws_run<true, 8>(J, Ns, dz, saved, slabs, dws_lds);
         else
             dws_run<true, 1>(J, Ns, dz, saved, slabs, dws_lds);
-    } else if (J.krows > 32) {
+    } else if (J.krows > 64) {
         dws_run<false, 3>(J, Ns, dz, saved, slabs, dws_lds);
+    } else if (J.krows > 32) {
+        dws_run<false, 2>(J, Ns, dz, saved, slabs, dws_lds);
     } else {
         dws_run<false, 1>(J, Ns, dz, saved, slabs, dws_lds);
     }
@@ -1597,11 +1638,11 @@ Plan make_plan(int flags) {
         P.w5te = new_f32(P.pLw[5], 256, 32, 1, &full, 1, &te0);
     }
     for (int i = 0; i < 8; i++) {
-        Seg s[3];
-        const int ns = layer_in_segs(F, i, s);
-        const int kp = layer_kpad(i);
-        P.fL[i] = new_img(P.pLw[i], 0, 16, kp / 32, 1, &full, ns, s);
-        P.tL[i] = new_img(P.pLw[i], 1, kp / 16, 8, ns, s, 1, &full);  // rows = padded input features
+        Seg s[3], sf[3];
+        const int ns = layer_in_segs(F, i, s);             // forward: t_emb folded with a uniform t
+        const int nsf = layer_in_segs(F, i, sf, false);    // backward: the full padded input
+        P.fL[i] = new_img(P.pLw[i], 0, 16, layer_kpad_f(F, i) / 32, 1, &full, ns, s);
+        P.tL[i] = new_img(P.pLw[i], 1, layer_kpad(i) / 16, 8, nsf, sf, 1, &full);  // rows = padded input features
         P.bL[i] = new_f32(P.pLb[i], 256, 1, 1, &full, 1, &one);
     }
     // heads: rows stacked in output order (nout <= 13) in one 16-row image each way
@@ -1702,12 +1743,13 @@ static int *pack_map_for(const Plan &P, int flags) {
 }
 
 // dW split plan: one 8-wave workgroup per CU (LDS 144 KiB); per-chunk cost in MFMA tiles + staging
-// k_dws per-chunk cost by job shape (dw_shape: COL 256x256, COL 32-row head, ROW 96-col, ROW 16-col),
+// k_dws per-chunk cost by job shape (dw_shape: COL 256x256, COL 32-row head, ROW 96-col, ROW 16-col,
+// ROW 64-col),
 // relative to the full tile, from the per-workgroup durations of tools/mlp_clock.py at 100k points
 // (profiles/r3p_mlp_clock_before.json: a full-tile chunk 4.5 us, a 96-col chunk 2.6 us, a head chunk
 // 1.5 us; the MFMA-tile model gave the narrow jobs too few workgroups, which then finished 25 % after
 // the rest. With these costs every job's workgroups end within 4 %: profiles/r3p_mlp_clock.json)
-static const double kDwsShapeCost[4] = {1.0, 0.33, 0.58, 0.30};
+static const double kDwsShapeCost[5] = {1.0, 0.33, 0.58, 0.30, 0.45};
 static WPlan split_wplan(const Flags &F) {
     static const bool model = [] {  // A/B only: the MFMA-tile cost model
         const char *e = getenv("DGS_DWS_TILE_MODEL");
@@ -1777,6 +1819,18 @@ static uint32_t *block_queue(hipStream_t stream, int kernel) {
         if (hipMemset(w, 0, 4 * sizeof(uint32_t)) != hipSuccess) return nullptr;
     }
     return w + 2 * kernel;
+}
+// k_timenet's output for a forward without saved activations (inference with a uniform t), one
+// TC_FLOATS buffer per (device, stream)
+static float *timenet_scratch(hipStream_t stream) {
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, float *> bufs;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    float *&b = bufs[{dev, stream}];
+    if (!b && hipMalloc(&b, TC_FLOATS * sizeof(float)) != hipSuccess) b = nullptr;
+    return b;
 }
 static int persistent_grid(int nblk, const uint32_t *queue) { return queue ? std::min(nblk, cu_count()) : nblk; }
 
@@ -1851,6 +1905,7 @@ int forward(int flags, int N, const float *xyz, const float *t, const float *pac
     a.mask = saved ? reinterpret_cast<uint32_t *>(saved + (size_t)P.F.nsaved * a.Ns) : nullptr;
     a.fT1 = P.fT1; a.fT2 = P.fT2; a.fHd = P.fHd;
     a.bT1 = P.bT1; a.bT2 = P.bT2; a.bHd = P.bHd; a.wT1 = P.wT1; a.wT2 = P.wT2;
+    a.w0te = P.w0te; a.w5te = P.w5te;
     for (int i = 0; i < 8; i++) { a.fL[i] = P.fL[i]; a.bL[i] = P.bL[i]; }
     a.flags = flags;
     const Blocks bs = block_split(N);
@@ -1861,14 +1916,24 @@ int forward(int flags, int N, const float *xyz, const float *t, const float *pac
     const int grid = persistent_grid(nblk, a.queue);
     {
         ScopedTimer tm("mlp_fwd", stream);
-        if (saved && P.F.blender) {
-            a.tc = saved + (size_t)P.F.nsaved * a.Ns + mask_words(P.F, a.Ns);
+        if (P.F.blender && (saved || P.F.uniform_t)) {
+            // the folded biases (uniform t) are needed without saved activations too (inference)
+            a.tc = saved ? saved + (size_t)P.F.nsaved * a.Ns + mask_words(P.F, a.Ns) : timenet_scratch(stream);
+            if (!a.tc) {
+                set_error("dgs_deform_forward: could not allocate the timenet scratch");
+                return DGS_ERR_HIP;
+            }
             hipLaunchKernelGGL(k_timenet, dim3(1), dim3(256), 0, stream, a);
         }
-        if (saved)
-            hipLaunchKernelGGL(k_fwd<true>, dim3(grid), dim3(NTHR), 0, stream, a);
+        const bool fold = P.F.uniform_t;  // t_emb folded into the biases (a.tc is set above)
+        if (saved && fold)
+            hipLaunchKernelGGL((k_fwd<true, true>), dim3(grid), dim3(NTHR), 0, stream, a);
+        else if (saved)
+            hipLaunchKernelGGL((k_fwd<true, false>), dim3(grid), dim3(NTHR), 0, stream, a);
+        else if (fold)
+            hipLaunchKernelGGL((k_fwd<false, true>), dim3(grid), dim3(NTHR), 0, stream, a);
         else
-            hipLaunchKernelGGL(k_fwd<false>, dim3(grid), dim3(NTHR), 0, stream, a);
+            hipLaunchKernelGGL((k_fwd<false, false>), dim3(grid), dim3(NTHR), 0, stream, a);
     }
     DGS_LAUNCH_CHECK("k_fwd", false, stream);
     return DGS_OK;
@@ -1903,6 +1968,10 @@ int backward(int flags, int N, const float *packed, const float *saved, const fl
     }
     DGS_LAUNCH_CHECK("k_bwd", false, stream);
     int rc;
+    if (F.uniform_t && (dw_mode() == 1 || dw_mode() == 2)) {  // A/B variants predate the folded t_emb jobs
+        set_error("dgs_deform_backward: DGS_MLP_SPLIT_DW=1/2 do not support a uniform t (folded t_emb)");
+        return DGS_ERR_ARGS;
+    }
     if (dw_mode() == 0)
         rc = mlp::dw_fp32(F, Ns, dz, saved, slabs, grads, stream);
     else if (dw_mode() == 1)
@@ -1918,6 +1987,7 @@ int backward(int flags, int N, const float *packed, const float *saved, const fl
     g.tc = saved + (size_t)F.nsaved * Ns + mask_words(F, Ns);
     g.gb0 = grads[P.pLb[0]]; g.gb5 = grads[P.pLb[5]];
     g.gT0w = grads[P.pT0w]; g.gT0b = grads[P.pT0b]; g.gT2w = grads[P.pT2w]; g.gT2b = grads[P.pT2b];
+    g.gW0 = grads[P.pLw[0]]; g.gW5 = grads[P.pLw[5]];
     g.tin = F.tin;
     hipLaunchKernelGGL(k_tgrad, dim3(1), dim3(1024), 0, stream, g);
     DGS_LAUNCH_CHECK("k_tgrad", false, stream);
@@ -1945,7 +2015,7 @@ static int dw_split_once(const Flags &F, size_t Ns, const float *dz, const float
     for (int q = 0; q < W.jobs.n; q++) {  // the shapes k_dws instantiates
         const WJob &j = W.jobs.j[q];
         const bool ok = (j.krows == 256 && (j.nrows == 256 || j.nrows == 32)) ||
-                        (j.nrows == 256 && (j.krows == 96 || j.krows == 16));
+                        (j.nrows == 256 && (j.krows == 96 || j.krows == 64 || j.krows == 16));
         if (!ok) {
             set_error("dgs_deform_backward: dW job shape outside k_dws's instantiations");
             return DGS_ERR_ARGS;

@@ -33,7 +33,7 @@ def test_host_only_queries():
     assert lib.dgs_deform_num_params(3) == 28
     assert lib.dgs_deform_outputs(1) == 10 and lib.dgs_deform_outputs(3) == 13
     # activations, relu bits (2 blocks + room for 3 more 16-point tail slots each), timenet
-    assert lib.dgs_deform_saved_floats(1, 100) == 2416 * 128 + 2304 * 2 * (2 + 3 * 2) + 512
+    assert lib.dgs_deform_saved_floats(1, 100) == 2416 * 128 + 2304 * 2 * (2 + 3 * 2) + 1024  # TC_FLOATS: t0 | TIN | TE | TH | C0 | C5
     assert lib.dgs_deform_packed_floats(1) > 522280
 
 

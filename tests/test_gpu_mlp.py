@@ -133,7 +133,8 @@ def test_expanded_time_input():
     fid = torch.tensor([0.42], device="cuda")
     a = net(x, fid.unsqueeze(0).expand(500, -1))[0]
     b = net(x, torch.full((500, 1), 0.42, device="cuda"))[0]
-    assert torch.equal(a, b)
+    # the stride-0 column runs DGS_MLP_UNIFORM_T (t_emb folded into the biases): fp32 rounding apart
+    assert torch.allclose(a, b, rtol=1e-5, atol=1e-6 * float(b.abs().max()))
 
 
 @pytest.mark.parametrize("name,N", [("blender", 20000), ("nonblender", 20000), ("6dof", 20000), ("fork", 20000),
@@ -188,8 +189,11 @@ def _raw_grads(G, d6, fork):
 def test_uniform_t_flag(name, N):
     """A stride-0 time column (train_baseline.py:107-110) sets DGS_MLP_UNIFORM_T: the backward skips
     the per-point t_emb GEMMs and k_tgrad forms the timenet gradients from the layer-0/5 bias
-    gradients. Outputs must equal the per-point path's bit for bit; gradients match the oracle
-    (1e-4 of each tensor's max) and the per-point path."""
+    gradients. On a blender network the uniform path also folds t_emb into the linear.0 / linear.5
+    biases (k_timenet's C0 / C5; the forward GEMMs and dW then cover x_emb | h only and k_tgrad writes
+    the t_emb weight columns), so its outputs equal the per-point path's to fp32 rounding (1e-5
+    relative + 1e-6 of the largest output), bit for bit otherwise; gradients match the oracle (1e-4
+    of each tensor's max) and the per-point path."""
     bl, d6, fork = VARIANTS[name]
     rng = np.random.default_rng(N + 1)
     x = rng.uniform(-1.3, 1.3, (N, 3)).astype(np.float32)
@@ -207,7 +211,11 @@ def test_uniform_t_flag(name, N):
         masks = mlp_relu_masks(raw, N, bl, False, th_saved=mode == "full")
         (raw * torch.from_numpy(G).float().cuda()).sum().backward()
         res[mode] = (raw.detach().clone(), {k: p.grad.clone() for k, p in net.named_parameters()}, masks)
-    assert torch.equal(res["expanded"][0], res["full"][0])
+    if bl:  # folded t_emb: a different fp32 summation order for linear.0 / linear.5
+        a, b = res["expanded"][0], res["full"][0]
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-6 * float(b.abs().max())), float((a - b).abs().max())
+    else:
+        assert torch.equal(res["expanded"][0], res["full"][0])
     out, c = mlp_ref.forward(w, x, np.full((N, 1), t0, np.float32), bl, d6)
     ref = mlp_ref.backward(w, c, out, _raw_grads(G, d6, fork), bl, d6, fork, relu_masks=res["expanded"][2])
     for k, g in res["expanded"][1].items():

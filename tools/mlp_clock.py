@@ -82,6 +82,9 @@ def main():
                      "cu_first_start_us_pct": [float(np.percentile(first, q)) / 100.0 for q in (0, 50, 100)],
                      "cu_last_end_us_pct": [float(np.percentile(last, q)) / 100.0 for q in (0, 50, 100)],
                      "busy_frac": float(busy.sum() / (len(keys) * span))}
+        if k == 2:  # per workgroup, in launch order (jobs own contiguous block ranges)
+            order = np.argsort(np.nonzero(ok)[0])
+            out[name]["block_us"] = [round(float(u) / 100.0, 1) for u in tick[order]]
         xcc = (hw >> np.uint64(32)).astype(np.int64)
         out[name]["per_xcc"] = {int(x): {"blocks": int((xcc == x).sum()), "block_us_median": float(np.median(tick[xcc == x])) / 100.0,
                                          "ghz_median": float(np.median(ghz[xcc == x])),
