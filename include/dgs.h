@@ -162,9 +162,11 @@ enum {
     DGS_MLP_NO_ROTSCALE = 4, /* DeformNetwork fork variant: rotation/scaling heads unused */
     DGS_MLP_EXACT_FP32 = 8, /* fp32-input MFMA path instead of the split-bf16 path */
     DGS_MLP_UNIFORM_T = 16  /* caller guarantees t[i] == t[0] for every point (one frame time, as
-                               train_baseline.py:107-110 feeds it): the timenet gradients are formed
-                               from the layer-0/5 bias gradients instead of per-point sums (split path,
-                               blender only; ignored otherwise) */
+                               train_baseline.py:107-110 feeds it): the timenet runs once per launch,
+                               t_emb is folded into the linear.0 / linear.5 biases (outputs equal the
+                               per-point path to fp32 rounding), and the timenet / t_emb-column
+                               gradients are formed from the layer-0/5 bias gradients instead of
+                               per-point sums (split path, blender only; ignored otherwise) */
 };
 
 /* Parameter table: device pointers in state_dict order of DeformNetworkBaseline
