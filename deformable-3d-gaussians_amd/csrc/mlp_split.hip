@@ -1749,7 +1749,9 @@ static int *pack_map_for(const Plan &P, int flags) {
 // (profiles/r3p_mlp_clock_before.json: a full-tile chunk 4.5 us, a 96-col chunk 2.6 us, a head chunk
 // 1.5 us; the MFMA-tile model gave the narrow jobs too few workgroups, which then finished 25 % after
 // the rest. With these costs every job's workgroups end within 4 %: profiles/r3p_mlp_clock.json)
-static const double kDwsShapeCost[5] = {1.0, 0.33, 0.58, 0.30, 0.45};
+// (the folded t_emb's 64-column ROW shape: 1.89 us per chunk vs 4.64 for a full tile, the head 1.59:
+// profiles/r3s_mlp_clock_fold.json)
+static const double kDwsShapeCost[5] = {1.0, 0.34, 0.58, 0.30, 0.41};
 static WPlan split_wplan(const Flags &F) {
     static const bool model = [] {  // A/B only: the MFMA-tile cost model
         const char *e = getenv("DGS_DWS_TILE_MODEL");
