@@ -1385,7 +1385,14 @@ __device__ __forceinline__ f32x16 mma6_into(const AFrag &a, const AFrag &b, f32x
 }
 
 // acc += t (v_pk_add_f32 or v_add_f32: measured alike here)
+#ifdef DGS_ADD16_SCALAR
+__device__ __forceinline__ void add16(f32x16 &acc, const f32x16 &t) {
+#pragma unroll
+    for (int r = 0; r < 16; r++) acc[r] = acc[r] + t[r];
+}
+#else
 __device__ __forceinline__ void add16(f32x16 &acc, const f32x16 &t) { acc += t; }
+#endif
 
 template <bool COL, int NS>
 __device__ __forceinline__ void dws_run(const WJob &J, size_t Ns, const float *__restrict__ dz,

@@ -7,7 +7,8 @@ from collections import defaultdict
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 # step boundaries: each step launches exactly one MLP forward (split-bf16 k_fwd or exact k_mlp_fwd)
-starts = [int(r["Start_Timestamp"]) for r in rows if "k_mlp_fwd<true>" in r["Kernel_Name"] or "mlps::k_fwd<true>" in r["Kernel_Name"]]
+starts = [int(r["Start_Timestamp"]) for r in rows
+          if "k_mlp_fwd<true>" in r["Kernel_Name"] or "mlps::k_fwd<true" in r["Kernel_Name"]]  # <SAVE[, FOLD]>
 if len(starts) < 3:
     sys.exit("not enough steps")
 lo, hi = starts[-6], starts[-1]   # last 5 complete steps
