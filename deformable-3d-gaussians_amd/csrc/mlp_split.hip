@@ -1358,7 +1358,12 @@ __global__ __launch_bounds__(DW_THREADS) void k_dwg(WJobs JT, size_t Ns, const f
 // Same job plan, slab layout and k_dw_reduce as the fp32 k_dw.
 // ------------------------------------------------------------------------------------------------
 constexpr int S_UNITS = NSPLIT * 2 * 8 * 64;  // 16-B units per chunk buffer
-constexpr int S_LDS = 2 * S_UNITS * 16;       // bytes (96 KiB)
+#ifdef DGS_DWS_GATE
+constexpr int S_NBUF = 3;  // chunk buffers: barrier-free hand-off (a wave may run a chunk ahead)
+#else
+constexpr int S_NBUF = 2;
+#endif
+constexpr int S_LDS = S_NBUF * S_UNITS * 16;  // bytes (96 / 144 KiB)
 static_assert(S_LDS <= 160 * 1024, "dWs LDS");
 
 // unit of (split p, k-step ks, row block rb, point half hh, row i): each 32-unit half is rotated
@@ -1468,6 +1473,16 @@ __device__ __forceinline__ void dws_run(const WJob &J, size_t Ns, const float *_
     for (int s = 0; s < NS; s++)
 #pragma unroll
         for (int r = 0; r < 16; r++) acc[s][r] = 0.f;
+#ifdef DGS_DWS_GATE
+    // hand-off counters (monotonic per buffer b): cwr[b] = wave-splits written into b, crd[b] =
+    // wave-reads of b finished; chunk jj (from c0) lives in buffer jj % 3
+    __shared__ uint32_t cwr[S_NBUF], crd[S_NBUF];
+    if (tid < S_NBUF) {
+        cwr[tid] = 0;
+        crd[tid] = 0;
+    }
+    __syncthreads();
+#endif
     if (c0 < c1) {
         sload(c0);
         pload(c0);
@@ -1475,11 +1490,64 @@ __device__ __forceinline__ void dws_run(const WJob &J, size_t Ns, const float *_
         for (int f = 0; f < NSF; f++) sput(f, 0, true);
         sload(min(c0 + 1, c1 - 1));
     }
+#ifdef DGS_DWS_GATE
+    lds_signal(cwr, lane);
+#else
     lds_barrier();
+#endif
     // shared float4 f of the next chunk is split after tile put_at(f) of this one (within the first
     // half of the tiles), then the loads of the chunk after are issued
     constexpr int NH = (NS + 1) / 2;
     auto put_at = [](int f) { return (f * NH) / NSF; };
+#ifdef DGS_DWS_GATE
+    // No workgroup barrier per chunk: a wave reads chunk jj's buffer once all 8 waves have written
+    // their part of it (cwr), and overwrites the buffer of chunk jj - 2 with chunk jj + 1 once all 8
+    // have finished reading it (crd). The two waves of a SIMD drift apart instead of meeting at a
+    // barrier, so one wave's private split (VALU, before its first MFMA) runs beside the other's
+    // MFMAs. LDS operations of a wave complete in issue order: a signal after the writes / reads.
+    auto chunk = [&](int c, auto BUFC) {
+        constexpr int buf = decltype(BUFC)::value;
+        constexpr int nbuf = (buf + 1) % S_NBUF;
+        const int jj = c - c0;
+        const bf16x8 *L = lds + buf * S_UNITS;
+        const bool more = c + 1 < c1;
+        bool freed = false;
+        auto put = [&](int f) {
+            if (!freed) lds_wait_ge(crd + nbuf, 8u * (uint32_t)((jj + 1) / S_NBUF), lds_peek(crd + nbuf));
+            freed = true;
+            sput(f, nbuf, more);
+        };
+        lds_wait_ge(cwr + buf, 8u * (uint32_t)(jj / S_NBUF + 1), lds_peek(cwr + buf));
+        if (pact) {
+            AFrag pf0 = split8(pr[0], pr[1]), pf1 = split8(pr[2], pr[3]);
+            if (!COL) bsum[0] += sum8(pr[0], pr[1]) + sum8(pr[2], pr[3]);
+            pload(min(c + 1, c1 - 1));
+#pragma unroll
+            for (int s = 0; s < NS; s++) {
+                const AFrag s0 = s_frag(L, 0, s, lane);
+                f32x16 T = COL ? mma6_into(s0, pf0, (f32x16)(0.f)) : mma6_into(pf0, s0, (f32x16)(0.f));
+                const AFrag s1 = s_frag(L, 1, s, lane);
+                add16(acc[s], COL ? mma6_into(s1, pf1, T) : mma6_into(pf1, s1, T));
+#pragma unroll
+                for (int f = 0; f < NSF; f++)
+                    if (put_at(f) == s) put(f);
+                if (s == put_at(NSF - 1)) sload(min(c + 2, c1 - 1));
+            }
+        } else {
+            pload(min(c + 1, c1 - 1));
+#pragma unroll
+            for (int f = 0; f < NSF; f++) put(f);
+            sload(min(c + 2, c1 - 1));
+        }
+        lds_signal(crd + buf, lane);
+        lds_signal(cwr + nbuf, lane);
+    };
+    for (int c = c0; c < c1; c += 3) {
+        chunk(c, std::integral_constant<int, 0>{});
+        if (c + 1 < c1) chunk(c + 1, std::integral_constant<int, 1>{});
+        if (c + 2 < c1) chunk(c + 2, std::integral_constant<int, 2>{});
+    }
+#else
     auto chunk = [&](int c, auto BUFC) {
         constexpr int buf = decltype(BUFC)::value;
         const bf16x8 *L = lds + buf * S_UNITS;
@@ -1514,6 +1582,7 @@ __device__ __forceinline__ void dws_run(const WJob &J, size_t Ns, const float *_
         chunk(c, std::integral_constant<int, 0>{});
         if (c + 1 < c1) chunk(c + 1, std::integral_constant<int, 1>{});
     }
+#endif
     float *slab = slabs + (size_t)blockIdx.x * SLAB;
     if (COL) {
         // bias row sums: the 8 lanes staging a row hold its partial sums (fixed xor-tree order)

@@ -501,6 +501,19 @@ __device__ __forceinline__ bool tile_reach(float2 g, float4 co, float x0, float 
     return q <= thr;
 }
 
+// The staged conic in exponent form: power * log2(e) = dx (q.x dx + q.y dy) + q.z dy^2 with
+// q = (-0.5 a, -b, -0.5 c) log2(e) and q.w = opacity, so G = 2^p is one v_exp_f32 (no scaling
+// multiply per pixel and Gaussian; 4 ops for the quadratic form). Every blend kernel evaluates
+// alpha through q_power / q_alpha with the same fused operations, so the forward's and the
+// backward's alphas agree bitwise (the backward's transmittance replay depends on it).
+constexpr float BL_L2E = 1.4426950408889634f;
+__device__ __forceinline__ float4 conic_q(float4 co) {
+    return make_float4(-0.5f * BL_L2E * co.x, -BL_L2E * co.y, -0.5f * BL_L2E * co.z, co.w);
+}
+__device__ __forceinline__ float q_power(float4 q, float dx, float dy) {
+    return fmaf(dx, fmaf(q.x, dx, q.y * dy), q.z * (dy * dy));
+}
+
 // Block-wide stable compaction slot of a kept item (tid order): (slot, kept count); two barriers
 __device__ __forceinline__ int2 compact_slot(bool keep, int tid, uint32_t *s_wcnt) {
     const unsigned long long m = __ballot(keep);
@@ -574,7 +587,7 @@ __global__ __launch_bounds__(256) void k_blend_fwd(const uint2 *__restrict__ ran
         const int2 sl = compact_slot(keep, tid, s_wcnt);
         if (keep) {
             s_xy[sl.x] = gl;
-            s_co[sl.x] = cl;
+            s_co[sl.x] = conic_q(cl);
             s_cd[sl.x] = rgbd[id];
             s_pos[sl.x] = prog;
         }
@@ -586,12 +599,12 @@ __global__ __launch_bounds__(256) void k_blend_fwd(const uint2 *__restrict__ ran
         for (int j = 0; j < n; j++) {
             if (__ballot(!done) == 0ull) break;
             const float2 g = s_xy[j];
-            const float4 co = s_co[j];
+            const float4 q = s_co[j];
             const float4 cd = s_cd[j];
             const uint32_t pos1 = (uint32_t)s_pos[j] + 1u;  // list position + 1 (n_contrib of the full list)
             const float dx = g.x - pfx, dy = g.y - pfy;
-            const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-            const float alpha = fminf(0.99f, co.w * __expf(power));
+            const float power = q_power(q, dx, dy);
+            const float alpha = fminf(0.99f, q.w * __builtin_amdgcn_exp2f(power));
             const float testT = T * (1.f - alpha);
             bool use = !done && !(power > 0.f) && !(alpha < 1.f / 255.f);
             const bool stop = use && testT < 0.0001f;
@@ -656,6 +669,7 @@ __global__ __launch_bounds__(256) void k_blend_bwd(const uint2 *__restrict__ ran
                                                    float *__restrict__ acc) {
     __shared__ float2 s_xy[TILE_PIX];
     __shared__ float4 s_co[TILE_PIX];
+    __shared__ float4 s_q[TILE_PIX];
     __shared__ float4 s_cd[TILE_PIX];
     __shared__ uint32_t s_id[TILE_PIX];
     __shared__ int s_pos[TILE_PIX];
@@ -717,6 +731,7 @@ __global__ __launch_bounds__(256) void k_blend_bwd(const uint2 *__restrict__ ran
             s_id[sl.x] = id;
             s_xy[sl.x] = gl;
             s_co[sl.x] = cl;
+            s_q[sl.x] = conic_q(cl);
             s_cd[sl.x] = rgbd[id];
             s_pos[sl.x] = prog;
         }
@@ -727,8 +742,8 @@ __global__ __launch_bounds__(256) void k_blend_bwd(const uint2 *__restrict__ ran
             float2 g = s_xy[j];
             float4 co = s_co[j];
             float dx = g.x - pfx, dy = g.y - pfy;
-            float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-            float G = __expf(power);
+            float power = q_power(s_q[j], dx, dy);
+            float G = __builtin_amdgcn_exp2f(power);
             float alpha = fminf(0.99f, co.w * G);
             bool act = inside && (uint32_t)contributor < last && power <= 0.f && alpha >= 1.f / 255.f;
             if (__ballot(act) == 0ull) continue;  // wave-uniform
@@ -837,6 +852,7 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
                                                    float *__restrict__ acc) {
     __shared__ float2 s_xy[B2];
     __shared__ float4 s_co[B2];
+    __shared__ float4 s_q[B2];
     __shared__ float4 s_cd[B2];
     __shared__ uint32_t s_id[B2];
     __shared__ int s_pos[B2];
@@ -878,12 +894,17 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
     __syncthreads();
     const int todo_total = (int)s_maxlast;  // Gaussians past every pixel's last contributor are skipped
     const float b0 = bg[0], b1 = bg[1], b2 = bg[2];
-    const f2 bgdot = b0 * dp0 + b1 * dp1 + b2 * dp2;
+    const f2 kbg = -Tfinal * (b0 * dp0 + b1 * dp1 + b2 * dp2);  // dL/dalpha's background term / (1 - alpha)
     const float hx = 0.5f * W, hy = 0.5f * H;
+    // the reduce-scatter leaves field 4k + {0, 2, 1, 3}[row] of register k in the row's lane 15: the
+    // per-pixel terms are summed unscaled and each field's constant factor is applied once here
+    const int frow = lane >> 4;
+    const float sc0 = frow == 0 ? -hx : frow == 2 ? -hy : -0.5f;        // mean2D x, conic x, mean2D y, conic y
+    const float sc1 = frow == 0 ? -0.5f : 1.f;                           // conic z, r, opacity, g
+    const float sc2 = frow == 1 ? hx : frow == 3 ? hy : 1.f;             // b, |mean2D x|, depth, |mean2D y|
     f2 T = Tfinal;
     const f2 zero = f2{0.f, 0.f};
     f2 acc0 = zero, acc1 = zero, acc2 = zero, accd = zero;
-    f2 lc0 = zero, lc1 = zero, lc2 = zero, lcd = zero, last_alpha = zero;
     const int rounds = div_up(todo_total, B2);
     const int end = (int)range.x + todo_total;
     for (int r = 0; r < rounds; r++) {
@@ -904,6 +925,7 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
             s_id[sl.x] = id;
             s_xy[sl.x] = gl;
             s_co[sl.x] = cl;
+            s_q[sl.x] = conic_q(cl);
             s_cd[sl.x] = rgbd[id];
             s_pos[sl.x] = prog;
         }
@@ -912,57 +934,54 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
         for (int j = 0; j < n; j++) {
             const uint32_t contributor = (uint32_t)(todo_total - 1 - s_pos[j]);  // position in the full list
             const float2 g = s_xy[j];
-            const float4 co = s_co[j];
+            const float4 q = s_q[j];
             const f2 dx = g.x - pfx;
             const float dy = g.y - pfy;
-            const f2 power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-            const f2 G = f2{__expf(power.x), __expf(power.y)};
-            const f2 alpha = f2{fminf(0.99f, co.w * G.x), fminf(0.99f, co.w * G.y)};
+            const f2 power = f2{q_power(q, dx.x, dy), q_power(q, dx.y, dy)};
+            const f2 G = f2{__builtin_amdgcn_exp2f(power.x), __builtin_amdgcn_exp2f(power.y)};
+            const f2 alpha = f2{fminf(0.99f, q.w * G.x), fminf(0.99f, q.w * G.y)};
             const bool act0 = in0 && contributor < last0 && power.x <= 0.f && alpha.x >= 1.f / 255.f;
             const bool act1 = in1 && contributor < last1 && power.y <= 0.f && alpha.y >= 1.f / 255.f;
             if (__ballot(act0 || act1) == 0ull) continue;  // wave-uniform
             const float4 cd = s_cd[j];
-            // 1 / (1 - alpha): hardware reciprocal + one Newton step (<= 1 ulp)
-            const f2 om = 1.f - alpha;
+            const float4 co = s_co[j];
+            // an inactive pixel of the pair runs with alpha = 0 and G = 0: T (1 / (1 - 0) = 1), its
+            // pending colour and every gradient term stay unchanged / zero without per-state selects
+            const f2 ae = sel2(act0, act1, alpha, zero);
+            const f2 Ge = sel2(act0, act1, G, zero);
+            // 1 / (1 - alpha): hardware reciprocal + one Newton step (<= 1 ulp; exactly 1 at alpha = 0)
+            const f2 om = 1.f - ae;
             f2 inv = f2{__builtin_amdgcn_rcpf(om.x), __builtin_amdgcn_rcpf(om.y)};
             inv = inv * (1.f - om * inv) + inv;
-            const f2 Tn = T * inv;
-            // the pending contribution of the previous active Gaussian of each pixel; an inactive
-            // pixel of the pair takes none (la = 0) and keeps its state below
-            const f2 la = sel2(act0, act1, last_alpha, zero);
-            acc0 = la * lc0 + (1.f - la) * acc0;
-            acc1 = la * lc1 + (1.f - la) * acc1;
-            acc2 = la * lc2 + (1.f - la) * acc2;
-            accd = la * lcd + (1.f - la) * accd;
-            const f2 w = sel2(act0, act1, alpha * Tn, zero);
-            f2 dLda = (cd.x - acc0) * dp0 + (cd.y - acc1) * dp1 + (cd.z - acc2) * dp2 + (cd.w - accd) * ddep;
-            dLda = dLda * Tn + (-Tfinal * inv) * bgdot;
-            dLda = sel2(act0, act1, dLda, zero);
-            lc0 = sel2(act0, act1, f2{cd.x, cd.x}, lc0);
-            lc1 = sel2(act0, act1, f2{cd.y, cd.y}, lc1);
-            lc2 = sel2(act0, act1, f2{cd.z, cd.z}, lc2);
-            lcd = sel2(act0, act1, f2{cd.w, cd.w}, lcd);
-            last_alpha = sel2(act0, act1, alpha, last_alpha);
-            T = sel2(act0, act1, Tn, T);
-            const f2 dLdG = co.w * dLda;
-            const f2 gdx = G * dx, gdy = G * dy;
-            const f2 dGdx = -gdx * co.x - gdy * co.y;
-            const f2 dGdy = -gdy * co.z - gdx * co.y;
-            const f2 vmx = dLdG * dGdx * hx, vmy = dLdG * dGdy * hy;
-            const f2 vcx = -0.5f * gdx * dx * dLdG, vcy = -0.5f * gdx * dy * dLdG, vcz = -0.5f * gdy * dy * dLdG;
-            const f2 vop = G * dLda;
+            T = T * inv;
+            const f2 w = ae * T;
+            // colour behind this Gaussian (acc) is updated eagerly after its use: the reference's
+            // deferred last_alpha * last_color + (1 - last_alpha) * acc at the next active Gaussian
+            const f2 d0 = cd.x - acc0, d1 = cd.y - acc1, d2 = cd.z - acc2, d3 = cd.w - accd;
+            f2 dLda = d0 * dp0 + d1 * dp1 + d2 * dp2 + d3 * ddep;
+            acc0 = ae * d0 + acc0;
+            acc1 = ae * d1 + acc1;
+            acc2 = ae * d2 + acc2;
+            accd = ae * d3 + accd;
+            dLda = dLda * T + kbg * inv;
+            // dG/dmean2D = -G (conic . d), dG/dconic = -G d d^T / 2: with u = dL/dG G the per-pixel
+            // terms are co (u d) and u d d^T, their factors (-hx, -hy, -0.5) applied after the sums
+            const f2 vop = Ge * dLda;
+            const f2 u = co.w * vop;
+            const f2 udx = u * dx, udy = u * dy;
+            const f2 mxp = co.x * udx + co.y * udy, myp = co.y * udx + co.z * udy;
+            const f2 cxp = udx * dx, cyp = udx * dy, czp = udy * dy;
             const f2 vr = w * dp0, vg = w * dp1, vb = w * dp2, vd = w * ddep;
-            // the pair's sums, then the reduce-scatter over the wave (as k_blend_bwd)
-            const float w0 = row_sum15(fold16(fold32(vmx.x + vmx.y, vmy.x + vmy.y), fold32(vcx.x + vcx.y, vcy.x + vcy.y)));
-            const float w1 = row_sum15(fold16(fold32(vcz.x + vcz.y, vop.x + vop.y), fold32(vr.x + vr.y, vg.x + vg.y)));
+            const float w0 = row_sum15(fold16(fold32(mxp.x + mxp.y, myp.x + myp.y), fold32(cxp.x + cxp.y, cyp.x + cyp.y)));
+            const float w1 = row_sum15(fold16(fold32(czp.x + czp.y, vop.x + vop.y), fold32(vr.x + vr.y, vg.x + vg.y)));
             const float w2 = row_sum15(fold16(fold32(vb.x + vb.y, vd.x + vd.y),
-                                              fold32(fabsf(vmx.x) + fabsf(vmx.y), fabsf(vmy.x) + fabsf(vmy.y))));
+                                              fold32(fabsf(mxp.x) + fabsf(mxp.y), fabsf(myp.x) + fabsf(myp.y))));
             if ((lane & 15) == 15) {
                 const int row = lane >> 4;
                 float *dst = acc + (size_t)s_id[j] * ACC_STRIDE + ((row & 1) << 1) + (row >> 1);
-                atomicAdd(dst, w0);
-                atomicAdd(dst + 4, w1);
-                atomicAdd(dst + 8, w2);
+                atomicAdd(dst, w0 * sc0);
+                atomicAdd(dst + 4, w1 * sc1);
+                atomicAdd(dst + 8, w2 * sc2);
             }
         }
     }
