@@ -549,22 +549,23 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
         hrd[tid] = 0;
     }
     // ---- positional encodings (utils/time_utils.py:42-54) into fp32 staging: feature 3 band + d,
-    // band 0 = x, band 1 + 2i = sin(2^i x), band 2 + 2i = cos(2^i x) ----
-    for (int e = tid; e < BMB * 3 * 11; e += NTHR) {
-        const int m = e % BMB, rr = e / BMB, d = rr % 3, i = rr / 3;  // i = 10: identity band
-        const int p = p0 + m;
-        const bool ok = p < pend;
-        const float x = ok ? a.xyz[3 * p + d] : 0.f;
-        if (i == 10) {
-            stage[d * BM + m] = x;
-        } else {
-            float sv, cv;
-            sincosf(x * (float)(1 << i), &sv, &cv);
-            stage[(3 * (1 + 2 * i) + d) * BM + m] = ok ? sv : 0.f;
-            stage[(3 * (2 + 2 * i) + d) * BM + m] = ok ? cv : 0.f;
-        }
+    // band 0 = x, band 1 + 2i = sin(2^i x), band 2 + 2i = cos(2^i x). The block's xyz rows are read
+    // once (one coalesced load per thread, a single HBM round trip) into the identity band, then the
+    // 10 sin/cos bands are evaluated from LDS in two rounds of the workgroup ----
+    if (tid < 3 * BMB) {
+        const int m = tid / 3, d = tid - 3 * m;
+        stage[d * BM + m] = p0 + m < pend ? a.xyz[3 * (size_t)p0 + tid] : 0.f;
     }
     if (tid < BMB) stage[63 * BM + tid] = 0.f;  // padding feature
+    __syncthreads();
+    for (int e = tid; e < BMB * 3 * 10; e += NTHR) {
+        const int m = e % BMB, rr = e / BMB, d = rr % 3, i = rr / 3;
+        const bool ok = p0 + m < pend;
+        float sv, cv;
+        sincosf(stage[d * BM + m] * (float)(1 << i), &sv, &cv);
+        stage[(3 * (1 + 2 * i) + d) * BM + m] = ok ? sv : 0.f;
+        stage[(3 * (2 + 2 * i) + d) * BM + m] = ok ? cv : 0.f;
+    }
     if (fold) {
     } else if (uniform_t) {  // TE and TIN: k_timenet's values broadcast over the points
         for (int e = tid; e < 48 * BMB; e += NTHR) {
@@ -894,7 +895,10 @@ __global__ __launch_bounds__(NTHR) void k_bwd(BwdArgs a) {
 // dL/dt_emb summed over points is S = W0[:, TE]^T gb0 + W5[:, TE]^T gb5 (gb = the layer-0 / 5 bias
 // gradients = sums of dZ over points), and then
 //   timenet.2: dW = S TH^T, db = S;   dZ_T1 = relu'(TH) (W_T2^T S);   timenet.0: dW = dZ_T1 TIN^T, db = dZ_T1
-// — the per-point sums of the general path (time_utils.py:74-76 autograd) regrouped; one workgroup.
+// — the per-point sums of the general path (time_utils.py:74-76 autograd) regrouped. TG_WG
+// workgroups: each evaluates S (same order in every one: identical values) and writes the outputs
+// of its TG_N rows n (the single-workgroup version was a 17 us latency chain); bitwise deterministic.
+constexpr int TG_WG = 8, TG_N = 256 / TG_WG;
 struct TGradArgs {
     const float *fp;
     int w0te, w5te, wT2;  // fp32 [256][32] t_emb columns of linear.0 / linear.5, [32][256] timenet.2
@@ -906,11 +910,13 @@ struct TGradArgs {
 };
 
 __global__ __launch_bounds__(1024) void k_tgrad(TGradArgs a) {
-    __shared__ float S[32], th[256], dz1[256];
+    __shared__ float S[32], th[TG_N], dz1[TG_N], Sp[32][33];
     const int j = threadIdx.x;
-    if (j < 256) th[j] = a.tc[TC_TH + j];
-    {  // S[k]: 32 lanes per k, each over 16 of the 512 (n, layer) terms, then a fixed xor tree
-        const int k = j >> 5, part = j & 31;
+    const int n0 = blockIdx.x * TG_N;
+    if (j < TG_N) th[j] = a.tc[TC_TH + n0 + j];
+    {  // S[k]: thread (part, k) sums 16 of the 512 (n, layer) terms (a wave reads two 128-B rows of
+       // the [n][32] weight images per step: coalesced), then 32 threads add the parts in order
+        const int k = j & 31, part = j >> 5;
         float s = 0.f;
 #pragma unroll
         for (int i = 0; i < 16; i++) {
@@ -919,41 +925,49 @@ __global__ __launch_bounds__(1024) void k_tgrad(TGradArgs a) {
             const float gb = n < 256 ? a.gb0[n] : a.gb5[n - 256];
             s = fmaf(w, gb, s);
         }
+        Sp[part][k] = s;
+        __syncthreads();
+        if (j < 32) {
+            float t = 0.f;
 #pragma unroll
-        for (int o = 1; o < 32; o <<= 1) s += __shfl_xor(s, o);
-        if (part == 0) S[k] = s;
+            for (int q = 0; q < 32; q++) t += Sp[q][j];
+            S[j] = t;
+        }
     }
     // the folded t_emb columns 63..92 of linear.0 / linear.5: dW = gb (x) te (the dW kernel covers
     // x_emb and h only)
-    for (int e = j; e < 256 * 30; e += 1024) {
-        const int n = e / 30, k = e - n * 30;
+    for (int e = j; e < TG_N * 30; e += 1024) {
+        const int n = n0 + e / 30, k = e % 30;
         const float te = a.tc[TC_TE + k];
         a.gW0[n * 93 + 63 + k] = a.gb0[n] * te;
         a.gW5[n * 349 + 63 + k] = a.gb5[n] * te;
     }
     __syncthreads();
-    for (int e = j; e < 30 * 256; e += 1024) a.gT2w[e] = S[e >> 8] * th[e & 255];
-    if (j < 30) a.gT2b[j] = S[j];
-    {  // dZ_T1[n]: 4 lanes per n over 8 of the 30 (+2 zero) k terms each, then a fixed xor tree
+    for (int e = j; e < 30 * TG_N; e += 1024) {
+        const int k = e / TG_N, n = e % TG_N;
+        a.gT2w[k * 256 + n0 + n] = S[k] * th[n];
+    }
+    if (blockIdx.x == 0 && j < 30) a.gT2b[j] = S[j];
+    if (j < 4 * TG_N) {  // dZ_T1[n]: 4 lanes per n over 8 of the 30 (+2 zero) k terms each, then a fixed xor tree
         const int n = j >> 2, q = j & 3;
         float d = 0.f;
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             const int k = q * 8 + i;
-            if (k < 30) d = fmaf(a.fp[a.wT2 + k * 256 + n], S[k], d);
+            if (k < 30) d = fmaf(a.fp[a.wT2 + k * 256 + n0 + n], S[k], d);
         }
         d += __shfl_xor(d, 1);
         d += __shfl_xor(d, 2);
         d = th[n] > 0.f ? d : 0.f;
         if (q == 0) {
             dz1[n] = d;
-            a.gT0b[n] = d;
+            a.gT0b[n0 + n] = d;
         }
     }
     __syncthreads();
-    for (int e = j; e < 256 * a.tin; e += 1024) {  // coalesced [256][tin] outer product
+    for (int e = j; e < TG_N * a.tin; e += 1024) {  // coalesced [256][tin] outer product (this block's rows)
         const int n = e / a.tin, f = e - n * a.tin;
-        a.gT0w[e] = dz1[n] * a.tc[TC_TIN + f];
+        a.gT0w[(n0 + n) * a.tin + f] = dz1[n] * a.tc[TC_TIN + f];
     }
 }
 
@@ -2067,7 +2081,10 @@ int backward(int flags, int N, const float *packed, const float *saved, const fl
     g.gT0w = grads[P.pT0w]; g.gT0b = grads[P.pT0b]; g.gT2w = grads[P.pT2w]; g.gT2b = grads[P.pT2b];
     g.gW0 = grads[P.pLw[0]]; g.gW5 = grads[P.pLw[5]];
     g.tin = F.tin;
-    hipLaunchKernelGGL(k_tgrad, dim3(1), dim3(1024), 0, stream, g);
+    {
+        ScopedTimer tm("mlp_tgrad", stream);
+        hipLaunchKernelGGL(k_tgrad, dim3(TG_WG), dim3(1024), 0, stream, g);
+    }
     DGS_LAUNCH_CHECK("k_tgrad", false, stream);
     return DGS_OK;
 }

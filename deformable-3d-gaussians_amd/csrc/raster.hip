@@ -487,11 +487,10 @@ __global__ __launch_bounds__(256) void k_ranges(const uint32_t *__restrict__ cou
 // clamped 1-D stationary point. The bound is widened by 1 % + 1e-3 so the fp32 rounding of either
 // side can never cull a contributor: images and gradients are unchanged (the list positions kept in
 // n_contrib are those of the full list).
-__device__ __forceinline__ bool tile_reach(float2 g, float4 co, float x0, float y0) {
-    if (!(co.w >= 1.f / 255.f)) return false;  // alpha <= o < 1/255 on every pixel
-    const float thr = 2.f * __logf(255.f * co.w) * 1.01f + 1e-3f;
-    const float dxl = g.x - (x0 + (float)(TILE_X - 1)), dxh = g.x - x0;
-    const float dyl = g.y - (y0 + (float)(TILE_Y - 1)), dyh = g.y - y0;
+// min over the pixel-centre rectangle [x0, x1] x [y0, y1] of the conic's quadratic form <= thr
+__device__ __forceinline__ bool rect_reach(float2 g, float4 co, float x0, float x1, float y0, float y1, float thr) {
+    const float dxl = g.x - x1, dxh = g.x - x0;
+    const float dyl = g.y - y1, dyh = g.y - y0;
     if (dxl <= 0.f && dxh >= 0.f && dyl <= 0.f && dyh >= 0.f) return true;
     auto Q = [&](float dx, float dy) { return co.x * dx * dx + 2.f * co.y * dx * dy + co.z * dy * dy; };
     float q = Q(dxl, fminf(fmaxf(-co.y * dxl / co.z, dyl), dyh));
@@ -499,6 +498,19 @@ __device__ __forceinline__ bool tile_reach(float2 g, float4 co, float x0, float 
     q = fminf(q, Q(fminf(fmaxf(-co.y * dyl / co.x, dxl), dxh), dyl));
     q = fminf(q, Q(fminf(fmaxf(-co.y * dyh / co.x, dxl), dxh), dyh));
     return q <= thr;
+}
+__device__ __forceinline__ float reach_thr(float o) { return 2.f * __logf(255.f * o) * 1.01f + 1e-3f; }
+__device__ __forceinline__ bool tile_reach(float2 g, float4 co, float x0, float y0) {
+    if (!(co.w >= 1.f / 255.f)) return false;  // alpha <= o < 1/255 on every pixel
+    return rect_reach(g, co, x0, x0 + (float)(TILE_X - 1), y0, y0 + (float)(TILE_Y - 1), reach_thr(co.w));
+}
+// the same test for the two 16 x 8 halves of the tile (bit 0: rows 0-7, bit 1: rows 8-15); a
+// Gaussian reaching neither would reach no pixel centre of the tile either
+__device__ __forceinline__ uint32_t half_reach(float2 g, float4 co, float x0, float y0) {
+    if (!(co.w >= 1.f / 255.f)) return 0u;
+    const float thr = reach_thr(co.w), x1 = x0 + (float)(TILE_X - 1);
+    return (rect_reach(g, co, x0, x1, y0, y0 + 7.f, thr) ? 1u : 0u) |
+           (rect_reach(g, co, x0, x1, y0 + 8.f, y0 + 15.f, thr) ? 2u : 0u);
 }
 
 // The staged conic in exponent form: power * log2(e) = dx (q.x dx + q.y dy) + q.z dy^2 with
@@ -860,8 +872,9 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
     __shared__ uint32_t s_maxlast;
     const int tile = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int tx0 = (tile % gx) * TILE_X, ty0 = (tile / gx) * TILE_Y;
-    const int px0 = tx0 + (lane & 7), px1 = px0 + 8, py = ty0 + 8 * (tid >> 6) + (lane >> 3);
+    const int px0 = tx0 + (lane & 7), px1 = px0 + 8, py = ty0 + 8 * wv + (lane >> 3);
     const bool in0 = px0 < W && py < H, in1 = px1 < W && py < H;
     const f2 pfx = f2{(float)px0, (float)px1};
     const float pfy = (float)py;
@@ -914,11 +927,19 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
         uint32_t id = 0;
         float2 gl;
         float4 cl;
+#ifdef DGS_BWD2_HALF
+        uint32_t hm = 0;
+#endif
         if (prog < todo_total) {
             id = vals[end - prog - 1];
             gl = xy[id];
             cl = conic_o[id];
+#ifdef DGS_BWD2_HALF
+            hm = half_reach(gl, cl, (float)tx0, (float)ty0);
+            keep = hm != 0;
+#else
             keep = tile_reach(gl, cl, (float)tx0, (float)ty0);
+#endif
         }
         const int2 sl = compact_slot_n<B2 / 64>(keep, tid, s_wcnt);
         if (keep) {
@@ -927,12 +948,22 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
             s_co[sl.x] = cl;
             s_q[sl.x] = conic_q(cl);
             s_cd[sl.x] = rgbd[id];
+#ifdef DGS_BWD2_HALF
+            s_pos[sl.x] = prog | (int)(hm << 30);
+#else
             s_pos[sl.x] = prog;
+#endif
         }
         __syncthreads();
         const int n = sl.y;
         for (int j = 0; j < n; j++) {
+#ifdef DGS_BWD2_HALF
+            const int sp = s_pos[j];
+            if (!((__builtin_amdgcn_readfirstlane(sp) >> (30 + wv)) & 1)) continue;  // misses this wave's half
+            const uint32_t contributor = (uint32_t)(todo_total - 1 - (sp & 0x3fffffff));
+#else
             const uint32_t contributor = (uint32_t)(todo_total - 1 - s_pos[j]);  // position in the full list
+#endif
             const float2 g = s_xy[j];
             const float4 q = s_q[j];
             const f2 dx = g.x - pfx;

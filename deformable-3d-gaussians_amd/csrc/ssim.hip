@@ -37,17 +37,30 @@ __device__ inline float wave_sum(float v) {
 }
 
 // NM maps of the halo tile (zero outside the image) from `src` planes (plane stride `plane`) into
-// LDS, 42 x 42 each
+// LDS, 42 x 42 each. Every load of the thread is issued before the first LDS store (unrolled: a
+// rolled loop waited out one HBM round trip per 256 elements, 7 in a row)
 template <int NM>
 __device__ __forceinline__ void load_tile(float (*sm)[S][SP], const float *const src[NM], int H, int W, int x0,
                                           int y0) {
-    for (int e = threadIdx.x; e < S * S; e += 256) {
+    constexpr int NIT = (S * S + 255) / 256;
+    float v[NIT][NM];
+#pragma unroll
+    for (int it = 0; it < NIT; it++) {
+        const int e = threadIdx.x + 256 * it;
         const int ly = e / S, lx = e - ly * S;
         const int gy = y0 + ly - R, gx = x0 + lx - R;
-        const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
-        const size_t p = (size_t)gy * W + gx;
+        const bool in = e < S * S && gy >= 0 && gy < H && gx >= 0 && gx < W;
+        const size_t p = in ? (size_t)gy * W + gx : 0;
 #pragma unroll
-        for (int q = 0; q < NM; q++) sm[q][ly][lx] = in ? src[q][p] : 0.f;
+        for (int q = 0; q < NM; q++) v[it][q] = in ? src[q][p] : 0.f;
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; it++) {
+        const int e = threadIdx.x + 256 * it;
+        const int ly = e / S, lx = e - ly * S;
+        if (e < S * S)
+#pragma unroll
+            for (int q = 0; q < NM; q++) sm[q][ly][lx] = v[it][q];
     }
 }
 

@@ -39,7 +39,7 @@ def main():
         torch.cuda.synchronize()
         lib.dgs_timing_enable(0)
         r = {}
-        for k in ("mlp_fwd", "mlp_bwd", "mlp_dw", "mlp_dw_reduce"):
+        for k in ("mlp_fwd", "mlp_bwd", "mlp_dw", "mlp_dw_reduce", "mlp_tgrad"):
             n = _lib.I(0)
             ms = lib.dgs_timing_query(k.encode(), n)
             r[k] = ms / max(n.value, 1)
