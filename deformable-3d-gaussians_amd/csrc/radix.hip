@@ -299,3 +299,24 @@ template int sort_pairs<uint16_t>(uint16_t *, uint16_t *, uint32_t *, uint32_t *
 
 }  // namespace radix
 }  // namespace dgs
+
+// include/dgs.h test hook: the sort with its result copied back into (k0, v0)
+extern "C" int dgs_debug_sort_pairs(void *k0, void *k1, uint32_t *v0, uint32_t *v1, int n, int key_bytes, int end_bit,
+                                    void *stream_) {
+    using namespace dgs;
+    hipStream_t stream = (hipStream_t)stream_;
+    if (n < 0 || !k0 || !k1 || !v0 || !v1 || (key_bytes != 2 && key_bytes != 4) || end_bit < 0 ||
+        end_bit > 8 * key_bytes) {
+        set_error("dgs_debug_sort_pairs: bad argument");
+        return DGS_ERR_ARGS;
+    }
+    int alt = 0, rc;
+    if (key_bytes == 4)
+        rc = radix::sort_pairs<uint32_t>((uint32_t *)k0, (uint32_t *)k1, v0, v1, n, end_bit, stream, &alt);
+    else
+        rc = radix::sort_pairs<uint16_t>((uint16_t *)k0, (uint16_t *)k1, v0, v1, n, end_bit, stream, &alt);
+    if (rc != DGS_OK || !alt) return rc;
+    DGS_HIP_CHECK(hipMemcpyAsync(k0, k1, (size_t)n * key_bytes, hipMemcpyDeviceToDevice, stream));
+    DGS_HIP_CHECK(hipMemcpyAsync(v0, v1, (size_t)n * 4, hipMemcpyDeviceToDevice, stream));
+    return DGS_OK;
+}

@@ -504,15 +504,6 @@ __device__ __forceinline__ bool tile_reach(float2 g, float4 co, float x0, float 
     if (!(co.w >= 1.f / 255.f)) return false;  // alpha <= o < 1/255 on every pixel
     return rect_reach(g, co, x0, x0 + (float)(TILE_X - 1), y0, y0 + (float)(TILE_Y - 1), reach_thr(co.w));
 }
-// the same test for the two 16 x 8 halves of the tile (bit 0: rows 0-7, bit 1: rows 8-15); a
-// Gaussian reaching neither would reach no pixel centre of the tile either
-__device__ __forceinline__ uint32_t half_reach(float2 g, float4 co, float x0, float y0) {
-    if (!(co.w >= 1.f / 255.f)) return 0u;
-    const float thr = reach_thr(co.w), x1 = x0 + (float)(TILE_X - 1);
-    return (rect_reach(g, co, x0, x1, y0, y0 + 7.f, thr) ? 1u : 0u) |
-           (rect_reach(g, co, x0, x1, y0 + 8.f, y0 + 15.f, thr) ? 2u : 0u);
-}
-
 // The staged conic in exponent form: power * log2(e) = dx (q.x dx + q.y dy) + q.z dy^2 with
 // q = (-0.5 a, -b, -0.5 c) log2(e) and q.w = opacity, so G = 2^p is one v_exp_f32 (no scaling
 // multiply per pixel and Gaussian; 4 ops for the quadratic form). Every blend kernel evaluates
@@ -927,19 +918,11 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
         uint32_t id = 0;
         float2 gl;
         float4 cl;
-#ifdef DGS_BWD2_HALF
-        uint32_t hm = 0;
-#endif
         if (prog < todo_total) {
             id = vals[end - prog - 1];
             gl = xy[id];
             cl = conic_o[id];
-#ifdef DGS_BWD2_HALF
-            hm = half_reach(gl, cl, (float)tx0, (float)ty0);
-            keep = hm != 0;
-#else
             keep = tile_reach(gl, cl, (float)tx0, (float)ty0);
-#endif
         }
         const int2 sl = compact_slot_n<B2 / 64>(keep, tid, s_wcnt);
         if (keep) {
@@ -948,22 +931,12 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
             s_co[sl.x] = cl;
             s_q[sl.x] = conic_q(cl);
             s_cd[sl.x] = rgbd[id];
-#ifdef DGS_BWD2_HALF
-            s_pos[sl.x] = prog | (int)(hm << 30);
-#else
             s_pos[sl.x] = prog;
-#endif
         }
         __syncthreads();
         const int n = sl.y;
         for (int j = 0; j < n; j++) {
-#ifdef DGS_BWD2_HALF
-            const int sp = s_pos[j];
-            if (!((__builtin_amdgcn_readfirstlane(sp) >> (30 + wv)) & 1)) continue;  // misses this wave's half
-            const uint32_t contributor = (uint32_t)(todo_total - 1 - (sp & 0x3fffffff));
-#else
             const uint32_t contributor = (uint32_t)(todo_total - 1 - s_pos[j]);  // position in the full list
-#endif
             const float2 g = s_xy[j];
             const float4 q = s_q[j];
             const f2 dx = g.x - pfx;

@@ -139,6 +139,11 @@ void dgs_raster_set_exact_scale_grad(int on);
  * current device since process start: must be 0; a non-zero count means MLP outputs / gradients of
  * some launch are invalid (GPU tests assert it stays 0). -1 if the counter could not be read. */
 long long dgs_debug_guard_expiries(void);
+/* The binning's stable LSD radix sort on device buffers (tests only): sorts n (key, value) pairs by
+ * key bits [0, end_bit) (32-bit keys when key_bytes == 4, 16-bit when 2; end_bit <= 8 * key_bytes)
+ * using (k1, v1) as scratch; the result is left in (k0, v0). Stream-ordered. */
+int dgs_debug_sort_pairs(void *k0, void *k1, uint32_t *v0, uint32_t *v1, int n, int key_bytes, int end_bit,
+                         void *stream);
 
 /* ---- timing hooks (bench.py): per-kernel-class HIP event accumulation on the launch stream ---- */
 void dgs_timing_enable(int on);
