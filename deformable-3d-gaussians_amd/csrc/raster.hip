@@ -47,42 +47,62 @@ constexpr int SH_ROW = 48, SH_PAD = 49;  // odd LDS row stride: a thread-per-row
 
 // The block's nrow SH rows into LDS rows of SH_PAD floats: from one (P, 16, 3) tensor, or split
 // (rest != nullptr) from features_dc (P, 1, 3) and features_rest (P, 15, 3) as the Gaussian model
-// stores them (no concatenated copy). All loads are 16-byte units of contiguous row blocks.
-__device__ __forceinline__ void sh_stage_in(float *s_sh, const float *shs, const float *rest, int b0, int nrow) {
-    if (!rest) {
-        const float4 *src = reinterpret_cast<const float4 *>(shs + (size_t)b0 * SH_ROW);
-        for (int u = threadIdx.x; u < nrow * (SH_ROW / 4); u += 256) {
-            const float4 v = src[u];
-            float *d = s_sh + (u / (SH_ROW / 4)) * SH_PAD + (u % (SH_ROW / 4)) * 4;
-            d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
-        }
-        return;
-    }
-    auto get = [&](const float *base, int rowlen, int off) {
-        const int n = nrow * rowlen;
-        const float *src = base + (size_t)b0 * rowlen;
-        for (int u = threadIdx.x; u < div_up(n, 4); u += 256) {
-            float w[4];
-            if (4 * u + 3 < n) {
-                const float4 v = reinterpret_cast<const float4 *>(src)[u];
-                w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
-            } else {  // the tensor's last partial unit: no read past its end
+// stores them (no concatenated copy). All loads are 16-byte units of contiguous row blocks, every
+// load of a thread issued before its first LDS store (a rolled loop waited out one HBM round trip
+// per 256 units: 12 in a row for the 256 rows of a block).
+template <int MAXU>
+__device__ __forceinline__ void sh_get(float *s_sh, const float *base, int rowlen, int off, int b0, int nrow) {
+    const int n = nrow * rowlen;
+    const float *src = base + (size_t)b0 * rowlen;
+    const int nu = div_up(n, 4);
+    auto put = [&](int u, const float *w) {
+        int r = 4 * u / rowlen, c = 4 * u - r * rowlen;  // one division per unit, then carry
 #pragma unroll
-                for (int j = 0; j < 4; j++) w[j] = 4 * u + j < n ? src[4 * u + j] : 0.f;
-            }
-            int r = 4 * u / rowlen, c = 4 * u - r * rowlen;  // one division per unit, then carry
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                if (4 * u + j < n) s_sh[r * SH_PAD + off + c] = w[j];
-                if (++c == rowlen) {
-                    c = 0;
-                    r++;
-                }
+        for (int j = 0; j < 4; j++) {
+            if (4 * u + j < n) s_sh[r * SH_PAD + off + c] = w[j];
+            if (++c == rowlen) {
+                c = 0;
+                r++;
             }
         }
     };
-    get(shs, 3, 0);
-    get(rest, SH_ROW - 3, 3);
+    if (n % 4 == 0) {  // whole units (every block but possibly the tensor's last): loads first
+        float4 v[MAXU];
+#pragma unroll
+        for (int k = 0; k < MAXU; k++) {
+            const int u = threadIdx.x + 256 * k;
+            if (u < nu) v[k] = reinterpret_cast<const float4 *>(src)[u];
+        }
+#pragma unroll
+        for (int k = 0; k < MAXU; k++) {
+            const int u = threadIdx.x + 256 * k;
+            if (u < nu) {
+                const float w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+                put(u, w);
+            }
+        }
+        return;
+    }
+    for (int u = threadIdx.x; u < nu; u += 256) {
+        float w[4];
+        if (4 * u + 3 < n) {
+            const float4 v = reinterpret_cast<const float4 *>(src)[u];
+            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+        } else {  // the tensor's last partial unit: no read past its end
+#pragma unroll
+            for (int j = 0; j < 4; j++) w[j] = 4 * u + j < n ? src[4 * u + j] : 0.f;
+        }
+        put(u, w);
+    }
+}
+
+__device__ __forceinline__ void sh_stage_in(float *s_sh, const float *shs, const float *rest, int b0, int nrow) {
+    if (!rest) {
+        sh_get<SH_ROW / 4>(s_sh, shs, SH_ROW, 0, b0, nrow);  // 256 rows x 12 units: 12 per thread
+        return;
+    }
+    sh_get<1>(s_sh, shs, 3, 0, b0, nrow);                                  // 192 units
+    sh_get<(256 * (SH_ROW - 3) / 4 + 255) / 256>(s_sh, rest, SH_ROW - 3, 3, b0, nrow);  // 2880 units
 }
 
 // LDS rows -> the (P, 16, 3) gradient, or split into the dc (P, 1, 3) / rest (P, 15, 3) gradients
