@@ -59,8 +59,8 @@ def parse():
     ap.add_argument("--kernel-timing", choices=["roofline", "major", "all", "none"], default="roofline",
                     help="kernel classes timed with HIP events inside the timed region. Each event record costs "
                          "~6 us of GPU idle on the launch stream (profiles/r2c trace), so the default times only the "
-                         "roofline kernel (mlp_dw: the longest launch of the step, 2 records per step); 'major' adds "
-                         "the other MFMA and blend classes, 'all' every class, 'none' nothing")
+                         "three MLP classes, the candidates for the longest launch of the step, on every 4th step; "
+                         "'major' adds the blend classes, 'all' every class, 'none' nothing (every step)")
     ap.add_argument("--6dof", dest="six_dof", action="store_true",
                     help="6-DoF screw deformation head (config 4, trex --is_6dof) instead of d_xyz")
     ap.add_argument("--raw-init", action="store_true",
@@ -258,10 +258,11 @@ def main():
         step(k)
     torch.cuda.synchronize()
     lib.dgs_timing_reset()
-    lib.dgs_timing_select({"roofline": b"mlp_dw", "major": b"mlp_fwd,mlp_bwd,mlp_dw,blend_fwd,blend_bwd", "all": b"",
-                           "none": b""}[args.kernel_timing])
-    # the roofline kernel is timed on every 4th step (each timed launch adds two stream markers, ~6 us of
-    # GPU idle each, inside the timed region); the other classes, when asked for, on every step
+    lib.dgs_timing_select({"roofline": b"mlp_fwd,mlp_bwd,mlp_dw", "major": b"mlp_fwd,mlp_bwd,mlp_dw,blend_fwd,blend_bwd",
+                           "all": b"", "none": b""}[args.kernel_timing])
+    # the roofline candidates are timed on every 4th step (each timed launch adds two stream markers, ~6 us
+    # of GPU idle each, inside the timed region); the other classes, when asked for, on every step. The
+    # roofline reports the timed class with the longest average launch (the dominant kernel)
     lib.dgs_timing_sample(4 if args.kernel_timing == "roofline" and args.steps >= 8 else 1)
     lib.dgs_timing_enable(0 if args.kernel_timing == "none" else 1)
     if world > 1:

@@ -991,6 +991,24 @@ struct RJobs {
 };
 
 // one thread per gradient element of every parameter; sums the splits in a fixed order
+// sum of one element over ns slabs in slab order (deterministic): RU loads issued before the adds
+// that consume them (one HBM round trip per RU slabs; adding the predicated 0.f is exact)
+#ifndef DGS_REDUCE_U
+#define DGS_REDUCE_U 8
+#endif
+__device__ __forceinline__ float slab_sum(const float *sl, int ns) {
+    constexpr int RU = DGS_REDUCE_U;
+    float s = 0.f;
+    for (int b = 0; b < ns; b += RU) {
+        float v[RU];
+#pragma unroll
+        for (int k = 0; k < RU; k++) v[k] = b + k < ns ? sl[(size_t)(b + k) * SLAB] : 0.f;
+#pragma unroll
+        for (int k = 0; k < RU; k++) s += v[k];
+    }
+    return s;
+}
+
 __global__ __launch_bounds__(256) void k_dw_reduce(RJobs R, const float *__restrict__ slabs) {
     int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= R.begin[R.n]) return;
@@ -1009,13 +1027,10 @@ __global__ __launch_bounds__(256) void k_dw_reduce(RJobs R, const float *__restr
         if (f < 0) return;  // a folded t_emb column: written by k_tgrad
         const int kt = f >= J.k1 ? 1 : 0, kl = f - (kt ? J.k1 : 0);
         const float *sl = slabs + (size_t)J.block0[kt] * SLAB + n * WT + kl;
-        // unrolled: the slab loads are issued together, the adds stay in slab order (deterministic)
-#pragma unroll 8
-        for (int sp = 0; sp < J.nsplit[kt]; sp++) s += sl[(size_t)sp * SLAB];
+        s = slab_sum(sl, J.nsplit[kt]);
     } else {
         const float *sl = slabs + (size_t)J.block0[0] * SLAB + WT * WT + n;
-#pragma unroll 8
-        for (int sp = 0; sp < J.nsplit[0]; sp++) s += sl[(size_t)sp * SLAB];
+        s = slab_sum(sl, J.nsplit[0]);
     }
     J.dst[idx] = s;
 }

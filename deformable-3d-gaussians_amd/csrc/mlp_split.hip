@@ -2006,17 +2006,17 @@ int forward(int flags, int N, const float *xyz, const float *t, const float *pac
     a.nblk = nblk;
     a.queue = nblk > 0 ? block_queue(stream, 0) : nullptr;
     const int grid = persistent_grid(nblk, a.queue);
-    {
-        ScopedTimer tm("mlp_fwd", stream);
-        if (P.F.blender && (saved || P.F.uniform_t)) {
-            // the folded biases (uniform t) are needed without saved activations too (inference)
-            a.tc = saved ? saved + (size_t)P.F.nsaved * a.Ns + mask_words(P.F, a.Ns) : timenet_scratch(stream);
-            if (!a.tc) {
-                set_error("dgs_deform_forward: could not allocate the timenet scratch");
-                return DGS_ERR_HIP;
-            }
-            hipLaunchKernelGGL(k_timenet, dim3(1), dim3(256), 0, stream, a);
+    if (P.F.blender && (saved || P.F.uniform_t)) {
+        // the folded biases (uniform t) are needed without saved activations too (inference)
+        a.tc = saved ? saved + (size_t)P.F.nsaved * a.Ns + mask_words(P.F, a.Ns) : timenet_scratch(stream);
+        if (!a.tc) {
+            set_error("dgs_deform_forward: could not allocate the timenet scratch");
+            return DGS_ERR_HIP;
         }
+        hipLaunchKernelGGL(k_timenet, dim3(1), dim3(256), 0, stream, a);
+    }
+    {
+        ScopedTimer tm("mlp_fwd", stream);  // k_fwd only: the class's FLOP count is the trunk's + heads'
         const bool fold = P.F.uniform_t;  // t_emb folded into the biases (a.tc is set above)
         if (saved && fold)
             hipLaunchKernelGGL((k_fwd<true, true>), dim3(grid), dim3(NTHR), 0, stream, a);

@@ -15,7 +15,8 @@ import sys
 from collections import defaultdict
 
 CLASSES = {  # bench.py kernel class -> substring(s) of the device symbol (split-bf16 | exact-fp32 MLP)
-    "mlp_fwd": ("mlps::k_fwd", "k_mlp_fwd"), "mlp_bwd": ("mlps::k_bwd", "k_mlp_bwd"),
+    # mlp_fwd: the training forward (saved activations) only, the launches bench.py times
+    "mlp_fwd": ("mlps::k_fwd<true", "k_mlp_fwd<true"), "mlp_bwd": ("mlps::k_bwd", "k_mlp_bwd"),
     "mlp_dw": ("mlp::k_dw(", "mlps::k_dw(", "mlps::k_dws(", "mlps::k_dwg(", "mlp4k_dw"), "mlp_dw_reduce": "k_dw_reduce",
     "preprocess_fwd": ("k_preprocess(", "k_preprocess<"), "duplicate": "k_duplicate", "ranges": "k_ranges",
     "blend_fwd": "k_blend_fwd", "blend_bwd": "k_blend_bwd", "preprocess_bwd": "k_preprocess_bwd",
