@@ -866,6 +866,9 @@ __device__ __forceinline__ f2 sel2(bool a, bool b, f2 x, f2 y) { return f2{a ? x
 #else
 #define BWD2_OCC
 #endif
+// DEPTH: the depth output has a gradient (dL_ddepth != nullptr); without one (every training step: the
+// loss reads only the image) the depth terms, the depth colour-behind state and its loads drop out
+template <bool DEPTH>
 __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restrict__ ranges, const uint32_t *__restrict__ vals,
                                                    uint32_t cap, int W, int H, int gx, const float *bg,
                                                    const float2 *__restrict__ xy, const float4 *__restrict__ conic_o,
@@ -902,7 +905,7 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
         dp0.x = dL_dpix[pid0];
         dp1.x = dL_dpix[HW + pid0];
         dp2.x = dL_dpix[2 * HW + pid0];
-        ddep.x = dL_ddepth ? dL_ddepth[pid0] : 0.f;
+        if (DEPTH) ddep.x = dL_ddepth[pid0];
     }
     if (in1) {
         Tfinal.y = final_T[pid1];
@@ -910,7 +913,7 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
         dp0.y = dL_dpix[pid1];
         dp1.y = dL_dpix[HW + pid1];
         dp2.y = dL_dpix[2 * HW + pid1];
-        ddep.y = dL_ddepth ? dL_ddepth[pid1] : 0.f;
+        if (DEPTH) ddep.y = dL_ddepth[pid1];
     }
     if (tid == 0) s_maxlast = 0;
     __syncthreads();
@@ -981,12 +984,16 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
             const f2 w = ae * T;
             // colour behind this Gaussian (acc) is updated eagerly after its use: the reference's
             // deferred last_alpha * last_color + (1 - last_alpha) * acc at the next active Gaussian
-            const f2 d0 = cd.x - acc0, d1 = cd.y - acc1, d2 = cd.z - acc2, d3 = cd.w - accd;
-            f2 dLda = d0 * dp0 + d1 * dp1 + d2 * dp2 + d3 * ddep;
+            const f2 d0 = cd.x - acc0, d1 = cd.y - acc1, d2 = cd.z - acc2;
+            f2 dLda = d0 * dp0 + d1 * dp1 + d2 * dp2;
+            if constexpr (DEPTH) {
+                const f2 d3 = cd.w - accd;
+                dLda = dLda + d3 * ddep;
+                accd = ae * d3 + accd;
+            }
             acc0 = ae * d0 + acc0;
             acc1 = ae * d1 + acc1;
             acc2 = ae * d2 + acc2;
-            accd = ae * d3 + accd;
             dLda = dLda * T + kbg * inv;
             // dG/dmean2D = -G (conic . d), dG/dconic = -G d d^T / 2: with u = dL/dG G the per-pixel
             // terms are co (u d) and u d d^T, their factors (-hx, -hy, -0.5) applied after the sums
@@ -995,7 +1002,7 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
             const f2 udx = u * dx, udy = u * dy;
             const f2 mxp = co.x * udx + co.y * udy, myp = co.y * udx + co.z * udy;
             const f2 cxp = udx * dx, cyp = udx * dy, czp = udy * dy;
-            const f2 vr = w * dp0, vg = w * dp1, vb = w * dp2, vd = w * ddep;
+            const f2 vr = w * dp0, vg = w * dp1, vb = w * dp2, vd = DEPTH ? w * ddep : zero;
             const float w0 = row_sum15(fold16(fold32(mxp.x + mxp.y, myp.x + myp.y), fold32(cxp.x + cxp.y, cyp.x + cyp.y)));
             const float w1 = row_sum15(fold16(fold32(czp.x + czp.y, vop.x + vop.y), fold32(vr.x + vr.y, vg.x + vg.y)));
             const float w2 = row_sum15(fold16(fold32(vb.x + vb.y, vd.x + vd.y),
@@ -1935,8 +1942,14 @@ static int raster_backward(dgs_raster_ctx *c, const float *dL_dcolor, const floa
             hipLaunchKernelGGL(k_blend_bwd, dim3(T), dim3(TILE_PIX), 0, stream, c->ranges, c->vals, cap, c->W, c->H, c->gx,
                                c->s.bg, c->xy, c->conic_o, c->rgbd, c->final_T, c->n_contrib, dL_dcolor, dL_ddepth, acc);
         else
-            hipLaunchKernelGGL(k_blend_bwd2, dim3(T), dim3(B2), 0, stream, c->ranges, c->vals, cap, c->W, c->H, c->gx,
-                               c->s.bg, c->xy, c->conic_o, c->rgbd, c->final_T, c->n_contrib, dL_dcolor, dL_ddepth, acc);
+            if (dL_ddepth)
+                hipLaunchKernelGGL(k_blend_bwd2<true>, dim3(T), dim3(B2), 0, stream, c->ranges, c->vals, cap, c->W, c->H,
+                                   c->gx, c->s.bg, c->xy, c->conic_o, c->rgbd, c->final_T, c->n_contrib, dL_dcolor,
+                                   dL_ddepth, acc);
+            else
+                hipLaunchKernelGGL(k_blend_bwd2<false>, dim3(T), dim3(B2), 0, stream, c->ranges, c->vals, cap, c->W, c->H,
+                                   c->gx, c->s.bg, c->xy, c->conic_o, c->rgbd, c->final_T, c->n_contrib, dL_dcolor,
+                                   nullptr, acc);
     }
     DGS_LAUNCH_CHECK("k_blend_bwd", dbg, stream);
     const float fx = c->W / (2.f * c->s.tanfovx), fy = c->H / (2.f * c->s.tanfovy);
