@@ -156,13 +156,15 @@ __device__ inline void mma6(const AFrag &a, const AFrag &b, f32x4 &acc, f32x4 &l
 
 #ifdef DGS_MLP_PROFILE  // diagnostic build only (tools/mlp_phase.py): per-phase s_memtime stamps
 __device__ unsigned long long *dgs_mlps_prof;
+// only the workgroup's first block (launched while every CU is busy) is stamped: p0 == blockIdx.x * BM
 #define DGS_STAMP(k)                                                                                   \
     do {                                                                                               \
-        if (threadIdx.x == 0) dgs_mlps_prof[blockIdx.x * 64 + (k)] = __builtin_amdgcn_s_memtime();     \
+        if (threadIdx.x == 0 && p0 == (int)blockIdx.x * BM)                                            \
+            dgs_mlps_prof[blockIdx.x * 64 + (k)] = __builtin_amdgcn_s_memtime();                       \
     } while (0)
 #define DGS_WSTAMP(k, L)                                                                               \
     do {                                                                                               \
-        if (L == 3 && (threadIdx.x & 63) == 0)                                                         \
+        if (L == 3 && (threadIdx.x & 63) == 0 && p0 == (int)blockIdx.x * BM)                           \
             dgs_mlps_prof[blockIdx.x * 64 + (k) + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memtime();  \
     } while (0)
 #else
@@ -668,6 +670,15 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
         const float *bias = fold && L == 0 ? a.tc + TC_C0 : fold && L == 5 ? a.tc + TC_C5 : a.fp + a.bL[L];
         const BiasPre bp{&bv, bias, r, lane};
         const HGate hg{hwr, hrd, L == 5 ? (fold ? 2 : 3) : 0, 2u * L, true, lane};
+#if defined(DGS_DIAG_GPRIO)  // experiment: issue priority by dispatch age during the GEMM only (younger = higher)
+        if (DGS_DIAG_GPRIO == 1) {
+            if (r >= 12) __builtin_amdgcn_s_setprio(1);
+        } else {
+            if (r >= 12) __builtin_amdgcn_s_setprio(3);
+            else if (r >= 8) __builtin_amdgcn_s_setprio(2);
+            else if (r >= 4) __builtin_amdgcn_s_setprio(1);
+        }
+#endif
         if (L == 0) {
             if constexpr (FOLD) gemm<2, NQB>(Aw, lds, g0, 0, lane, c, bp);  // XE only
             else gemm<3, NQB>(Aw, lds, g0, 0, lane, c, bp);                 // XE | TE
@@ -677,6 +688,9 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
         } else {
             gemm<8, NQB>(Aw, lds, g0, 0, lane, c, bp, hg);
         }
+#if defined(DGS_DIAG_GPRIO)
+        __builtin_amdgcn_s_setprio(0);
+#endif
         DGS_STAMP(4 + 2 * L);
         DGS_WSTAMP(22, L);  // per wave: GEMM end (layer 3)
 #ifdef DGS_DIAG_EPI_PRIO  // experiment: raised issue priority through the epilogue
@@ -721,7 +735,7 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
     }
     DGS_STAMP(21);
 #ifdef DGS_MLP_PROFILE
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0 && p0 == (int)blockIdx.x * BM) {
         dgs_mlps_prof[blockIdx.x * 64 + 60] = __builtin_amdgcn_s_memrealtime();
         dgs_mlps_prof[blockIdx.x * 64 + 61] = __builtin_amdgcn_s_memtime();
     }
