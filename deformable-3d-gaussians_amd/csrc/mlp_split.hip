@@ -704,7 +704,9 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
         }
         if (L == 3 && r == 0) DGS_STAMP(54);
         // this wave's rows are H k-step r / 2: every wave must have read it in this layer
+#ifndef DGS_DIAG_NO_WAR  // timing experiment only (races): no wait for the readers of the overwritten k-step
         if (L > 0) lds_wait_ge(hrd + (r >> 1), 16u * L, lds_peek(hrd + (r >> 1)));
+#endif
         if (L == 3 && r == 0) DGS_STAMP(56);
 #pragma unroll
         for (int q = 0; q < NQB; q++) acc_to_lds(c[q], lds, G_H, r, q, lane);
