@@ -11,7 +11,11 @@ starts = [int(r["Start_Timestamp"]) for r in rows
           if "k_mlp_fwd<true>" in r["Kernel_Name"] or "mlps::k_fwd<true" in r["Kernel_Name"]]  # <SAVE[, FOLD]>
 if len(starts) < 3:
     sys.exit("not enough steps")
-lo, hi = starts[-6], starts[-1]   # last 5 complete steps
+# last 5 complete timed steps: the final k_fwd is bench.py's pair-count render after the timed loop,
+# so the window ends at the one before it (the post-loop host work is not step idle)
+if len(starts) < 8:
+    sys.exit("not enough steps")
+lo, hi = starts[-7], starts[-2]
 steps = 5
 busy = 0
 per = defaultdict(float)
