@@ -77,7 +77,7 @@ constexpr int ST_TE = 64, ST_TIN = 96;
 constexpr int MR_TH = M_TH / 16;
 
 static_assert(G_TE == G_XE + 8 && G_H == G_TE + 4, "XE|TE|H must be contiguous");
-static_assert(G_FWD * UG * 16 <= 160 * 1024 && G_BWD * UG * 16 <= 160 * 1024, "LDS");
+static_assert(G_FWD * UG * 16 + 8 * 256 * 4 <= 160 * 1024 && G_BWD * UG * 16 <= 160 * 1024, "LDS (k_fwd: + trunk biases)");
 static_assert(112 * BM * 4 <= 32 * UG * 16, "fp32 staging must fit the H region");
 
 // ------------------------------------------------------------------------------------------------
@@ -494,19 +494,12 @@ __global__ __launch_bounds__(256) void k_timenet(FwdArgs a) {
     }
 }
 
-// this lane's bias rows of the layer, loaded ahead of the GEMM
-struct BiasPre {
-    float4 *b;
-    const float *bias;
-    int r, lane;
-    __device__ void operator()() const { *b = load_bias4(bias, r, lane); }
-};
-
 // One block of NQB 16-point column tiles (NQB = 4: the 64-point blocks; NQB = 1: the 16-point tail
 // blocks that spread the last, sparse round of blocks over the idle CUs). p0: first point; slot: the
 // block's relu'-mask slot.
 template <bool SAVE, int NQB, bool FOLD>
-__device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_t *hwr, uint32_t *hrd, int p0, int slot) {
+__device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_t *hwr, uint32_t *hrd, const float4 *sb,
+                                          int p0, int slot) {
     constexpr int BMB = 16 * NQB;  // points of this block (the LDS images keep the BM-point stride)
     float *lf = reinterpret_cast<float *>(lds);
     float *stage = lf + G_H * UG * 4;  // fp32 [112][BM] feature staging (H region, before the trunk)
@@ -666,9 +659,11 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
         const int nk = layer_kpad_f(F, L) / 32;
         zero_tiles(c);
         const bf16x8 *Aw = a.img + (size_t)(a.fL[L] + r * nk) * KSLOT;
-        float4 bv;  // loaded behind the A prologue: its latency is covered by the GEMM
-        const float *bias = fold && L == 0 ? a.tc + TC_C0 : fold && L == 5 ? a.tc + TC_C5 : a.fp + a.bL[L];
-        const BiasPre bp{&bv, bias, r, lane};
+        float4 bv;
+        // the bias comes from the workgroup's LDS copy after the GEMM (sb): a register preload
+        // across the GEMM was spilled at 128 VGPRs and its scratch reload sat in every epilogue
+        using PreT = NoPre;
+        const PreT bp{};
         const HGate hg{hwr, hrd, L == 5 ? (fold ? 2 : 3) : 0, 2u * L, true, lane};
 #if defined(DGS_DIAG_GPRIO)  // experiment: issue priority by dispatch age during the GEMM only (younger = higher)
         if (DGS_DIAG_GPRIO == 1) {
@@ -683,7 +678,7 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
             if constexpr (FOLD) gemm<2, NQB>(Aw, lds, g0, 0, lane, c, bp);  // XE only
             else gemm<3, NQB>(Aw, lds, g0, 0, lane, c, bp);                 // XE | TE
         } else if (L == 5) {
-            if constexpr (FOLD) gemm<10, NQB, BiasPre, HGate, 2>(Aw, lds, g0, 0, lane, c, bp, hg);  // XE | H
+            if constexpr (FOLD) gemm<10, NQB, PreT, HGate, 2>(Aw, lds, g0, 0, lane, c, bp, hg);  // XE | H
             else gemm<11, NQB>(Aw, lds, g0, 0, lane, c, bp, hg);                                    // XE | TE | H
         } else {
             gemm<8, NQB>(Aw, lds, g0, 0, lane, c, bp, hg);
@@ -691,6 +686,7 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
 #if defined(DGS_DIAG_GPRIO)
         __builtin_amdgcn_s_setprio(0);
 #endif
+        bv = sb[64 * L + 4 * r + kq];
         DGS_STAMP(4 + 2 * L);
         DGS_WSTAMP(22, L);  // per wave: GEMM end (layer 3)
 #ifdef DGS_DIAG_EPI_PRIO  // experiment: raised issue priority through the epilogue
@@ -749,12 +745,20 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
     __shared__ bf16x8 lds[G_FWD * UG];
     __shared__ uint32_t hwr[8], hrd[8];  // trunk hand-off counters (HGate)
     __shared__ int s_next;
+    // trunk biases (launch constants: FOLD's linear.0 / linear.5 biases come from k_timenet), one
+    // float4 per (layer, 4 rows); the first block's staging barriers publish them
+    __shared__ float4 s_bias[8 * 64];
+    for (int i = threadIdx.x; i < 8 * 64; i += NTHR) {
+        const int L = i >> 6;
+        const float *bias = FOLD && L == 0 ? a.tc + TC_C0 : FOLD && L == 5 ? a.tc + TC_C5 : a.fp + a.bL[L];
+        s_bias[i] = reinterpret_cast<const float4 *>(bias)[i & 63];
+    }
     CLK_BEGIN();
     for (int b = blockIdx.x;;) {
         int nx = 0;
         if (a.queue && threadIdx.x == 0) nx = queue_take(a.queue);
-        if (b < a.nfull) fwd_block<SAVE, NQ, FOLD>(a, lds, hwr, hrd, b * BM, b);
-        else fwd_block<SAVE, 1, FOLD>(a, lds, hwr, hrd, a.nfull * BM + (b - a.nfull) * 16, b);
+        if (b < a.nfull) fwd_block<SAVE, NQ, FOLD>(a, lds, hwr, hrd, s_bias, b * BM, b);
+        else fwd_block<SAVE, 1, FOLD>(a, lds, hwr, hrd, s_bias, a.nfull * BM + (b - a.nfull) * 16, b);
         if (!a.queue) break;
         if (threadIdx.x == 0) s_next = nx;
         __syncthreads();  // also: the next block's staging overwrites LDS this one's heads read
