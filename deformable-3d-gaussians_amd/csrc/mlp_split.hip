@@ -77,7 +77,7 @@ constexpr int ST_TE = 64, ST_TIN = 96;
 constexpr int MR_TH = M_TH / 16;
 
 static_assert(G_TE == G_XE + 8 && G_H == G_TE + 4, "XE|TE|H must be contiguous");
-static_assert(G_FWD * UG * 16 + 8 * 256 * 4 <= 160 * 1024 && G_BWD * UG * 16 <= 160 * 1024, "LDS (k_fwd: + trunk biases)");
+static_assert(G_FWD * UG * 16 + (8 * 256 + 16) * 4 <= 160 * 1024 && G_BWD * UG * 16 <= 160 * 1024, "LDS (k_fwd: + trunk biases)");
 static_assert(112 * BM * 4 <= 32 * UG * 16, "fp32 staging must fit the H region");
 
 // ------------------------------------------------------------------------------------------------
@@ -724,7 +724,7 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
     if (hq >= 0) {
         f32x4 c1[1] = {zero4()};
         gemm<8, 1>(a.img + (size_t)a.fHd * KSLOT, lds, G_H, hq, lane, c1, NoPre(), HGate{hwr, hrd, 0, 16u, false, lane});
-        const float4 b = load_bias4(a.fp + a.bHd, 0, lane);
+        const float4 b = sb[8 * 64 + kq];
         c1[0] += f32x4{b.x, b.y, b.z, b.w};
         const int p = p0 + 16 * hq + col;
 #pragma unroll
@@ -745,12 +745,16 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
     __shared__ bf16x8 lds[G_FWD * UG];
     __shared__ uint32_t hwr[8], hrd[8];  // trunk hand-off counters (HGate)
     __shared__ int s_next;
-    // trunk biases (launch constants: FOLD's linear.0 / linear.5 biases come from k_timenet), one
-    // float4 per (layer, 4 rows); the first block's staging barriers publish them
-    __shared__ float4 s_bias[8 * 64];
-    for (int i = threadIdx.x; i < 8 * 64; i += NTHR) {
+    // trunk and head biases (launch constants: FOLD's linear.0 / linear.5 biases come from
+    // k_timenet), one float4 per (layer, 4 rows), the heads' 16 rows last; the first block's staging
+    // barriers publish them
+    __shared__ float4 s_bias[8 * 64 + 4];
+    for (int i = threadIdx.x; i < 8 * 64 + 4; i += NTHR) {
         const int L = i >> 6;
-        const float *bias = FOLD && L == 0 ? a.tc + TC_C0 : FOLD && L == 5 ? a.tc + TC_C5 : a.fp + a.bL[L];
+        const float *bias = L == 8                ? a.fp + a.bHd
+                            : FOLD && L == 0      ? a.tc + TC_C0
+                            : FOLD && L == 5      ? a.tc + TC_C5
+                                                  : a.fp + a.bL[L];
         s_bias[i] = reinterpret_cast<const float4 *>(bias)[i & 63];
     }
     CLK_BEGIN();
