@@ -215,13 +215,16 @@ struct ClkStamp {
 #define CLK_BEGIN()
 #define CLK_END(k)
 #endif
+#ifndef DGS_SPIN_SLEEP
+#define DGS_SPIN_SLEEP 1  // s_sleep units (64 clocks) between polls of a hand-off counter
+#endif
 __device__ __forceinline__ uint32_t lds_peek(const uint32_t *f) {
     return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ void lds_wait_ge(const uint32_t *f, uint32_t target, uint32_t seen) {
     int guard = 0;
     for (; __builtin_amdgcn_readfirstlane(seen) < target && guard < (1 << 20); guard++) {
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(DGS_SPIN_SLEEP);
         seen = lds_peek(f);
     }
     if (guard == (1 << 20) && __builtin_amdgcn_readfirstlane(seen) < target && (threadIdx.x & 63) == 0)
