@@ -51,10 +51,8 @@ def parse():
     ap.add_argument("--n", type=int, default=100_000)
     ap.add_argument("--res", type=int, default=800)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-warmup", type=int, default=1)
-    ap.add_argument("--cpu-steps", type=int, default=5,
-                    help="timed CPU-oracle steps (median). SURVEY.md 8d asks 3 warm-up + 20; the default keeps the "
-                         "bench within minutes (~20 s of CPU work) and the line states the protocol used")
+    ap.add_argument("--cpu-warmup", type=int, default=3)
+    ap.add_argument("--cpu-steps", type=int, default=20, help="timed CPU steps (median; SURVEY.md 8d: 3 + 20)")
     ap.add_argument("--no-adam", action="store_true", help="time only the reference's span (fwd+bwd)")
     ap.add_argument("--kernel-timing", choices=["roofline", "major", "all", "none"], default="roofline",
                     help="kernel classes timed with HIP events inside the timed region. Each event record costs "
@@ -131,51 +129,70 @@ KERNEL_CLASSES = ["mlp_fwd", "mlp_bwd", "mlp_dw", "mlp_dw_reduce", "mlp_tgrad", 
                   "blend_fwd", "blend_bwd", "preprocess_bwd", "ssim_fwd", "ssim_bwd", "inputs_fwd", "inputs_bwd", "adam"]
 
 
-def cpu_baseline(N, res, steps, warmup=1):
-    """The oracle (oracle/mlp_ref.py float64 numpy MLP + oracle/raster_ref.c OpenMP rasterizer + torch-CPU
-    L1/SSIM) timed on the host: `warmup` untimed then `steps` timed full steps of the same workload."""
-    from deformgs.synthetic import synth_camera, synth_gaussians
-    from oracle import mlp_ref
-    from oracle.raster import OracleRaster, make_settings
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown CPU"
+
+
+def cpu_baseline(N, res, steps, warmup=3):
+    """SURVEY.md 8d's CPU column: the build's CPU restatement of the same step on the host — the
+    reference's own torch forward of DeformNetworkBaseline (deform_network.glue_forward: PE by cat of
+    sin / cos bands, timenet, 8 x Linear + ReLU with the skip, heads; fp32, autograd backward) + the C
+    raster oracle (oracle/raster_ref.c: OpenMP forward and OpenMP backward over fixed tile chunks) + the
+    reference's torch-CPU L1 / SSIM; `warmup` untimed then `steps` timed full steps (median)."""
+    from deformgs.deform_network import DeformNetworkBaseline
     from deformgs.loss import l1_loss, ssim
-    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
-    from weights import mlp_weights
+    from deformgs.synthetic import synth_camera, synth_gaussians
     threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
+    os.environ.setdefault("OMP_NUM_THREADS", str(threads))
+    from oracle.raster import OracleRaster, make_settings
     torch.set_num_threads(threads)
     g = synth_gaussians(N, seed=0, device="cpu")
     cam = synth_camera(res, res, index=0, fid=0.5, device="cpu")
-    p = mlp_weights(mlp_ref.param_shapes(True, False), seed=1)
-    for k in p:  # same steady-state head scale as the GPU run
-        if k.startswith(("gaussian_warp", "gaussian_rotation", "gaussian_scaling")):
-            p[k] = p[k] * 0.01
+    torch.manual_seed(0)
+    net = DeformNetworkBaseline(is_blender=True)
+    with torch.no_grad():  # same steady-state head scale as the GPU run
+        for head in (net.gaussian_warp, net.gaussian_rotation, net.gaussian_scaling):
+            head.weight.mul_(0.01)
+            head.bias.mul_(0.01)
     gt = torch.rand((3, res, res), generator=torch.Generator().manual_seed(7))
     s = make_settings(res, res, math.tan(cam.FoVx / 2), math.tan(cam.FoVy / 2), [0, 0, 0], 1.0,
                       cam.world_view_transform.numpy(), cam.full_proj_transform.numpy(), 3, cam.camera_center.numpy())
-    xyz = g["xyz"].numpy()
+    xyz = g["xyz"]
     shs = torch.cat([g["features_dc"], g["features_rest"]], 1).numpy()
+    sc = torch.exp(g["scaling"])
+    rq = torch.nn.functional.normalize(g["rotation"])
+    op = torch.sigmoid(g["opacity"]).numpy()
+    t = torch.full((N, 1), 0.5)
     times = []
     for it in range(warmup + steps):
         t0 = time.perf_counter()
-        t = np.full((N, 1), 0.5, np.float32)
-        out, c = mlp_ref.forward(p, xyz, t, True, False)
-        means = (xyz + out["d_xyz"]).astype(np.float32)
-        scales = (np.exp(g["scaling"].numpy()) + out["d_scale"]).astype(np.float32)
-        rq = g["rotation"].numpy()
-        rots = (rq / np.linalg.norm(rq, axis=1, keepdims=True) + out["d_rot"]).astype(np.float32)
-        op = torch.sigmoid(g["opacity"]).numpy()
+        net.zero_grad(set_to_none=True)
+        d_xyz, d_rot, d_scale = net.glue_forward(xyz, t)
+        means = (xyz + d_xyz).detach().numpy()
+        scales = (sc + d_scale).detach().numpy()
+        rots = (rq + d_rot).detach().numpy()
         o = OracleRaster(s, means, shs=shs, opacities=op, scales=scales, rotations=rots)
         img = torch.from_numpy(o.color).requires_grad_(True)
         loss = 0.8 * l1_loss(img, gt) + 0.2 * (1.0 - ssim(img, gt))
         loss.backward()
         gr = o.backward(img.grad.numpy())
-        gout = {"d_xyz": gr["means3D"], "d_rot": gr["rotations"], "d_scale": gr["scales"]}
-        mlp_ref.backward(p, c, out, gout, True, False)
+        torch.autograd.backward([d_xyz, d_rot, d_scale], [torch.from_numpy(gr[k]) for k in
+                                                          ("means3D", "rotations", "scales")])
         if it >= warmup:
             times.append(time.perf_counter() - t0)
     return dict(value=1.0 / float(np.median(times)), unit="iters/s", cores=threads, kind="port",
-                sample=f"median of {steps} timed full steps after {warmup} warm-up (SURVEY 8d's 3 + 20 reduced to keep "
-                       f"the CPU leg ~20 s) of synth-{N // 1000}k at {res}x{res}; float64 numpy MLP (BLAS threads="
-                       f"{threads}) + C raster oracle (OpenMP forward, serial backward) + torch-CPU SSIM")
+                cpu=_cpu_model(),
+                sample=f"median of {steps} timed full steps after {warmup} warm-up (SURVEY 8d protocol) of "
+                       f"synth-{N // 1000}k at {res}x{res} on {threads} threads of {_cpu_model()}: fp32 torch-CPU "
+                       f"DeformNetworkBaseline (the reference's forward, autograd backward) + C raster oracle "
+                       f"(OpenMP forward and backward) + torch-CPU L1/SSIM; no Adam",
+                median_s=float(np.median(times)), min_s=float(np.min(times)))
 
 
 def main():
@@ -263,7 +280,7 @@ def main():
     # the roofline candidates are timed on every 4th step (each timed launch adds two stream markers, ~6 us
     # of GPU idle each, inside the timed region); the other classes, when asked for, on every step. The
     # roofline reports the timed class with the longest average launch (the dominant kernel)
-    lib.dgs_timing_sample(4 if args.kernel_timing == "roofline" and args.steps >= 8 else 1)
+    lib.dgs_timing_sample(4 if args.kernel_timing == "roofline" and args.steps >= 8 else 1)  # (period below)
     lib.dgs_timing_enable(0 if args.kernel_timing == "none" else 1)
     if world > 1:
         dist.barrier()
@@ -296,19 +313,22 @@ def main():
     pair_cap = int(lib.dgs_debug_pair_cap(local))  # the speculative capacity the sort-path loops cover
     n_tiles = -(-R // 16) * -(-R // 16)
 
+    # per class: accumulated ms over the timed launches, how many were timed, how many ran (the
+    # roofline candidates are timed on every `period`-th launch)
+    period = 4 if args.kernel_timing == "roofline" and args.steps >= 8 else 1
     kernels = {}
     for name in KERNEL_CLASSES:
         n_l = _lib.I(0)
         ms = lib.dgs_timing_query(name.encode(), n_l)
         if n_l.value:
-            kernels[name] = (ms, n_l.value)
+            kernels[name] = (ms, n_l.value, int(lib.dgs_timing_launches(name.encode())))
     HW = R * R
     best = None
-    for name, (ms, n) in kernels.items():
+    for name, (ms, n, _) in kernels.items():
         info = kernel_algorithmic(name, N, P_pairs, HW, cap=pair_cap, T=n_tiles)
         if info is None:
             continue
-        if best is None or ms > best[1]:
+        if best is None or ms / n > best[1] / best[2]:  # the longest AVERAGE launch: the dominant kernel
             best = (name, ms, n, info)
     roofline = None
     if best:
@@ -361,7 +381,10 @@ def main():
                    "parallelism": f"dp{world} (frame-parallel, "
                    + ("RCCL" if world == 1 or dist.get_backend() == "nccl" else dist.get_backend()) + " grad all-reduce)"},
         "roofline": roofline,
-        "kernels_ms_per_step": {k: v[0] / args.steps for k, v in kernels.items()},
+        # average timed launch x launches per step (every launch ran, every `period`-th was timed)
+        "kernels_ms_per_step": {k: v[0] / v[1] * v[2] / args.steps for k, v in kernels.items()},
+        "kernel_timing": {"period": period, "timed_launches": {k: v[1] for k, v in kernels.items()},
+                          "launches": {k: v[2] for k, v in kernels.items()}},
         # host time per step: issuing forward + backward (including the wait for the pair count
         # inside it) and the optimizer step; a count wait near 0 means the host, not the GPU, paced it
         "host_ms_per_step": {"fwd_bwd": state["host_fb"] / args.steps * 1e3, "count_wait": wait_ms / args.steps,

@@ -72,7 +72,7 @@ ScopedTimer::ScopedTimer(const char *n, hipStream_t s) : name(n), stream(s), ev0
     std::lock_guard<std::mutex> lk(g_tmu);
     if (!g_timing_sel.empty() && !g_timing_sel.count(n)) return;
     // each event record is a stream marker (~6 us of GPU idle): sampled launches only
-    if (g_period > 1 && (g_seen[n]++ % g_period) != 0) return;
+    if ((g_seen[n]++ % g_period) != 0) return;
     hipEvent_t e = take_event();
     (void)hipEventRecord(e, stream);
     ev0 = (void *)e;
@@ -123,6 +123,12 @@ extern "C" double dgs_timing_query(const char *name, int *launches) {
     }
     if (launches) *launches = it->second.second;
     return it->second.first;
+}
+
+extern "C" long long dgs_timing_launches(const char *name) {
+    std::lock_guard<std::mutex> lk(dgs::g_tmu);
+    auto it = dgs::g_seen.find(name);
+    return it == dgs::g_seen.end() ? 0 : it->second;
 }
 
 extern "C" void dgs_timing_reset(void) {

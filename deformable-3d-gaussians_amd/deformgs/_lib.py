@@ -65,6 +65,7 @@ _SIGS = {
     "dgs_timing_reset": ([], None),
     "dgs_timing_select": ([ctypes.c_char_p], None),
     "dgs_timing_sample": ([I], None),
+    "dgs_timing_launches": ([ctypes.c_char_p], ctypes.c_longlong),
     "dgs_deform_num_params": ([I], I),
     "dgs_deform_packed_floats": ([I], SZ),
     "dgs_deform_saved_floats": ([I, I], SZ),

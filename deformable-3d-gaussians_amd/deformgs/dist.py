@@ -142,11 +142,16 @@ class OverlappedGradAllReduce:
             off += n
 
     def discard(self):
-        """Drop this step's reduction (the step is being redone): the early collective, if it was
-        started, is waited for (every rank issued it, so the communicator stays in step) and ignored;
-        call arm() again before the redone backward."""
-        if self._pending is not None:
-            self._pending[1].wait()
+        """Drop this step's reduction (the step is being redone). Every rank must have issued exactly
+        one early collective for the discarded backward before the redo issues its own: the early
+        collective this rank started is waited for and ignored; a rank whose hook never fired (some
+        early gradient stayed None) issues the same throwaway early reduction __call__ would, so it
+        pairs with the ranks whose hook did fire. Call arm() again before the redone backward."""
+        if self.world() > 1 and self._armed:
+            if self._pending is not None:
+                self._pending[1].wait()
+            else:
+                self._reduce(self._early)
         self._pending, self._armed = None, False
 
     def __call__(self):
@@ -180,15 +185,20 @@ class OverflowAgreement:
         if not dist.is_initialized() or dist.get_world_size(self.group) == 1:
             return bool(local_overflow)
         if self._gloo is None:
-            if dist.get_backend(self.group) == "gloo":
-                self._gloo = self.group
+            if os.environ.get("DGS_AGREE_BACKEND", "gloo") != "gloo":
+                self._gloo = False  # the device flag on the main group (the same env on every rank)
             else:
-                try:  # a host group beside RCCL; DGS_AGREE_BACKEND=default keeps the flag on the main group
-                    if os.environ.get("DGS_AGREE_BACKEND", "gloo") != "gloo":
-                        raise RuntimeError("host group disabled")
+                # a host group of its own, also when the main group is gloo: the flag then never
+                # interleaves with the gradient collectives (a rank whose early collective started
+                # and one whose did not still agree). new_group is collective: a rank that cannot
+                # create it fails here (no silent fallback to the main group, which would leave the
+                # ranks' 1-int all-reduces on different groups and deadlock the first deferred step)
+                try:
                     self._gloo = dist.new_group(backend="gloo")
-                except Exception:  # (same outcome on every rank: the group is created collectively)
-                    self._gloo = False
+                except Exception as e:
+                    raise RuntimeError("OverflowAgreement: could not create the gloo host group on this rank; "
+                                       "set DGS_AGREE_BACKEND=default on every rank to agree over the main "
+                                       "group instead") from e
         if self._gloo is False:  # a device flag on the main group (queues behind its collectives)
             dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
             flag = torch.tensor([1 if local_overflow else 0], dtype=torch.int32, device=dev)

@@ -35,8 +35,11 @@ def synth_gaussians(N, seed=0, device="cuda", sh_degree=3):
                 features_dc=t(f_dc), features_rest=t(f_rest))
 
 
-def synth_camera(width, height, index=0, fid=0.0, device="cuda"):
-    """Camera `index` of a ring of views around the origin (rank r renders view r)."""
-    az = 2.0 * math.pi * (index % 16) / 16.0
-    el = 0.25 * math.sin(0.7 * index)
+def synth_camera(width, height, index=0, fid=0.0, device="cuda", az=None, el=None):
+    """Camera `index` of a ring of views around the origin (rank r renders view r); `az` / `el`
+    (radians) place it explicitly instead."""
+    if az is None:
+        az = 2.0 * math.pi * (index % 16) / 16.0
+    if el is None:
+        el = 0.25 * math.sin(0.7 * index)
     return orbit_camera(az, el, DNERF_RADIUS, DNERF_FOV, width, height, fid=fid, data_device=device)

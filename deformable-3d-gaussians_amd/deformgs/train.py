@@ -215,16 +215,24 @@ def training(dataset, opt, pipe, testing_iterations, saving_iterations, scene, g
 
 class SyntheticScene:
     """Stand-in for scene.Scene (scene/__init__.py:23-112) on synthetic data (the D-NeRF / NeRF-DS
-    datasets are not available here): `n_train` train and `n_test` test cameras on the D-NeRF ring
-    with fids spread over [0, 1), each holding `original_image` = a render of a ground-truth
-    deformable model (synth Gaussians moving with a smooth per-Gaussian trajectory in t), so the loop
-    has a real target to converge to. cameras_extent = 1.1 x the largest camera distance from the
-    mean camera centre (dataset_readers.py:77-98 getNerfppNorm). init_gaussians(model) seeds the
-    trained model from a perturbed copy of the ground truth's positions (the reader's random point
-    cloud, dataset_readers.py:286-290, stands behind the same role)."""
+    datasets are not available here): `n_train` train and `n_test` test cameras around the object, each
+    holding `original_image` = a render of a ground-truth deformable model, so the loop has a real
+    target to converge to. cameras_extent = 1.1 x the largest camera distance from the mean camera
+    centre (dataset_readers.py:77-98 getNerfppNorm). init_gaussians(model) seeds the trained model from
+    a perturbed copy of the ground truth's positions (the reader's random point cloud,
+    dataset_readers.py:286-290, stands behind the same role).
 
-    def __init__(self, n_gaussians, width, height, n_train=30, n_test=5, seed=0, device="cuda", motion=0.08,
-                 white_background=False):
+    motion="smooth" (default): the ground truth deforms by a displacement FIELD that is smooth in
+    position and time, d(x, t) = a (sin(2 pi t + w x_y + p0), sin(2 pi t + w x_z + p1), sin(2 pi t + w
+    x_x + p2)) — a D-NeRF-like scene that a deformation network can learn and interpolate; "random":
+    every Gaussian follows its own random sinusoid (round-3 behaviour: memorisable per frame only).
+    interleave=True (default): train frames take fids k/n_train on the camera ring and every test
+    camera sits between two train cameras, at the midpoint of their azimuths and of their frame times,
+    so the test views measure interpolation in view and time (the D-NeRF split's held-out role);
+    False: test cameras continue the train ring (round-3 behaviour)."""
+
+    def __init__(self, n_gaussians, width, height, n_train=30, n_test=5, seed=0, device="cuda", motion="smooth",
+                 amplitude=0.08, white_background=False, interleave=True):
         from .arguments import PipelineParams as _PP
         from .gaussian_model import GaussianModel
         from .synthetic import synth_camera, synth_gaussians
@@ -234,15 +242,39 @@ class SyntheticScene:
         gt = GaussianModel(3)
         gt.from_tensors(g["xyz"], g["features_dc"], g["features_rest"], g["scaling"], g["rotation"], g["opacity"])
         rng = np.random.default_rng(seed + 100)
-        self.dirs = torch.tensor(rng.standard_normal((n_gaussians, 3)), dtype=torch.float32, device=device) * motion
-        self.phase = torch.tensor(rng.uniform(0, 2 * np.pi, (n_gaussians, 1)), dtype=torch.float32, device=device)
+        self.kind = motion
+        if motion == "random":
+            self.dirs = torch.tensor(rng.standard_normal((n_gaussians, 3)), dtype=torch.float32,
+                                     device=device) * amplitude
+            self.phase = torch.tensor(rng.uniform(0, 2 * np.pi, (n_gaussians, 1)), dtype=torch.float32, device=device)
+        elif motion == "smooth":
+            self.amp = float(amplitude)
+            self.freq = 2.0
+            self.phases = [float(v) for v in rng.uniform(0, 2 * np.pi, 3)]
+        else:
+            raise ValueError(motion)
         bg = torch.tensor([1.0, 1.0, 1.0] if white_background else [0.0, 0.0, 0.0], device=device)
         self.train, self.test = [], []
-        for k in range(n_train + n_test):
-            fid = (k * 0.618033988749895) % 1.0
-            cam = synth_camera(width, height, index=k, fid=fid, device=device)
+        specs = []
+        if interleave:
+            az = [2 * np.pi * k / n_train for k in range(n_train)]
+            el = [0.25 * np.sin(0.7 * k) for k in range(n_train)]
+            fids = [k / n_train for k in range(n_train)]
+            specs += [(az[k], el[k], fids[k]) for k in range(n_train)]
+            for j in range(n_test):
+                k = (j * n_train) // max(n_test, 1) + n_train // (2 * max(n_test, 1))
+                k1 = (k + 1) % n_train
+                specs.append((az[k] + np.pi / n_train, 0.5 * (el[k] + el[k1]), (k + 0.5) / n_train))
+        else:
+            for k in range(n_train + n_test):
+                specs.append((None, None, (k * 0.618033988749895) % 1.0, k))
+        for k, sp in enumerate(specs):
+            if interleave:
+                cam = synth_camera(width, height, fid=float(sp[2]), device=device, az=float(sp[0]), el=float(sp[1]))
+            else:
+                cam = synth_camera(width, height, index=sp[3], fid=sp[2], device=device)
             with torch.no_grad():
-                d_xyz = self.motion(fid)
+                d_xyz = self.motion(float(cam.fid))
                 img = render(cam, gt, _PP(), bg, d_xyz, 0.0, 0.0)["render"]
             cam.original_image = img.clamp(0.0, 1.0)
             (self.train if k < n_train else self.test).append(cam)
@@ -250,7 +282,13 @@ class SyntheticScene:
         self.cameras_extent = float(np.max(np.linalg.norm(centers - centers.mean(0), axis=1)) * 1.1)
 
     def motion(self, fid):
-        return self.dirs * torch.sin(2 * np.pi * fid + self.phase)
+        if self.kind == "random":
+            return self.dirs * torch.sin(2 * np.pi * fid + self.phase)
+        x = self.gt_tensors["xyz"]
+        w, p = self.freq, self.phases
+        ph = 2 * np.pi * fid
+        return self.amp * torch.stack([torch.sin(ph + w * x[:, 1] + p[0]), torch.sin(ph + w * x[:, 2] + p[1]),
+                                       torch.sin(ph + w * x[:, 0] + p[2])], 1)
 
     def getTrainCameras(self):
         return self.train

@@ -155,6 +155,8 @@ void dgs_timing_reset(void);
 /* Time only every `period`-th launch of each selected class (1 = every launch, the default): each
  * timed launch costs two stream markers, ~6 us of GPU idle each. */
 void dgs_timing_sample(int period);
+/* Launches of a selected class since the last reset, timed or not (timed = ceil(launches / period)). */
+long long dgs_timing_launches(const char *name);
 
 /* ---- deformation MLP (utils/time_utils.py:56-201), fused PE + 8x256 MLP ----
  * Default: fp32 GEMMs on bf16 MFMA over an exact hi/mid/lo operand split (six products per fp32

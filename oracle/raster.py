@@ -47,6 +47,9 @@ def lib():
         _lib.or_num_rendered.restype = ctypes.c_int
         _lib.or_geometry.argtypes = [P] * 6
         _lib.or_pixel_state.argtypes = [P] * 3
+        _lib.or_preprocess_raw.argtypes = [P] * 4
+        _lib.or_flip_flags.argtypes = [P, ctypes.c_float, P, P]
+        _lib.or_flip_flags.restype = ctypes.c_int
     return _lib
 
 
@@ -123,6 +126,24 @@ class OracleRaster:
         n = np.zeros((H, W), np.int32)
         lib().or_pixel_state(self._st, _ptr(T), _ptr(n))
         return T, n
+
+    def preprocess_raw(self):
+        """radf = 3 sqrt(lambda_max) (radius = ceil(radf)), vz = view-space z, pxy = pixel centre."""
+        N = self.N
+        radf = np.zeros((N,), np.float32)
+        vz = np.zeros((N,), np.float32)
+        pxy = np.zeros((N, 2), np.float32)
+        lib().or_preprocess_raw(self._st, _ptr(radf), _ptr(vz), _ptr(pxy))
+        return dict(radf=radf, vz=vz, pxy=pxy)
+
+    def flip_flags(self, eps):
+        """(per-Gaussian flags, per-pixel flags) of blend decisions within relative eps of their
+        threshold (raster_ref.c or_flip_flags)."""
+        H, W = self.s.image_height, self.s.image_width
+        g = np.zeros((self.N,), np.uint8)
+        px = np.zeros((H, W), np.uint8)
+        lib().or_flip_flags(self._st, float(eps), _ptr(g), _ptr(px))
+        return g.astype(bool), px.astype(bool)
 
     def backward(self, dL_dcolor, dL_ddepth=None):
         N, M = self.N, self.M

@@ -63,6 +63,7 @@ typedef struct {
     float *means3D, *shs, *colors_in, *opac, *scales, *rots, *cov_in;
     /* per-Gaussian geometry */
     float *depth, *xy, *conic_o, *rgb, *cov3D;
+    float *radf, *vz, *pxy; /* 3 sqrt(lambda_max) before the ceil; view-space z; pixel centre */
     int *radii, *tiles;
     uint8_t *clamped;
     /* binning */
@@ -210,6 +211,9 @@ int or_forward(const ORSettings *s, int N, int M, const float *means3D, const fl
     st->radii = (int *)calloc(N, sizeof(int));
     st->tiles = (int *)calloc(N, sizeof(int));
     st->clamped = (uint8_t *)calloc((size_t)N * 3, 1);
+    st->radf = (float *)calloc(N, sizeof(float));
+    st->vz = (float *)calloc(N, sizeof(float));
+    st->pxy = (float *)calloc((size_t)N * 2, sizeof(float));
 
     const float fx = W / (2.f * s->tanfovx), fy = H / (2.f * s->tanfovy);
 #pragma omp parallel for schedule(static)
@@ -217,6 +221,7 @@ int or_forward(const ORSettings *s, int N, int M, const float *means3D, const fl
         const float *p = st->means3D + 3 * i;
         float pv[3];
         xform43(s->viewmatrix, p, pv);
+        st->vz[i] = pv[2];
         if (pv[2] <= 0.2f) continue;
         float *cov = st->cov3D + 6 * i;
         if (st->cov_in)
@@ -232,12 +237,15 @@ int or_forward(const ORSettings *s, int N, int M, const float *means3D, const fl
         float mid = 0.5f * (c2[0] + c2[2]);
         float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
         float l2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
-        int rad = (int)ceilf(3.f * sqrtf(fmaxf(l1, l2)));
+        st->radf[i] = 3.f * sqrtf(fmaxf(l1, l2));
+        int rad = (int)ceilf(st->radf[i]);
         float ph[4];
         xform44(s->projmatrix, p, ph);
         float pw = 1.f / (ph[3] + 0.0000001f);
         float px = ((ph[0] * pw + 1.f) * W - 1.f) * 0.5f;
         float py = ((ph[1] * pw + 1.f) * H - 1.f) * 0.5f;
+        st->pxy[2 * i] = px; /* also for Gaussians culled by an empty rect (tests: rect margins) */
+        st->pxy[2 * i + 1] = py;
         int rminx = (int)fminf(st->grid_x, fmaxf(0, (int)((px - rad) / BX)));
         int rminy = (int)fminf(st->grid_y, fmaxf(0, (int)((py - rad) / BY)));
         int rmaxx = (int)fminf(st->grid_x, fmaxf(0, (int)((px + rad + BX - 1) / BX)));
@@ -377,16 +385,20 @@ int or_backward(void *p, const float *dL_dpix, const float *dL_ddepth, float *dL
     const ORSettings *s = &st->s;
     const int N = st->N, M = st->M, H = s->image_height, W = s->image_width;
     const int T = st->grid_x * st->grid_y;
-    /* per-Gaussian accumulators (render backward) */
-    float *g_m2 = (float *)calloc((size_t)N * 2, sizeof(float));
-    float *g_dens = (float *)calloc((size_t)N * 2, sizeof(float));
-    float *g_con = (float *)calloc((size_t)N * 3, sizeof(float));
-    float *g_op = (float *)calloc(N, sizeof(float));
-    float *g_col = (float *)calloc((size_t)N * 3, sizeof(float));
-    float *g_dep = (float *)calloc(N, sizeof(float));
+    /* per-Gaussian accumulators (render backward). The tiles are split into NCH fixed contiguous
+       chunks, each with its own accumulators, summed per Gaussian in chunk order afterwards: the float
+       sums depend on (N, tiles) only, never on the thread count, so the result is reproducible and the
+       chunks run in parallel (OpenMP). */
+    enum { NF = 12 }; /* m2 xy, |m2| xy, conic xyz, opacity, rgb, depth */
+    int NCH = T < 32 ? (T > 0 ? T : 1) : 32;
+    while (NCH > 1 && (size_t)NCH * N * NF * sizeof(float) > ((size_t)768 << 20)) NCH /= 2;
+    float *chunk_acc = (float *)calloc((size_t)NCH * N * NF + 1, sizeof(float));
     const float hx = 0.5f * W, hy = 0.5f * H;
-    /* serial over tiles so the float sums are reproducible */
-    for (int t = 0; t < T; t++) {
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int ch = 0; ch < NCH; ch++) {
+        float *A = chunk_acc + (size_t)ch * N * NF;
+        const int t_lo = (int)((long long)T * ch / NCH), t_hi = (int)((long long)T * (ch + 1) / NCH);
+        for (int t = t_lo; t < t_hi; t++) {
         int tx = t % st->grid_x, ty = t / st->grid_x;
         for (int ly = 0; ly < BY; ly++)
             for (int lx = 0; lx < BX; lx++) {
@@ -406,6 +418,7 @@ int or_backward(void *p, const float *dL_dpix, const float *dL_ddepth, float *dL
                 int lo = st->range_lo[t];
                 for (int j = lo + last - 1; j >= lo; j--) {
                     int g = st->vals[j];
+                    float *a = A + (size_t)g * NF;
                     float dx = st->xy[2 * g] - pfx, dy = st->xy[2 * g + 1] - pfy;
                     const float *co = st->conic_o + 4 * g;
                     float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
@@ -421,13 +434,13 @@ int or_backward(void *p, const float *dL_dpix, const float *dL_ddepth, float *dL
                         acc[c] = last_alpha * lastc[c] + (1.f - last_alpha) * acc[c];
                         lastc[c] = col;
                         dL_dalpha += (col - acc[c]) * dpix[c];
-                        g_col[3 * g + c] += dchdcol * dpix[c];
+                        a[8 + c] += dchdcol * dpix[c];
                     }
                     float dg = st->depth[g];
                     accd = last_alpha * lastd + (1.f - last_alpha) * accd;
                     lastd = dg;
                     dL_dalpha += (dg - accd) * ddep;
-                    g_dep[g] += dchdcol * ddep;
+                    a[11] += dchdcol * ddep;
                     dL_dalpha *= Tt;
                     last_alpha = alpha;
                     dL_dalpha += (-Tfinal / (1.f - alpha)) * bgdot;
@@ -438,17 +451,39 @@ int or_backward(void *p, const float *dL_dpix, const float *dL_ddepth, float *dL
                     float dGdx = -gdx * co[0] - gdy * co[1];
                     float dGdy = -gdy * co[2] - gdx * co[1];
                     float gmx = dL_dG * dGdx * hx, gmy = dL_dG * dGdy * hy;
-                    g_m2[2 * g] += gmx;
-                    g_m2[2 * g + 1] += gmy;
-                    g_dens[2 * g] += fabsf(gmx);
-                    g_dens[2 * g + 1] += fabsf(gmy);
-                    g_con[3 * g] += -0.5f * gdx * dx * dL_dG;
-                    g_con[3 * g + 1] += -0.5f * gdx * dy * dL_dG;
-                    g_con[3 * g + 2] += -0.5f * gdy * dy * dL_dG;
-                    g_op[g] += G * dL_dalpha;
+                    a[0] += gmx;
+                    a[1] += gmy;
+                    a[2] += fabsf(gmx);
+                    a[3] += fabsf(gmy);
+                    a[4] += -0.5f * gdx * dx * dL_dG;
+                    a[5] += -0.5f * gdx * dy * dL_dG;
+                    a[6] += -0.5f * gdy * dy * dL_dG;
+                    a[7] += G * dL_dalpha;
                 }
             }
+        }
     }
+    float *g_m2 = (float *)calloc((size_t)N * 2 + 1, sizeof(float));
+    float *g_dens = (float *)calloc((size_t)N * 2 + 1, sizeof(float));
+    float *g_con = (float *)calloc((size_t)N * 3 + 1, sizeof(float));
+    float *g_op = (float *)calloc((size_t)N + 1, sizeof(float));
+    float *g_col = (float *)calloc((size_t)N * 3 + 1, sizeof(float));
+    float *g_dep = (float *)calloc((size_t)N + 1, sizeof(float));
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < N; i++) {
+        float r[NF] = {0};
+        for (int ch = 0; ch < NCH; ch++) {
+            const float *a = chunk_acc + ((size_t)ch * N + i) * NF;
+            for (int k = 0; k < NF; k++) r[k] += a[k];
+        }
+        g_m2[2 * i] = r[0]; g_m2[2 * i + 1] = r[1];
+        g_dens[2 * i] = r[2]; g_dens[2 * i + 1] = r[3];
+        g_con[3 * i] = r[4]; g_con[3 * i + 1] = r[5]; g_con[3 * i + 2] = r[6];
+        g_op[i] = r[7];
+        g_col[3 * i] = r[8]; g_col[3 * i + 1] = r[9]; g_col[3 * i + 2] = r[10];
+        g_dep[i] = r[11];
+    }
+    free(chunk_acc);
     const float fx = W / (2.f * s->tanfovx), fy = H / (2.f * s->tanfovy);
     memset(dL_dmeans3D, 0, sizeof(float) * 3 * N);
     if (dL_dshs) memset(dL_dshs, 0, sizeof(float) * 3 * M * N);
@@ -465,6 +500,7 @@ int or_backward(void *p, const float *dL_dpix, const float *dL_ddepth, float *dL
         dL_dopac[i] = g_op[i];
         if (dL_dcolors) for (int c = 0; c < 3; c++) dL_dcolors[3 * i + c] = g_col[3 * i + c];
     }
+#pragma omp parallel for schedule(static)
     for (int i = 0; i < N; i++) {
         if (st->radii[i] <= 0) continue;
         const float *pm = st->means3D + 3 * i;
@@ -681,7 +717,7 @@ void or_free(void *p) {
     free(st->rots); free(st->cov_in); free(st->depth); free(st->xy); free(st->conic_o);
     free(st->rgb); free(st->cov3D); free(st->radii); free(st->tiles); free(st->clamped);
     free(st->keys); free(st->vals); free(st->range_lo); free(st->range_hi); free(st->final_T);
-    free(st->n_contrib);
+    free(st->n_contrib); free(st->radf); free(st->vz); free(st->pxy);
     free(st);
 }
 
@@ -701,4 +737,80 @@ void or_pixel_state(void *p, float *final_T, int *n_contrib) {
     size_t n = (size_t)st->s.image_height * st->s.image_width;
     if (final_T) memcpy(final_T, st->final_T, sizeof(float) * n);
     if (n_contrib) memcpy(n_contrib, st->n_contrib, sizeof(int) * n);
+}
+
+/* Per-Gaussian preprocess values behind the integer outputs (tests): radf = 3 sqrt(lambda_max)
+   before the ceil (radius = ceil(radf)), vz = view-space z (culled at <= 0.2), pxy = pixel centre
+   (also for Gaussians whose tile rectangle came out empty). 0 where the Gaussian was culled earlier. */
+void or_preprocess_raw(void *p, float *radf, float *vz, float *pxy) {
+    ORState *st = (ORState *)p;
+    int N = st->N;
+    if (radf) memcpy(radf, st->radf, sizeof(float) * N);
+    if (vz) memcpy(vz, st->vz, sizeof(float) * N);
+    if (pxy) memcpy(pxy, st->pxy, sizeof(float) * 2 * N);
+}
+
+/* Near-threshold decisions of the blend (tests). Replays every pixel's front-to-back loop and marks
+   the discrete decisions whose input sits within a relative `eps` of its threshold, where two fp32
+   implementations of the same math (another exp, fma contraction, exponent-form conic) may decide
+   differently: the power > 0 skip (|power| <= eps), the alpha < 1/255 skip (|alpha - 1/255| <=
+   eps/255), the alpha clamp at 0.99 (|o G - 0.99| <= 0.99 eps) and the T (1 - alpha) < 1e-4 stop
+   (|T (1 - alpha) - 1e-4| <= 1e-4 eps). Such a decision changes the transmittance of everything
+   behind it in that pixel (and whether the pixel stops there), so pflag[pixel] = 1 and every
+   Gaussian listed in that pixel from the first such decision through one past the stop gets
+   gflag = 1 (the Gaussians whose gradient from that pixel can differ by more than rounding).
+   Returns the number of flagged pixels. */
+int or_flip_flags(void *p, float eps, uint8_t *gflag, uint8_t *pflag) {
+    ORState *st = (ORState *)p;
+    const int H = st->s.image_height, W = st->s.image_width;
+    const int T = st->grid_x * st->grid_y;
+    memset(gflag, 0, (size_t)st->N);
+    if (pflag) memset(pflag, 0, (size_t)H * W);
+    int flagged = 0;
+#pragma omp parallel for schedule(dynamic, 4) reduction(+ : flagged)
+    for (int t = 0; t < T; t++) {
+        int tx = t % st->grid_x, ty = t / st->grid_x;
+        const int lo = st->range_lo[t], hi = st->range_hi[t];
+        for (int ly = 0; ly < BY; ly++)
+            for (int lx = 0; lx < BX; lx++) {
+                int px = tx * BX + lx, py = ty * BY + ly;
+                if (px >= W || py >= H) continue;
+                float pfx = (float)px, pfy = (float)py;
+                float Tt = 1.f;
+                int first = -1, stop = hi - 1;
+                for (int j = lo; j < hi; j++) {
+                    int g = st->vals[j];
+                    float dx = st->xy[2 * g] - pfx, dy = st->xy[2 * g + 1] - pfy;
+                    const float *co = st->conic_o + 4 * g;
+                    float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                    int near = fabsf(power) <= eps;
+                    if (power > 0.f) {
+                        if (near && first < 0) first = j;
+                        continue;
+                    }
+                    float og = co[3] * expf(power);
+                    float alpha = fminf(0.99f, og);
+                    near |= fabsf(alpha - 1.f / 255.f) <= eps / 255.f;
+                    near |= fabsf(og - 0.99f) <= 0.99f * eps;
+                    if (alpha < 1.f / 255.f) {
+                        if (near && first < 0) first = j;
+                        continue;
+                    }
+                    float testT = Tt * (1.f - alpha);
+                    near |= fabsf(testT - 0.0001f) <= 0.0001f * eps;
+                    if (near && first < 0) first = j;
+                    if (testT < 0.0001f) {
+                        stop = j;
+                        break;
+                    }
+                    Tt = testT;
+                }
+                if (first < 0) continue;
+                flagged++;
+                if (pflag) pflag[py * W + px] = 1;
+                int end = stop + 1 < hi ? stop + 1 : hi - 1;
+                for (int j = first; j <= end; j++) gflag[st->vals[j]] = 1; /* benign race: all write 1 */
+            }
+    }
+    return flagged;
 }

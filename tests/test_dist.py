@@ -235,3 +235,48 @@ def test_viewpoint_stack_matches_reference_formula():
     # more frames asked for than exist: indices repeat, as upstream
     st2 = build_viewpoint_stack(cams[:5], 9)
     assert len(st2) == 9 and len({id(c) for c in st2}) == 5
+
+
+def _agreement_uneven_case(rank, world):
+    """The discarded step: on rank 1 the early parameter b gets no gradient, so its hook group never
+    completes there and no early collective starts; discard() must issue the throwaway early
+    reduction on rank 1 to pair with rank 0's, then the redone step reduces normally."""
+    from deformgs.dist import OverflowAgreement
+    agree = OverflowAgreement()
+    a = torch.nn.Parameter(torch.zeros(4))
+    b = torch.nn.Parameter(torch.zeros(3))
+    c = torch.nn.Parameter(torch.zeros(2))
+    ar = OverlappedGradAllReduce(lambda: [a, b], lambda: [c])
+    ar.arm()
+    loss = ((rank + 1.0) * 100 * a).sum()
+    if rank == 0:
+        loss = loss + (7.0 * b).sum()
+    loss.backward()
+    started = ar._pending is not None
+    assert agree(rank == 0)
+    ar.discard()
+    for p in (a, b, c):
+        p.grad = None
+    ar.arm()
+    ((rank + 1.0) * a).sum().backward()
+    ((rank + 1.0) * 2 * b).sum().backward()
+    (c * (rank + 1.0)).sum().backward()
+    ar()
+    # one more plain step: collectives still paired
+    for p in (a, b, c):
+        p.grad = None
+    ar.arm()
+    ((rank + 1.0) * (a.sum() + b.sum())).backward()
+    (c * 3.0).sum().backward()
+    ar()
+    return started, a.grad.clone(), b.grad.clone(), c.grad.clone()
+
+
+def test_overflow_discard_when_one_rank_missed_the_early_hook():
+    out = _run(_agreement_uneven_case)
+    assert out[0][0] and not out[1][0]
+    for rank in (0, 1):
+        _, ag, bg, cg = out[rank]
+        torch.testing.assert_close(ag, torch.full((4,), 1.5))
+        torch.testing.assert_close(bg, torch.full((3,), 1.5))
+        torch.testing.assert_close(cg, torch.full((2,), 3.0))

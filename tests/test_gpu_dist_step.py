@@ -77,3 +77,44 @@ def test_two_rank_step_averages_gradients(tmp_path, mode):
         assert bool(((a - want).abs() <= tol).all()), (i, float((a - want).abs().max()))
     for i, (a, b) in enumerate(zip(r0["params"], r1["params"])):
         assert torch.equal(a, b), f"parameter {i} differs between ranks after Adam"
+
+
+@pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")
+@pytest.mark.parametrize("variant", ["blender", "nonblender"])
+def test_two_rank_loop_stays_replicated_through_densification(tmp_path, variant):
+    """The training LOOP (deformgs/train.py training(), train_baseline.py:56-182) with 2 ranks on the one
+    GPU (gloo): 34 iterations across the warm-up boundary, three densify_and_prune calls, an opacity
+    reset and the stack refill (tests/dist_loop_worker.py). Replicas must stay IDENTICAL (SURVEY.md
+    §8e): at every densify / reset iteration and at the end, the Gaussian count and every Gaussian and
+    network parameter are bitwise equal on both ranks (the per-rank densification statistics are summed /
+    maxed across ranks right before densify_and_prune, and the split noise is rank-identical). The loop must actually densify (the count changes)."""
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), DGS_DEVICE="0", DGS_DIST_BACKEND="gloo")
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "dist_loop_worker.py"), str(tmp_path),
+                                       variant], env=env, cwd=ROOT))
+    rcs = []
+    for p in procs:
+        try:
+            rcs.append(p.wait(timeout=110))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            rcs.append(-9)
+    assert rcs == [0, 0], rcs
+    r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
+    assert r0["n"] == r1["n"], (r0["n"], r1["n"])
+    n = r0["n"]
+    assert n[9] != n[8], "the first densify_and_prune (iteration 10) must change the count"
+    assert r0["expiries"] == 0 and r1["expiries"] == 0
+    for it in sorted(r0["snaps"]):
+        a, b = r0["snaps"][it], r1["snaps"][it]
+        assert a["n"] == b["n"], it
+        for i, (x, y) in enumerate(zip(a["params"], b["params"])):
+            assert torch.equal(x, y), f"iteration {it}: parameter {i} differs between ranks"
+    for i, (x, y) in enumerate(zip(r0["end"]["params"], r1["end"]["params"])):
+        assert torch.equal(x, y), f"end: parameter {i} differs between ranks"
+    # the ranks rendered different frames: their local losses differ (the test is not vacuous)
+    assert r0["loss"] != r1["loss"]

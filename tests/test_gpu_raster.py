@@ -11,7 +11,8 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import frac_close, oracle_run, rel_err, scene, settings_for_gpu
+from helpers import (check_gaussian_grad, check_image, check_integer_outputs, frac_close, oracle_run, rel_err, scene,
+                     settings_for_gpu, tail_flags, write_stats)
 
 pytestmark = pytest.mark.gpu
 
@@ -53,6 +54,7 @@ def _run_gpu(inputs, rs, dcolor, ddepth, use_cov=False, use_colors=False, requir
         kw["scales"] = t["scales"]
         kw["rotations"] = t["rotations"]
     color, radii, depth = r(**kw)
+    _run_gpu.num_rendered = int(color.grad_fn.num_rendered)
     loss = (color * torch.tensor(dcolor, device=dev)).sum()
     if ddepth is not None:
         loss = loss + (depth * torch.tensor(ddepth, device=dev)).sum()
@@ -63,16 +65,24 @@ def _run_gpu(inputs, rs, dcolor, ddepth, use_cov=False, use_colors=False, requir
     return color.detach().cpu().numpy(), radii.cpu().numpy(), depth.detach().cpu().numpy(), grads
 
 
-def _check(o, g, color, radii, depth, grads, keys):
-    assert (radii == o.radii).mean() >= 0.9999, "radii must match the oracle (integer output)"
-    err = np.abs(color - o.color)
-    assert err.mean() <= 1e-5, f"image mean abs err {err.mean()}"
-    assert (err <= 1e-4).mean() >= 0.999
-    derr = np.abs(depth - o.depth)
-    assert (derr <= 1e-4 * max(1.0, np.abs(o.depth).max())).mean() >= 0.999
-    for k, ok in keys:
-        a, b = grads[k].reshape(-1), g[ok].reshape(-1)
-        assert frac_close(a, b, atol=2e-3 * np.abs(b).max(), rtol=1e-3) >= 0.995, (k, rel_err(a, b))
+def _check(o, g, color, radii, depth, grads, keys, nr=None, tag=None):
+    """radii exact and num_rendered equal to the oracle's (up to fp32-ambiguous ceil / rect / cull
+    decisions, helpers.check_integer_outputs); image mean |err| <= 1e-5 and >= 99.9 % within 1e-4,
+    every larger error at a pixel with a near-threshold blend decision; gradients >= 99.5 % within
+    2e-3 of the max + 1e-3 relative, every element outside that on a Gaussian with a near-threshold
+    decision (helpers.tail_flags)."""
+    stats = {}
+    try:
+        amb = check_integer_outputs(o, radii, nr, stats)
+        gflag, pflag = tail_flags(o, amb)
+        check_image(color, o, pflag, stats)
+        derr = np.abs(depth - o.depth)
+        assert (derr <= 1e-4 * max(1.0, np.abs(o.depth).max())).mean() >= 0.999
+        for k, ok in keys:
+            check_gaussian_grad(grads[k], g[ok], gflag, k, stats)
+    finally:
+        if tag:
+            write_stats(tag, stats)
 
 
 @pytest.mark.parametrize("cfg", CONFIGS)
@@ -86,7 +96,8 @@ def test_raster_sh_scale_rot(cfg, binning):
     color, radii, depth, grads = _run_gpu(inputs, rs, dcolor, ddepth)
     _check(o, g, color, radii, depth, grads,
            [("means3D", "means3D"), ("shs", "shs"), ("opacities", "opacities"), ("scales", "scales"),
-            ("rotations", "rotations"), ("means2D", "means2D"), ("means2D_densify", "means2D_densify")])
+            ("rotations", "rotations"), ("means2D", "means2D"), ("means2D_densify", "means2D_densify")],
+           nr=_run_gpu.num_rendered, tag=f"raster_sh_scale_rot[{N}x{H}x{W},{binning}]")
 
 
 def test_raster_precomputed_colors_and_cov():
@@ -102,7 +113,8 @@ def test_raster_precomputed_colors_and_cov():
     o, g = oracle_run(inputs, rs, dcolor, None, use_cov=True, use_colors=True)
     color, radii, depth, grads = _run_gpu(sub, rs, dcolor, None, use_cov=True, use_colors=True)
     _check(o, g, color, radii, depth, grads,
-           [("means3D", "means3D"), ("opacities", "opacities"), ("cov3D", "cov3D"), ("colors", "colors")])
+           [("means3D", "means3D"), ("opacities", "opacities"), ("cov3D", "cov3D"), ("colors", "colors")],
+           nr=_run_gpu.num_rendered, tag="raster_precomputed")
 
 
 def test_raster_sh_degrees():
@@ -112,7 +124,8 @@ def test_raster_sh_degrees():
         dcolor = rng.standard_normal((3, 64, 64)).astype(np.float32)
         o, g = oracle_run(inputs, rs, dcolor, None)
         color, radii, depth, grads = _run_gpu(inputs, rs, dcolor, None)
-        _check(o, g, color, radii, depth, grads, [("shs", "shs"), ("means3D", "means3D")])
+        _check(o, g, color, radii, depth, grads, [("shs", "shs"), ("means3D", "means3D")], nr=_run_gpu.num_rendered,
+               tag=f"raster_sh_degree{deg}")
 
 
 def test_raster_edge_cases():
