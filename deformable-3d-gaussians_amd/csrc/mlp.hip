@@ -661,11 +661,7 @@ struct MaskPre {
     const uint32_t *words;  // &mask[block][mrow0 + n0]: 64 u16, one per lane
     int lane;
     __device__ void operator()() const {
-#ifdef DGS_DIAG_NO_MASK  // timing experiment only: masks all-ones, no loads (wrong gradients)
-        mk->w = 0xffffu;
-#else
         mk->w = reinterpret_cast<const unsigned short *>(words)[lane];
-#endif
     }
 };
 

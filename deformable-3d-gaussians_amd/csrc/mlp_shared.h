@@ -290,9 +290,7 @@ __device__ inline void mask_apply(V &acc, uint32_t bits) {
 // kernels reads global memory another wave of the block wrote.
 __device__ inline void lds_barrier() {
     __builtin_amdgcn_s_waitcnt(0xc07f);  // gfx9 encoding: vmcnt 63, expcnt 7, lgkmcnt 0
-#ifndef DGS_DIAG_NO_BARRIER  // timing experiment only (races: wrong results)
     __builtin_amdgcn_s_barrier();
-#endif
 }
 
 // A wave's 32-row tile of a feature-major [rows][Ns] array, addressed through a buffer descriptor

@@ -274,11 +274,7 @@ __device__ inline void gemm(const bf16x8 *__restrict__ Aw, const bf16x8 *lds, in
     const int kq = lane >> 4, col = lane & 15;
     const bf16x8 *Ap = Aw + lane;
     const bf16x8 *Bp = lds + (g0 + kq) * UG + 16 * q0 + col;
-#ifdef DGS_DIAG_A_STATIC  // timing experiment only (wrong results): every k-step re-reads k-step 0's A
-    constexpr int AK = 0;
-#else
     constexpr int AK = KSLOT;
-#endif
     constexpr int BK = KG * UG;
     auto bofs = [](int k) { return (k + (k >= SKIP ? 1 : 0)) * BK; };  // compile-time per unrolled k
     constexpr int RING = 2;
@@ -514,14 +510,6 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
     const int r = __builtin_amdgcn_readfirstlane(tid >> 6);  // n-tile of this wave (provably uniform)
     const int kq = lane >> 4, col = lane & 15;
     const int pend = min(a.N, p0 + BMB);  // real points of the block: [p0, pend)
-#ifdef DGS_DIAG_PRIO  // experiment: static priority for the last-dispatched wave of each SIMD
-    if (r >= 12) __builtin_amdgcn_s_setprio(1);
-#endif
-#ifdef DGS_DIAG_PRIO2  // experiment: graded priority by dispatch order within a SIMD
-    if (r >= 12) __builtin_amdgcn_s_setprio(3);
-    else if (r >= 8) __builtin_amdgcn_s_setprio(2);
-    else if (r >= 4) __builtin_amdgcn_s_setprio(1);
-#endif
     const Flags F = make_flags(a.flags);
     const size_t Ns = a.Ns;
     const __amdgpu_buffer_rsrc_t mrsrc = __builtin_amdgcn_make_buffer_rsrc(
@@ -668,15 +656,6 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
         using PreT = NoPre;
         const PreT bp{};
         const HGate hg{hwr, hrd, L == 5 ? (fold ? 2 : 3) : 0, 2u * L, true, lane};
-#if defined(DGS_DIAG_GPRIO)  // experiment: issue priority by dispatch age during the GEMM only (younger = higher)
-        if (DGS_DIAG_GPRIO == 1) {
-            if (r >= 12) __builtin_amdgcn_s_setprio(1);
-        } else {
-            if (r >= 12) __builtin_amdgcn_s_setprio(3);
-            else if (r >= 8) __builtin_amdgcn_s_setprio(2);
-            else if (r >= 4) __builtin_amdgcn_s_setprio(1);
-        }
-#endif
         if (L == 0) {
             if constexpr (FOLD) gemm<2, NQB>(Aw, lds, g0, 0, lane, c, bp);  // XE only
             else gemm<3, NQB>(Aw, lds, g0, 0, lane, c, bp);                 // XE | TE
@@ -686,16 +665,9 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
         } else {
             gemm<8, NQB>(Aw, lds, g0, 0, lane, c, bp, hg);
         }
-#if defined(DGS_DIAG_GPRIO)
-        __builtin_amdgcn_s_setprio(0);
-#endif
         bv = sb[64 * L + 4 * r + kq];
         DGS_STAMP(4 + 2 * L);
         DGS_WSTAMP(22, L);  // per wave: GEMM end (layer 3)
-#ifdef DGS_DIAG_EPI_PRIO  // experiment: raised issue priority through the epilogue
-        __builtin_amdgcn_s_setprio(2);
-#endif
-#ifndef DGS_DIAG_NO_EPI  // timing experiment only (wrong results): no bias/relu/mask/split/store epilogue
         bias_relu(c, bv, true);
         if (SAVE) {
             store_mask(relu_bits(c), 16 * L + r);
@@ -703,17 +675,11 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
         }
         if (L == 3 && r == 0) DGS_STAMP(54);
         // this wave's rows are H k-step r / 2: every wave must have read it in this layer
-#ifndef DGS_DIAG_NO_WAR  // timing experiment only (races): no wait for the readers of the overwritten k-step
         if (L > 0) lds_wait_ge(hrd + (r >> 1), 16u * L, lds_peek(hrd + (r >> 1)));
-#endif
         if (L == 3 && r == 0) DGS_STAMP(56);
 #pragma unroll
         for (int q = 0; q < NQB; q++) acc_to_lds(c[q], lds, G_H, r, q, lane);
-#endif
         lds_signal(hwr + (r >> 1), lane);
-#ifdef DGS_DIAG_EPI_PRIO
-        __builtin_amdgcn_s_setprio(0);
-#endif
         if (L == 3 && r == 0) DGS_STAMP(55);
         DGS_STAMP(5 + 2 * L);
     }
@@ -1399,11 +1365,7 @@ __global__ __launch_bounds__(DW_THREADS) void k_dwg(WJobs JT, size_t Ns, const f
 // Same job plan, slab layout and k_dw_reduce as the fp32 k_dw.
 // ------------------------------------------------------------------------------------------------
 constexpr int S_UNITS = NSPLIT * 2 * 8 * 64;  // 16-B units per chunk buffer
-#ifdef DGS_DWS_GATE
-constexpr int S_NBUF = 3;  // chunk buffers: barrier-free hand-off (a wave may run a chunk ahead)
-#else
 constexpr int S_NBUF = 2;
-#endif
 constexpr int S_LDS = S_NBUF * S_UNITS * 16;  // bytes (96 / 144 KiB)
 static_assert(S_LDS <= 160 * 1024, "dWs LDS");
 
@@ -1431,14 +1393,7 @@ __device__ __forceinline__ f32x16 mma6_into(const AFrag &a, const AFrag &b, f32x
 }
 
 // acc += t (v_pk_add_f32 or v_add_f32: measured alike here)
-#ifdef DGS_ADD16_SCALAR
-__device__ __forceinline__ void add16(f32x16 &acc, const f32x16 &t) {
-#pragma unroll
-    for (int r = 0; r < 16; r++) acc[r] = acc[r] + t[r];
-}
-#else
 __device__ __forceinline__ void add16(f32x16 &acc, const f32x16 &t) { acc += t; }
-#endif
 
 template <bool COL, int NS>
 __device__ __forceinline__ void dws_run(const WJob &J, size_t Ns, const float *__restrict__ dz,
@@ -1464,11 +1419,7 @@ __device__ __forceinline__ void dws_run(const WJob &J, size_t Ns, const float *_
     // private: lane (i, h) holds row 32 w + i, points 8 h .. + 7 of each k-step (fragment layout)
     const int pvoff = ((32 * wave + i) * (int)Ns + 8 * h) * 4;
     float4 pr[4];  // [k-step][half]
-#ifdef DGS_DWS_L2  // timing experiment only (wrong results): every chunk re-reads chunks 0 / 1 (cache-resident)
-#define DWS_C(c) ((c) & 1)
-#else
 #define DWS_C(c) (c)
-#endif
     auto pload = [&](int c) {
 #pragma unroll
         for (int q = 0; q < 4; q++)
@@ -1514,16 +1465,6 @@ __device__ __forceinline__ void dws_run(const WJob &J, size_t Ns, const float *_
     for (int s = 0; s < NS; s++)
 #pragma unroll
         for (int r = 0; r < 16; r++) acc[s][r] = 0.f;
-#ifdef DGS_DWS_GATE
-    // hand-off counters (monotonic per buffer b): cwr[b] = wave-splits written into b, crd[b] =
-    // wave-reads of b finished; chunk jj (from c0) lives in buffer jj % 3
-    __shared__ uint32_t cwr[S_NBUF], crd[S_NBUF];
-    if (tid < S_NBUF) {
-        cwr[tid] = 0;
-        crd[tid] = 0;
-    }
-    __syncthreads();
-#endif
     if (c0 < c1) {
         sload(c0);
         pload(c0);
@@ -1531,64 +1472,11 @@ __device__ __forceinline__ void dws_run(const WJob &J, size_t Ns, const float *_
         for (int f = 0; f < NSF; f++) sput(f, 0, true);
         sload(min(c0 + 1, c1 - 1));
     }
-#ifdef DGS_DWS_GATE
-    lds_signal(cwr, lane);
-#else
     lds_barrier();
-#endif
     // shared float4 f of the next chunk is split after tile put_at(f) of this one (within the first
     // half of the tiles), then the loads of the chunk after are issued
     constexpr int NH = (NS + 1) / 2;
     auto put_at = [](int f) { return (f * NH) / NSF; };
-#ifdef DGS_DWS_GATE
-    // No workgroup barrier per chunk: a wave reads chunk jj's buffer once all 8 waves have written
-    // their part of it (cwr), and overwrites the buffer of chunk jj - 2 with chunk jj + 1 once all 8
-    // have finished reading it (crd). The two waves of a SIMD drift apart instead of meeting at a
-    // barrier, so one wave's private split (VALU, before its first MFMA) runs beside the other's
-    // MFMAs. LDS operations of a wave complete in issue order: a signal after the writes / reads.
-    auto chunk = [&](int c, auto BUFC) {
-        constexpr int buf = decltype(BUFC)::value;
-        constexpr int nbuf = (buf + 1) % S_NBUF;
-        const int jj = c - c0;
-        const bf16x8 *L = lds + buf * S_UNITS;
-        const bool more = c + 1 < c1;
-        bool freed = false;
-        auto put = [&](int f) {
-            if (!freed) lds_wait_ge(crd + nbuf, 8u * (uint32_t)((jj + 1) / S_NBUF), lds_peek(crd + nbuf));
-            freed = true;
-            sput(f, nbuf, more);
-        };
-        lds_wait_ge(cwr + buf, 8u * (uint32_t)(jj / S_NBUF + 1), lds_peek(cwr + buf));
-        if (pact) {
-            AFrag pf0 = split8(pr[0], pr[1]), pf1 = split8(pr[2], pr[3]);
-            if (!COL) bsum[0] += sum8(pr[0], pr[1]) + sum8(pr[2], pr[3]);
-            pload(min(c + 1, c1 - 1));
-#pragma unroll
-            for (int s = 0; s < NS; s++) {
-                const AFrag s0 = s_frag(L, 0, s, lane);
-                f32x16 T = COL ? mma6_into(s0, pf0, (f32x16)(0.f)) : mma6_into(pf0, s0, (f32x16)(0.f));
-                const AFrag s1 = s_frag(L, 1, s, lane);
-                add16(acc[s], COL ? mma6_into(s1, pf1, T) : mma6_into(pf1, s1, T));
-#pragma unroll
-                for (int f = 0; f < NSF; f++)
-                    if (put_at(f) == s) put(f);
-                if (s == put_at(NSF - 1)) sload(min(c + 2, c1 - 1));
-            }
-        } else {
-            pload(min(c + 1, c1 - 1));
-#pragma unroll
-            for (int f = 0; f < NSF; f++) put(f);
-            sload(min(c + 2, c1 - 1));
-        }
-        lds_signal(crd + buf, lane);
-        lds_signal(cwr + nbuf, lane);
-    };
-    for (int c = c0; c < c1; c += 3) {
-        chunk(c, std::integral_constant<int, 0>{});
-        if (c + 1 < c1) chunk(c + 1, std::integral_constant<int, 1>{});
-        if (c + 2 < c1) chunk(c + 2, std::integral_constant<int, 2>{});
-    }
-#else
     auto chunk = [&](int c, auto BUFC) {
         constexpr int buf = decltype(BUFC)::value;
         const bf16x8 *L = lds + buf * S_UNITS;
@@ -1623,7 +1511,6 @@ __device__ __forceinline__ void dws_run(const WJob &J, size_t Ns, const float *_
         chunk(c, std::integral_constant<int, 0>{});
         if (c + 1 < c1) chunk(c + 1, std::integral_constant<int, 1>{});
     }
-#endif
     float *slab = slabs + (size_t)blockIdx.x * SLAB;
     if (COL) {
         // bias row sums: the 8 lanes staging a row hold its partial sums (fixed xor-tree order)

@@ -559,12 +559,8 @@ __device__ __forceinline__ int2 compact_slot(bool keep, int tid, uint32_t *s_wcn
 // pair costs the wave's whole gradient reduction in the backward): blend_bwd 0.336 -> 0.319 ms at
 // P = 1.0 M pairs (3 A/B pairs, tools/variant_session.sh), forward unchanged. DGS_BLEND_STRIP: strips.
 __device__ __forceinline__ int2 tile_pixel(int tid) {
-#ifdef DGS_BLEND_STRIP
-    return make_int2(tid % TILE_X, tid / TILE_X);
-#else
     const int w = tid >> 6, l = tid & 63;
     return make_int2((w & 1) * 8 + (l & 7), (w >> 1) * 8 + (l >> 3));
-#endif
 }
 
 __global__ __launch_bounds__(256) void k_blend_fwd(const uint2 *__restrict__ ranges, const uint32_t *__restrict__ vals,
@@ -812,10 +808,6 @@ __global__ __launch_bounds__(256) void k_blend_bwd(const uint2 *__restrict__ ran
             }
             // pairs (a, b) fold to rows [a_lo, b_lo, a_hi, b_hi] of w: row r of w_k holds field
             // 4k + {0, 2, 1, 3}[r] (ACC_MX..ACC_DY order)
-#ifdef DGS_DIAG_NORED  // timing experiment only (wrong results): no reduction / atomics
-            if (lane == 0 && v_mx == 1234.5f) acc[0] = v_my + v_cx + v_cy + v_cz + v_op + v_r + v_g + v_b + v_d;
-            continue;
-#endif
             const float w0 = row_sum15(fold16(fold32(v_mx, v_my), fold32(v_cx, v_cy)));
             const float w1 = row_sum15(fold16(fold32(v_cz, v_op), fold32(v_r, v_g)));
             const float w2 = row_sum15(fold16(fold32(v_b, v_d), fold32(fabsf(v_mx), fabsf(v_my))));
@@ -866,11 +858,7 @@ __device__ __forceinline__ int2 compact_slot_n(bool keep, int tid, uint32_t *s_w
 
 __device__ __forceinline__ f2 sel2(bool a, bool b, f2 x, f2 y) { return f2{a ? x.x : y.x, b ? x.y : y.y}; }
 
-#ifdef DGS_BWD2_WAVES  // experiment: occupancy target (registers capped accordingly)
-#define BWD2_OCC __attribute__((amdgpu_waves_per_eu(DGS_BWD2_WAVES)))
-#else
 #define BWD2_OCC
-#endif
 // DEPTH: the depth output has a gradient (dL_ddepth != nullptr); without one (every training step: the
 // loss reads only the image) the depth terms, the depth colour-behind state and its loads drop out
 template <bool DEPTH>
