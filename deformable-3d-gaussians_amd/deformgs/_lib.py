@@ -86,6 +86,8 @@ _SIGS = {
     "dgs_gaussian_inputs_se3_backward": ([I, I, P, P, I] + [P] * 15 + [P], I),
     "dgs_se3_forward": ([I, P, I, P, P], I),
     "dgs_se3_backward": ([I, P, I, P, P, I, P], I),
+    # (dgs_train_step_args*, int* overflowed, int* num_rendered, stream): deformgs/native_step.py
+    "dgs_train_step": ([P, ctypes.POINTER(I), ctypes.POINTER(I), P], I),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -276,6 +276,42 @@ typedef struct dgs_row_job {
 } dgs_row_job;
 int dgs_select_rows(int nrows, const uint8_t *mask, int njobs, const dgs_row_job *jobs, void *stream);
 
+/* ---- one training iteration in one call (train_baseline.py:104-128) ----
+ * deform.step -> render() input glue -> split-SH rasterizer -> (1 - lambda) L1 + lambda (1 - SSIM) ->
+ * backward (loss, rasterizer, input glue, deformation network): the fused path of
+ * deformgs/train_step.forward_backward issued from C++ (same entry points, same order, same stream)
+ * instead of through the PyTorch autograd engine. All buffers are the caller's, sized for P; gradients
+ * are overwritten in place (dgs_adam_step reads them). deform = 0: the warm-up iterations (deltas 0.0,
+ * the network does not run; train_baseline.py:106-107). t: device scalar, the frame time fid +
+ * ast_noise (train_baseline.py:107-112); t_full (P floats) is needed unless the network is the blender
+ * one on the split path (whose kernels read t[0]). deferred_count: as dgs_raster_set_deferred_count for
+ * this call; *overflowed = 1 when the speculative pair capacity overflowed (redo the step with 0).
+ * *num_rendered = the pair count, -1 when deferred. */
+typedef struct dgs_train_step_args {
+    int P;
+    const float *xyz, *f_dc, *f_rest, *scaling, *rotation, *opacity;   /* (P,3) (P,1,3) (P,15,3) (P,3) (P,4) (P,1) */
+    int deform;
+    int mlp_flags;                       /* DGS_MLP_* of the network (DGS_MLP_UNIFORM_T is implied) */
+    const float *const *mlp_params;      /* host array of device pointers, dgs_deform_pack order */
+    float *const *mlp_grads;             /* host array, same order (overwritten) */
+    float *mlp_packed, *mlp_saved, *mlp_scratch;  /* dgs_deform_{packed,saved,scratch}_floats */
+    float *mlp_out, *mlp_dout;           /* (P, dgs_deform_outputs) */
+    const float *t;
+    float *t_full;
+    dgs_raster_settings rs;
+    const float *gt;                     /* (3,H,W) */
+    float lambda_dssim;
+    float *means3D, *scales, *rotations, *opacities;  /* render inputs (P,3) (P,3) (P,4) (P,1) */
+    float *image, *depth;                /* (3,H,W) (1,H,W) */
+    int *radii;                          /* (P,) */
+    uint8_t *visible;                    /* (P,) radii > 0, may be NULL */
+    float *loss3, *loss_scratch, *dimage;   /* (3,): loss, L1, SSIM; dgs_l1_ssim_scratch_floats; (3,H,W) */
+    float *d_means3D, *d_means2D, *d_means2D_densify, *d_opacities, *d_scales, *d_rotations;
+    float *g_xyz, *g_dc, *g_rest, *g_scaling, *g_rotation, *g_opacity;  /* parameter gradients */
+    int deferred_count;
+} dgs_train_step_args;
+int dgs_train_step(const dgs_train_step_args *a, int *overflowed, int *num_rendered, void *stream);
+
 #ifdef __cplusplus
 }
 #endif
