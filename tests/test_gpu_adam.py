@@ -71,3 +71,40 @@ def test_adam_two_optimizers_one_launch():
         r2.step()
     for a, b in zip(a1 + a2, b1 + b2):
         torch.testing.assert_close(a.detach(), b.detach(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")
+def test_adam_persistent_gradient_buffers_fast_path():
+    """The native training step keeps each parameter's gradient in the same buffer every iteration;
+    step_all then reuses its launch tables and only updates the step counts and bias corrections
+    (deformgs/adam.py _FAST). With the learning rates changing every step and the gradients rewritten
+    in place, the result must still be torch.optim.Adam's; a replaced parameter (densification)
+    drops back to the full path."""
+    from deformgs import adam as adam_mod
+    from deformgs.adam import Adam, step_all
+    dev = torch.device("cuda")
+    pa, pb = _params(dev, 5), _params(dev, 5)
+    ga = [{"params": [p], "lr": 1e-3 * (i + 1), "name": f"g{i}"} for i, p in enumerate(pa)]
+    gb = [{"params": [p], "lr": 1e-3 * (i + 1), "name": f"g{i}"} for i, p in enumerate(pb)]
+    ours = Adam(ga, lr=0.0, eps=1e-15)
+    ref = torch.optim.Adam(gb, lr=0.0, eps=1e-15, foreach=False)
+    bufs = [torch.empty_like(p) for p in pa]
+    gen = torch.Generator(device="cpu").manual_seed(2)
+    hits = 0
+    for it in range(8):
+        for a, b, buf in zip(pa, pb, bufs):
+            buf.copy_(torch.randn(a.shape, generator=gen).to(dev))
+            a.grad = buf
+            b.grad = buf.clone()
+        before = [id(v) for v in adam_mod._FAST.values()]
+        step_all(ours)
+        hits += int(bool(before) and before == [id(v) for v in adam_mod._FAST.values()])
+        ref.step()
+        for go, gr in zip(ours.param_groups, ref.param_groups):
+            go["lr"] *= 0.9
+            gr["lr"] *= 0.9
+    assert hits >= 6, hits  # every step after the first reused the tables
+    torch.cuda.synchronize()
+    for a, b in zip(pa, pb):
+        torch.testing.assert_close(a.detach(), b.detach(), rtol=1e-5, atol=1e-6)
+        assert float(ours.state[a]["step"]) == float(ref.state[b]["step"]) == 8.0
