@@ -75,11 +75,12 @@ def _check(o, g, color, radii, depth, grads, keys, nr=None, tag=None):
     try:
         amb = check_integer_outputs(o, radii, nr, stats)
         gflag, pflag = tail_flags(o, amb)
+        tight = {e: tail_flags(o, amb, float(e))[0] for e in ("1e-5", "1e-6")}  # recorded only
         check_image(color, o, pflag, stats)
         derr = np.abs(depth - o.depth)
         assert (derr <= 1e-4 * max(1.0, np.abs(o.depth).max())).mean() >= 0.999
         for k, ok in keys:
-            check_gaussian_grad(grads[k], g[ok], gflag, k, stats)
+            check_gaussian_grad(grads[k], g[ok], gflag, k, stats, tighter=tight)
     finally:
         if tag:
             write_stats(tag, stats)
