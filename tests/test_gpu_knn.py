@@ -44,3 +44,15 @@ def test_knn_duplicates_and_single():
     np.testing.assert_allclose(got, _exact(pts), rtol=1e-6, atol=0)
     one = distCUDA2(torch.zeros((1, 3), device="cuda")).cpu().numpy()
     assert one.tolist() == [0.0]
+
+
+@pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")
+def test_knn_fewer_than_three_neighbours_pinned():
+    """The documented deviation from upstream simple-knn for P < 4, pinned by hand:
+    the mean over the neighbours that exist. P = 2 at distance 2: 4 each; P = 3 on a line at 0, 1, 3:
+    (1 + 9) / 2, (1 + 4) / 2, (9 + 4) / 2."""
+    from deformgs.gaussian_model import distCUDA2
+    two = distCUDA2(torch.tensor([[0.0, 0, 0], [2.0, 0, 0]], device="cuda")).cpu().numpy()
+    assert two.tolist() == [4.0, 4.0]
+    three = distCUDA2(torch.tensor([[0.0, 0, 0], [1.0, 0, 0], [3.0, 0, 0]], device="cuda")).cpu().numpy()
+    assert three.tolist() == [5.0, 2.5, 6.5]
