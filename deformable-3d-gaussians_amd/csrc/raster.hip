@@ -310,11 +310,13 @@ __device__ inline bool gauss_rect(uint32_t g, const float2 *xy, const int *radii
 
 __global__ __launch_bounds__(256) void k_rect_count(int P, const uint32_t *__restrict__ order, const float2 *__restrict__ xy,
                                                     const int *__restrict__ radii, int gx, int gy,
-                                                    uint32_t *__restrict__ cnt, uint32_t *__restrict__ total) {
+                                                    uint32_t *__restrict__ cnt, uint32_t *__restrict__ total,
+                                                    uint32_t *__restrict__ maxtodo) {
     extern __shared__ uint32_t h[];  // [T]  (total[0] = pair count, total[1] = column-scan ticket)
     const int T = gx * gy;
     for (int t = threadIdx.x; t < T; t += 256) h[t] = 0;
     if (blockIdx.x == 0 && threadIdx.x < 2) total[threadIdx.x] = 0;  // k_rect_colscan adds into them
+    if (maxtodo && blockIdx.x == 0 && threadIdx.x == 0) *maxtodo = 0;  // k_blend_fwd maxes into it
     __syncthreads();
     const int j = blockIdx.x * 256 + threadIdx.x;
     int4 rc;
@@ -563,12 +565,26 @@ __device__ __forceinline__ int2 tile_pixel(int tid) {
     return make_int2((w & 1) * 8 + (l & 7), (w >> 1) * 8 + (l >> 3));
 }
 
+// Segmented blend backward (k_blend_bwd2s): the forward leaves, every SEG list positions of a tile,
+// each pixel's (T, C) before that position (a "checkpoint", state before the Gaussians from there on),
+// and the tile's backward work (the largest last-contributor position + 1); the backward then runs
+// every SEG-long segment of every tile as an independent work item (segment-major), starting from the
+// checkpoint at the segment's end instead of replaying the whole list from the end.
+constexpr int SEG = 128;
+// checkpoint slot of list position gp (absolute, gp = tile start + a multiple of SEG, strictly inside the
+// tile's list): gp / SEG is unique across tiles (the next tile's first boundary lies >= SEG past every
+// boundary of this one)
+__device__ __forceinline__ uint32_t ckpt_slot(uint32_t gp) { return gp / SEG; }
+
+template <bool CK>  // CK: write the segmented backward's checkpoints, final state and per-tile work
 __global__ __launch_bounds__(256) void k_blend_fwd(const uint2 *__restrict__ ranges, const uint32_t *__restrict__ vals,
                                                    uint32_t cap, int W, int H, int gx, const float2 *__restrict__ xy,
                                                    const float4 *__restrict__ conic_o, const float4 *__restrict__ rgbd,
                                                    const float *bg, float *__restrict__ final_T,
                                                    uint32_t *__restrict__ n_contrib, float *__restrict__ out_color,
-                                                   float *__restrict__ out_depth) {
+                                                   float *__restrict__ out_depth, float4 *__restrict__ ckpt,
+                                                   uint32_t *__restrict__ tile_todo, uint32_t *__restrict__ maxtodo,
+                                                   float4 *__restrict__ cfin) {
     __shared__ float2 s_xy[TILE_PIX];
     __shared__ float4 s_co[TILE_PIX];
     __shared__ float4 s_cd[TILE_PIX];
@@ -612,6 +628,15 @@ __global__ __launch_bounds__(256) void k_blend_fwd(const uint2 *__restrict__ ran
         }
         __syncthreads();
         const int n = sl.y;
+        // checkpoints (segmented backward): the state before positions 256 r + 128 and 256 (r + 1); the
+        // first half of the batch (threads 0..127 = waves 0, 1) staged jmid kept Gaussians
+        const int jmid = CK ? (int)(s_wcnt[0] + s_wcnt[1]) : -1;
+        const uint32_t pix = (uint32_t)(tp.y * TILE_X + tp.x);
+        auto put_ckpt = [&](int p) {  // p: position in the tile's list (a multiple of SEG, > 0)
+            if (CK && inside && p < todo_total)
+                ckpt[(size_t)ckpt_slot(range.x + (uint32_t)p) * TILE_PIX + pix] = make_float4(T, C0, C1, C2);
+        };
+        bool mid_done = false;
         // branch-free per lane (a skipped Gaussian adds cd * 0): the skips and the stop of the
         // reference's loop become predicates, so the wave runs no exec-mask bookkeeping per
         // Gaussian; it leaves the batch once all of its lanes are done. Every staged word is a
@@ -620,6 +645,12 @@ __global__ __launch_bounds__(256) void k_blend_fwd(const uint2 *__restrict__ ran
         // (12 -> 10 LDS cycles per Gaussian and wave: blend_fwd -3.5 %)
         int lastj = 0;  // batch index + 1 of this batch's last contributor (0: none)
         for (int j = 0; j < n; j++) {
+            if constexpr (CK) {
+                if (j == jmid) {
+                    put_ckpt(r * TILE_PIX + SEG);
+                    mid_done = true;
+                }
+            }
             if (__ballot(!done) == 0ull) break;
             const int pos1 = j + 1;
             const float2 g = s_xy[j];
@@ -642,9 +673,25 @@ __global__ __launch_bounds__(256) void k_blend_fwd(const uint2 *__restrict__ ran
             lastj = use ? pos1 : lastj;
         }
         if (lastj) last = (uint32_t)s_pos[lastj - 1] + 1u;  // list position + 1 (n_contrib of the full list)
+        if constexpr (CK) {  // (a wave that left the batch early: its pixels are done, their state is final)
+            if (!mid_done) put_ckpt(r * TILE_PIX + SEG);
+            put_ckpt((r + 1) * TILE_PIX);
+        }
+    }
+    if constexpr (CK) {  // the tile's backward work: the largest last-contributor position + 1
+        __shared__ uint32_t s_todo;
+        if (tid == 0) s_todo = 0;
+        __syncthreads();
+        if (inside) atomicMax(&s_todo, last);
+        __syncthreads();
+        if (tid == 0) {
+            tile_todo[tile] = s_todo;
+            atomicMax(maxtodo, s_todo);
+        }
     }
     if (inside) {
         int pid = py * W + px;
+        if constexpr (CK) cfin[pid] = make_float4(T, C0, C1, C2);  // the final state (segmented backward)
         final_T[pid] = T;
         n_contrib[pid] = last;
         int HW = H * W;
@@ -1011,6 +1058,180 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
     }
 }
 
+// Segmented blend backward (no depth gradient: every training step). A persistent grid takes work items
+// (segment s, tile) in segment-major order from a queue; item (s, tile) replays list positions
+// [SEG s, min(SEG (s + 1), todo)) of the tile back to front, starting from the forward's checkpoint at
+// the segment's end: T = the transmittance before that position, and the colour behind it (acc) =
+// (C_final - C_before) / T. A long tile list thus runs as several concurrent work items instead of one
+// serial replay, and the grid is filled with ~2x the waves of k_blend_bwd2. The per-(pixel, Gaussian)
+// arithmetic and the reduction are k_blend_bwd2's. Numerics: acc's rounding error is ~1 ulp / T, but
+// it enters dL/dalpha multiplied by the Gaussian's own transmittance (<= T), so the gradient error stays
+// at the ulp level of dL/dpix.
+constexpr int BWD_SEG_WGS_PER_CU = 12;
+__global__ __launch_bounds__(B2) void k_blend_bwd2s(const uint2 *__restrict__ ranges, const uint32_t *__restrict__ vals,
+                                                   uint32_t cap, int W, int H, int gx, int T_tiles, const float *bg,
+                                                   const float2 *__restrict__ xy, const float4 *__restrict__ conic_o,
+                                                   const float4 *__restrict__ rgbd, const float *__restrict__ final_T,
+                                                   const uint32_t *__restrict__ n_contrib,
+                                                   const float4 *__restrict__ cfin, const float4 *__restrict__ ckpt,
+                                                   const uint32_t *__restrict__ tile_todo,
+                                                   const uint32_t *__restrict__ maxtodo, uint32_t *__restrict__ queue,
+                                                   const float *__restrict__ dL_dpix, float *__restrict__ acc) {
+    __shared__ float2 s_xy[B2];
+    __shared__ float4 s_co[B2];
+    __shared__ float4 s_q[B2];
+    __shared__ float4 s_cd[B2];
+    __shared__ uint32_t s_id[B2];
+    __shared__ int s_pos[B2];
+    __shared__ uint32_t s_wcnt[B2 / 64];
+    __shared__ int s_item;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int HW = H * W;
+    const float b0 = bg[0], b1 = bg[1], b2 = bg[2];
+    const float hx = 0.5f * W, hy = 0.5f * H;
+    const int frow = lane >> 4;
+    const float sc0 = frow == 0 ? -hx : frow == 2 ? -hy : -0.5f;
+    const float sc1 = frow == 0 ? -0.5f : 1.f;
+    const float sc2 = frow == 1 ? hx : frow == 3 ? hy : 1.f;
+    const f2 zero = f2{0.f, 0.f};
+    const int nitems = div_up((int)*maxtodo, SEG) * T_tiles;
+    for (;;) {
+        __syncthreads();  // the previous item's staged LDS and s_item are consumed
+        if (tid == 0) s_item = (int)atomicAdd(queue, 1u);
+        __syncthreads();
+        const int item = s_item;
+        if (item >= nitems) break;
+        const int seg = item / T_tiles, tile = item - seg * T_tiles;
+        const int todo = (int)tile_todo[tile];
+        const int a = seg * SEG;
+        if (a >= todo) continue;
+        const int bnd = min(a + SEG, todo);  // the segment [a, bnd) of the tile's list
+        const int tx0 = (tile % gx) * TILE_X, ty0 = (tile / gx) * TILE_Y;
+        const int lx0 = lane & 7, ly = 8 * wv + (lane >> 3);
+        const int px0 = tx0 + lx0, px1 = px0 + 8, py = ty0 + ly;
+        const bool in0 = px0 < W && py < H, in1 = px1 < W && py < H;
+        const f2 pfx = f2{(float)px0, (float)px1};
+        const float pfy = (float)py;
+        uint2 range = ranges[tile];
+        range.x = min(range.x, cap);
+        const int pid0 = py * W + px0, pid1 = py * W + px1;
+        f2 Tfinal = f2{1.f, 1.f}, dp0 = zero, dp1 = zero, dp2 = zero;
+        uint32_t last0 = 0, last1 = 0;
+        f2 T = f2{1.f, 1.f}, acc0 = zero, acc1 = zero, acc2 = zero;
+        const bool from_end = bnd == todo;
+        const float4 *ck = from_end ? nullptr : ckpt + (size_t)ckpt_slot(range.x + (uint32_t)bnd) * TILE_PIX + ly * TILE_X + lx0;
+        if (in0) {
+            Tfinal.x = final_T[pid0];
+            last0 = n_contrib[pid0];
+            dp0.x = dL_dpix[pid0];
+            dp1.x = dL_dpix[HW + pid0];
+            dp2.x = dL_dpix[2 * HW + pid0];
+            if (from_end) {
+                T.x = Tfinal.x;
+            } else {
+                const float4 c = ck[0], f = cfin[pid0];
+                const float it = 1.f / c.x;
+                T.x = c.x;
+                acc0.x = (f.y - c.y) * it;
+                acc1.x = (f.z - c.z) * it;
+                acc2.x = (f.w - c.w) * it;
+            }
+        }
+        if (in1) {
+            Tfinal.y = final_T[pid1];
+            last1 = n_contrib[pid1];
+            dp0.y = dL_dpix[pid1];
+            dp1.y = dL_dpix[HW + pid1];
+            dp2.y = dL_dpix[2 * HW + pid1];
+            if (from_end) {
+                T.y = Tfinal.y;
+            } else {
+                const float4 c = ck[8], f = cfin[pid1];
+                const float it = 1.f / c.x;
+                T.y = c.x;
+                acc0.y = (f.y - c.y) * it;
+                acc1.y = (f.z - c.z) * it;
+                acc2.y = (f.w - c.w) * it;
+            }
+        }
+        const f2 kbg = -Tfinal * (b0 * dp0 + b1 * dp1 + b2 * dp2);
+        // stage the segment (<= SEG = B2 positions) back to front, tile-culled and compacted
+        const int len = bnd - a;
+        bool keep = false;
+        uint32_t id = 0;
+        float2 gl;
+        float4 cl;
+        if (tid < len) {
+            id = vals[range.x + bnd - 1 - tid];
+            gl = xy[id];
+            cl = conic_o[id];
+            keep = tile_reach(gl, cl, (float)tx0, (float)ty0);
+        }
+        const int2 sl = compact_slot_n<B2 / 64>(keep, tid, s_wcnt);
+        if (keep) {
+            s_id[sl.x] = id;
+            s_xy[sl.x] = gl;
+            s_co[sl.x] = cl;
+            s_q[sl.x] = conic_q(cl);
+            s_cd[sl.x] = rgbd[id];
+            s_pos[sl.x] = tid;
+        }
+        __syncthreads();
+        const int n = sl.y;
+        for (int j = 0; j < n; j++) {
+            const uint32_t contributor = (uint32_t)(bnd - 1 - s_pos[j]);  // position in the tile's list
+            const float2 g = s_xy[j];
+            const float4 q = s_q[j];
+            const f2 dx = g.x - pfx;
+            const float dy = g.y - pfy;
+            const f2 power = f2{q_power(q, dx.x, dy), q_power(q, dx.y, dy)};
+            const f2 G = f2{__builtin_amdgcn_exp2f(power.x), __builtin_amdgcn_exp2f(power.y)};
+            const f2 alpha = f2{fminf(0.99f, q.w * G.x), fminf(0.99f, q.w * G.y)};
+            const bool act0 = in0 && contributor < last0 && power.x <= 0.f && alpha.x >= 1.f / 255.f;
+            const bool act1 = in1 && contributor < last1 && power.y <= 0.f && alpha.y >= 1.f / 255.f;
+            if (__ballot(act0 || act1) == 0ull) continue;  // wave-uniform
+            const float4 cd = s_cd[j];
+            const float4 co = s_co[j];
+            const f2 ae = sel2(act0, act1, alpha, zero);
+            const f2 Ge = sel2(act0, act1, G, zero);
+            const f2 om = 1.f - ae;
+            f2 inv = f2{__builtin_amdgcn_rcpf(om.x), __builtin_amdgcn_rcpf(om.y)};
+            inv = inv * (1.f - om * inv) + inv;
+            T = T * inv;
+            const f2 w = ae * T;
+            const f2 d0 = cd.x - acc0, d1 = cd.y - acc1, d2 = cd.z - acc2;
+            f2 dLda = d0 * dp0 + d1 * dp1 + d2 * dp2;
+            acc0 = ae * d0 + acc0;
+            acc1 = ae * d1 + acc1;
+            acc2 = ae * d2 + acc2;
+            dLda = dLda * T + kbg * inv;
+            const f2 vop = Ge * dLda;
+            const f2 u = co.w * vop;
+            const f2 udx = u * dx, udy = u * dy;
+            const f2 mxp = co.x * udx + co.y * udy, myp = co.y * udx + co.z * udy;
+            const f2 cxp = udx * dx, cyp = udx * dy, czp = udy * dy;
+            const f2 vr = w * dp0, vg = w * dp1, vb = w * dp2;
+            const float w0 = row_sum15(fold16(fold32(mxp.x + mxp.y, myp.x + myp.y), fold32(cxp.x + cxp.y, cyp.x + cyp.y)));
+            const float w1 = row_sum15(fold16(fold32(czp.x + czp.y, vop.x + vop.y), fold32(vr.x + vr.y, vg.x + vg.y)));
+            const float w2 = row_sum15(fold16(fold32(vb.x + vb.y, 0.f),
+                                              fold32(fabsf(mxp.x) + fabsf(mxp.y), fabsf(myp.x) + fabsf(myp.y))));
+            if ((lane & 15) == 15) {
+                const int row = lane >> 4;
+                float *dst = acc + (size_t)s_id[j] * ACC_STRIDE + ((row & 1) << 1) + (row >> 1);
+                atomicAdd(dst, w0 * sc0);
+                atomicAdd(dst + 4, w1 * sc1);
+                atomicAdd(dst + 8, w2 * sc2);
+            }
+        }
+    }
+    // the last workgroup to leave resets the queue for the next launch (every take has returned)
+    if (tid == 0 && atomicAdd(queue + 1, 1u) == gridDim.x - 1) {
+        atomicExch(queue, 0u);
+        atomicExch(queue + 1, 0u);
+    }
+}
+
 __device__ inline void dR_dq(float4 q, const float dR[9], float4 &dq) {
     float r = q.x, x = q.y, y = q.z, z = q.w;
     dq.x = 2.f * (-z * dR[1] + y * dR[2] + z * dR[3] - x * dR[5] - y * dR[6] + x * dR[7]);
@@ -1335,6 +1556,12 @@ struct dgs_raster_ctx {
     // (re)allocated, so it only ever holds 0 or words a colscan launch wrote (never stale count-matrix
     // data whose upper half could equal the current generation)
     DevBuf rtot;
+    // segmented blend backward (DGS_BLEND_SEG): the forward's per-pixel checkpoints every SEG list
+    // positions, and [work queue (2) | maxtodo | - | tile_todo (T)] (zeroed when (re)allocated; the
+    // queue resets itself at the end of every launch, maxtodo is zeroed by k_rect_count)
+    DevBuf ckb, segq;
+    bool seg_ok = false;  // this forward wrote the checkpoints
+    float4 *cfin = nullptr;  // the forward's final (T, C) per pixel (segmented backward)
     bool bwd_done = false;  // a backward already consumed the accumulators (a second one re-zeroes them)
     // carved views
     float2 *xy = nullptr;
@@ -1374,6 +1601,21 @@ bool blend_one_pixel() {
         return e && e[0] == '1';
     }();
     return v;
+}
+
+// DGS_BLEND_SEG=1: segmented blend backward (k_blend_bwd2s: SEG-long segments of every tile's list as
+// independent work items, from checkpoints the forward leaves) instead of k_blend_bwd2's one serial
+// replay per tile
+std::atomic<int> g_blend_seg{-1};  // -1: not decided yet (DGS_BLEND_SEG), else dgs_debug_set_blend_seg
+bool blend_segmented() {
+    int v = g_blend_seg.load();
+    if (v < 0) {
+        const char *e = getenv("DGS_BLEND_SEG");
+        int want = e && e[0] == '1' ? 1 : 0;
+        g_blend_seg.compare_exchange_strong(v, want);
+        v = g_blend_seg.load();
+    }
+    return v == 1;
 }
 
 // DGS_HIPCUB_SORT=1: hipcub::DeviceRadixSort for the depth and tile sorts instead of radix.hip
@@ -1645,10 +1887,21 @@ static int bin_and_blend(dgs_raster_ctx *c, int cap, int P, int device, hipStrea
         DGS_HIP_CHECK(hipMemsetAsync(c->ranges, 0, 8ull * T, stream));
         c->vals = nullptr;
     }
+    float4 *ckpt = nullptr, *cfin = nullptr;
+    uint32_t *todo = nullptr;
+    if (c->seg_ok) {
+        const size_t nck = (size_t)TILE_PIX * ((size_t)std::max(cap, 0) / SEG + 4);
+        if (int rc = c->ckb.ensure(16ull * (nck + (size_t)c->H * c->W))) return rc;
+        ckpt = (float4 *)c->ckb.p;
+        cfin = ckpt + nck;
+        c->cfin = cfin;
+        todo = (uint32_t *)c->segq.p + 4;
+    }
     {
         ScopedTimer tm("blend_fwd", stream);
-        hipLaunchKernelGGL(k_blend_fwd, dim3(T), dim3(TILE_PIX), 0, stream, c->ranges, c->vals, (uint32_t)cap, c->W, c->H, c->gx, c->xy,
-                           c->conic_o, c->rgbd, c->s.bg, c->final_T, c->n_contrib, out_color, out_depth);
+        hipLaunchKernelGGL(ckpt ? k_blend_fwd<true> : k_blend_fwd<false>, dim3(T), dim3(TILE_PIX), 0, stream, c->ranges, c->vals, (uint32_t)cap, c->W, c->H, c->gx, c->xy,
+                           c->conic_o, c->rgbd, c->s.bg, c->final_T, c->n_contrib, out_color, out_depth, ckpt, todo,
+                           todo ? todo - 2 : nullptr, cfin);
     }
     DGS_LAUNCH_CHECK("k_blend_fwd", dbg, stream);
     return DGS_OK;
@@ -1787,6 +2040,12 @@ static int raster_forward(const dgs_raster_settings *s, int P, int M, const floa
         if (c->rtot.cap != tot_cap) DGS_HIP_CHECK(hipMemsetAsync(c->rtot.p, 0, c->rtot.cap, stream));
         c->rect_tot = (unsigned long long *)c->rtot.p;
     }
+    c->seg_ok = c->rect_mode && blend_segmented();
+    if (c->seg_ok) {
+        const size_t cap0 = c->segq.cap;
+        if (int rc = c->segq.ensure(4ull * (T + 4))) return rc;
+        if (c->segq.cap != cap0) DGS_HIP_CHECK(hipMemsetAsync(c->segq.p, 0, c->segq.cap, stream));
+    }
 
     const float fx = c->W / (2.f * s->tanfovx), fy = c->H / (2.f * s->tanfovy);
     int nr = 0;
@@ -1837,7 +2096,7 @@ static int raster_forward(const dgs_raster_settings *s, int P, int M, const floa
             {
                 ScopedTimer tm("count", stream);
                 hipLaunchKernelGGL(k_rect_count, dim3(nb), dim3(256), 4ull * T, stream, P, c->order, c->xy, c->radii, c->gx,
-                                   c->gy, c->rect_cnt, c->rect_total);
+                                   c->gy, c->rect_cnt, c->rect_total, c->seg_ok ? (uint32_t *)c->segq.p + 2 : nullptr);
             }
             DGS_LAUNCH_CHECK("k_rect_count", dbg, stream);
             {
@@ -1934,7 +2193,14 @@ static int raster_backward(dgs_raster_ctx *c, const float *dL_dcolor, const floa
         if (blend_one_pixel())
             hipLaunchKernelGGL(k_blend_bwd, dim3(T), dim3(TILE_PIX), 0, stream, c->ranges, c->vals, cap, c->W, c->H, c->gx,
                                c->s.bg, c->xy, c->conic_o, c->rgbd, c->final_T, c->n_contrib, dL_dcolor, dL_ddepth, acc);
-        else
+        else if (c->seg_ok && !dL_ddepth) {
+            static int cus = 0;
+            if (!cus) DGS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+            uint32_t *q = (uint32_t *)c->segq.p;
+            hipLaunchKernelGGL(k_blend_bwd2s, dim3(cus * BWD_SEG_WGS_PER_CU), dim3(B2), 0, stream, c->ranges, c->vals, cap,
+                               c->W, c->H, c->gx, T, c->s.bg, c->xy, c->conic_o, c->rgbd, c->final_T, c->n_contrib,
+                               c->cfin, (const float4 *)c->ckb.p, q + 4, q + 2, q, dL_dcolor, acc);
+        } else
             if (dL_ddepth)
                 hipLaunchKernelGGL(k_blend_bwd2<true>, dim3(T), dim3(B2), 0, stream, c->ranges, c->vals, cap, c->W, c->H,
                                    c->gx, c->s.bg, c->xy, c->conic_o, c->rgbd, c->final_T, c->n_contrib, dL_dcolor,
@@ -2018,7 +2284,7 @@ extern "C" void dgs_raster_ctx_free(dgs_raster_ctx *c) {
         g_pool.push_back(c);
     } else {
         c->geom.release(); c->bin.release(); c->img.release(); c->acc.release(); c->tmp.release(); c->rect.release();
-        c->rtot.release();
+        c->rtot.release(); c->ckb.release(); c->segq.release();
         if (c->h_total) (void)hipHostFree(c->h_total);
         delete c;
     }
@@ -2036,6 +2302,8 @@ extern "C" void dgs_debug_set_pair_cap(int device, int cap) {
 }
 
 extern "C" int dgs_debug_pair_cap(int device) { return pair_cap_get(device); }
+
+extern "C" void dgs_debug_set_blend_seg(int on) { g_blend_seg.store(on ? 1 : 0); }
 
 extern "C" void dgs_debug_set_binning(int mode) { g_binning.store(mode == 1 ? 1 : 0); }
 

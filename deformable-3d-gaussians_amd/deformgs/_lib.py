@@ -60,6 +60,7 @@ _SIGS = {
     "dgs_debug_sort_pairs": ([P, P, P, P, I, I, I, P], I),
     "dgs_raster_deferred_overflows": ([], ctypes.c_longlong),
     "dgs_debug_set_binning": ([I], None),
+    "dgs_debug_set_blend_seg": ([I], None),
     "dgs_timing_enable": ([I], None),
     "dgs_timing_query": ([ctypes.c_char_p, ctypes.POINTER(I)], ctypes.c_double),
     "dgs_timing_reset": ([], None),

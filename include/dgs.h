@@ -129,6 +129,11 @@ void dgs_debug_set_pair_cap(int device, int cap);
 int dgs_debug_pair_cap(int device);
 void dgs_debug_set_binning(int mode);
 long long dgs_debug_binning_redos(void);
+/* Blend backward scheme (rect binning, no depth gradient): 1 = segmented (k_blend_bwd2s: every 128 list
+ * positions of a tile an independent work item, started from per-pixel checkpoints the forward writes);
+ * 0 = one serial back-to-front replay per tile (k_blend_bwd2). Default from DGS_BLEND_SEG. Applies to
+ * forwards issued after the call. */
+void dgs_debug_set_blend_seg(int on);
 /* host nanoseconds spent waiting for num_rendered (and the number of waits) since process start */
 long long dgs_debug_count_wait_ns(long long *waits);
 /* dL/dscales convention. 0 (default) = the upstream CUDA op's: the gradient w.r.t. the modified scale

@@ -423,3 +423,39 @@ def test_scale_gradient_conventions():
         lib.dgs_raster_set_exact_scale_grad(0)
     np.testing.assert_allclose(ex["scales"], up["scales"] * np.float32(1.3), rtol=1e-4,
                                atol=1e-6 * np.abs(up["scales"]).max())
+
+
+@pytest.mark.parametrize("case", [
+    # N, H, W, cam, scale_boost: config 1, ragged tiles with big Gaussians (long lists: many segments),
+    # the bench workload
+    (5000, 256, 256, 0, 0.0), (2000, 61, 83, 3, 1.0), (3000, 128, 96, 5, 2.0), (100_000, 800, 800, 0, 0.0)])
+def test_segmented_blend_backward(case):
+    """k_blend_bwd2s (dgs_debug_set_blend_seg(1)): every 128 list positions of every tile replayed as an
+    independent work item from the forward's per-pixel (T, C) checkpoints. Same checks vs the oracle as
+    every raster test (image, radii, pair count, gradients with their tails accounted for), and the
+    gradients equal the serial replay's (k_blend_bwd2) to 1e-4 relative + 1e-6 of each tensor's max
+    (float atomics in arrival order; T and the colour behind restart from the checkpoints)."""
+    from deformgs import _lib
+    lib = _lib.load()
+    N, H, W, ci, boost = case
+    inputs, rs, _ = scene(N, H, W, cam_index=ci, scale_boost=boost, seed=12)
+    rng = np.random.default_rng(7)
+    dcolor = rng.standard_normal((3, H, W)).astype(np.float32)
+    o, g = oracle_run(inputs, rs, dcolor, None)
+    res = {}
+    try:
+        for seg in (0, 1):
+            lib.dgs_debug_set_blend_seg(seg)
+            res[seg] = _run_gpu(inputs, rs, dcolor, None) + (_run_gpu.num_rendered,)
+    finally:
+        lib.dgs_debug_set_blend_seg(0)
+    color, radii, depth, grads, nr = res[1]
+    for a, b in zip(res[1][:3], res[0][:3]):
+        np.testing.assert_array_equal(a, b)  # the forward is the same with or without checkpoints
+    _check(o, g, color, radii, depth, grads,
+           [("means3D", "means3D"), ("shs", "shs"), ("opacities", "opacities"), ("scales", "scales"),
+            ("rotations", "rotations"), ("means2D", "means2D"), ("means2D_densify", "means2D_densify")],
+           nr=nr, tag=f"raster_segmented[{N}x{H}x{W}]")
+    for k in grads:
+        ref = res[0][3][k]
+        np.testing.assert_allclose(grads[k], ref, rtol=1e-4, atol=1e-6 * max(1.0, np.abs(ref).max()), err_msg=k)
