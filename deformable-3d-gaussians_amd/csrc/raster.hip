@@ -2273,6 +2273,12 @@ extern "C" int dgs_raster_backward_split_sh(dgs_raster_ctx *c, const float *dL_d
                            dL_dscales, dL_drotations, stream);
 }
 
+extern "C" int dgs_raster_ctx_num_rendered(dgs_raster_ctx *c) {
+    if (!c) return -1;
+    if (resolve_count(c, c->last_stream)) return -1;
+    return c->num_rendered;
+}
+
 extern "C" void dgs_raster_ctx_free(dgs_raster_ctx *c) {
     if (!c) return;
     (void)resolve_count(c, c->last_stream);  // a deferred count nobody read (forward without backward)

@@ -42,9 +42,18 @@ extern "C" int dgs_train_step(const dgs_train_step_args *a, int *overflowed, int
         set_error("dgs_train_step: the deformation network needs its parameter / gradient tables and buffers");
         return DGS_ERR_ARGS;
     }
+    const int phase = a->phase ? a->phase : 3;
+    if (phase < 1 || phase > 3) {
+        set_error("dgs_train_step: phase must be 0..3");
+        return DGS_ERR_ARGS;
+    }
+    const int flags = a->mlp_flags | DGS_MLP_UNIFORM_T;
+    if (phase == 2)  // the network backward of the preceding phase-1 call
+        return warm ? dgs_deform_backward(flags, P, a->mlp_packed, a->mlp_saved, a->mlp_dout, a->mlp_scratch,
+                                          a->mlp_grads, stream)
+                    : DGS_OK;
     long long over0 = dgs_raster_deferred_overflows();
     // ---- deform.step(xyz.detach(), t) (scene/deform_model.py:323-324) with one frame time ----
-    const int flags = a->mlp_flags | DGS_MLP_UNIFORM_T;
     if (warm) {
         if (int rc = dgs_deform_pack(flags, a->mlp_params, a->mlp_packed, stream)) return rc;
         // the split path of a blender network reads t[0] only (k_timenet); every other kernel a column
@@ -104,10 +113,11 @@ extern "C" int dgs_train_step(const dgs_train_step_args *a, int *overflowed, int
                                               a->g_scaling, a->g_rotation, a->g_opacity, warm ? a->mlp_dout : nullptr,
                                               warm ? nout : 10, stream);
     }
-    if (!rc && warm) rc = dgs_deform_backward(flags, P, a->mlp_packed, a->mlp_saved, a->mlp_dout, a->mlp_scratch,
+    if (!rc && warm && phase == 3) rc = dgs_deform_backward(flags, P, a->mlp_packed, a->mlp_saved, a->mlp_dout, a->mlp_scratch,
                                               a->mlp_grads, stream);
-    // the whole step is queued: now the deferred pair count may be resolved (a host wait at most)
-    if (num_rendered) *num_rendered = nr;
+    // the whole step (phase 1: up to the Gaussian gradients) is queued: now the deferred pair count may
+    // be resolved (a host wait at most)
+    if (num_rendered) *num_rendered = nr >= 0 ? nr : dgs_raster_ctx_num_rendered(ctx);
     dgs_raster_ctx_free(ctx);
     dgs_raster_set_deferred_count(0);
     if (overflowed) *overflowed = dgs_raster_deferred_overflows() != over0;

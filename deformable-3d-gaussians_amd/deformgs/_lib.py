@@ -49,6 +49,7 @@ _SIGS = {
     "dgs_raster_forward_split_sh": ([ctypes.POINTER(RasterSettings), I] + [P] * 10 + [ctypes.POINTER(P), ctypes.POINTER(I), P], I),
     "dgs_raster_backward_split_sh": ([P] * 11 + [P], I),
     "dgs_raster_ctx_free": ([P], None),
+    "dgs_raster_ctx_num_rendered": ([P], I),
     "dgs_mark_visible": ([I, P, P, P, P, P], I),
     "dgs_debug_set_pair_cap": ([I, I], None),
     "dgs_debug_binning_redos": ([], ctypes.c_longlong),

@@ -161,11 +161,18 @@ class OverlappedGradAllReduce:
         self._armed = False
         early = self._early
         pending = self._pending
+        late = [p for p in self.late_fn() if p.requires_grad]
+        # a late group without any gradient (the network in the warm-up iterations, the same on every
+        # rank) is not reduced: its parameters keep .grad None, so Adam skips them as on one rank
+        if all(p.grad is None for p in late):
+            late = []
         if pending is None:  # the hook did not fire on this rank: reduce the early group here
             self._reduce(early)
-            self._reduce([p for p in self.late_fn() if p.requires_grad])
+            if late:
+                self._reduce(late)
         else:
-            self._reduce([p for p in self.late_fn() if p.requires_grad])
+            if late:
+                self._reduce(late)
             self._reduce(early, *pending)
         self._pending = None
 

@@ -9,9 +9,13 @@ which set the speed of the small configurations (BASELINE config 2, 16k Gaussian
 Buffers are allocated once per Gaussian count (densification reallocates them); the parameter
 gradients live in persistent buffers handed to the parameters as .grad, overwritten every step.
 
-Used by train_step() for single-rank steps on the fused path (DGS_NATIVE_STEP=0 turns it off); the
-multi-rank step keeps the autograd path, whose post-accumulate-grad hooks overlap the gradient
-all-reduce with the network's backward (deformgs/dist.py).
+Used by train_step() on the fused path (DGS_NATIVE_STEP=0 turns it off). Data-parallel steps
+(`step_data_parallel`) split the call in two: phase 1 runs up to the Gaussian parameter gradients and
+resolves the pair count; the ranks agree on an overflow redo (dist.OverflowAgreement); ONE async
+all-reduce of the Gaussian gradients (a flat buffer the parameters' .grad tensors are views of: no
+concatenation, no copy back) is started and overlaps phase 2, the network backward; then the network
+gradients' all-reduce. The autograd path's hooks (dist.OverlappedGradAllReduce) do the same
+overlap with a concatenation per step.
 """
 import ctypes
 import math
@@ -39,7 +43,7 @@ class TrainStepArgs(ctypes.Structure):
         ("d_means3D", P_), ("d_means2D", P_), ("d_means2D_densify", P_), ("d_opacities", P_), ("d_scales", P_),
         ("d_rotations", P_),
         ("g_xyz", P_), ("g_dc", P_), ("g_rest", P_), ("g_scaling", P_), ("g_rotation", P_), ("g_opacity", P_),
-        ("deferred_count", I_),
+        ("deferred_count", I_), ("phase", I_),
     ]
 
 
@@ -106,9 +110,10 @@ class NativeStep:
             "mlp_scratch": e(lib.dgs_deform_scratch_floats(flags | 16, N)),
             "mlp_out": e(N, nout), "mlp_dout": e(N, nout), "t_full": e(max(N, 1)),
         }
-        # persistent parameter gradients (handed to the parameters as .grad; overwritten every step)
-        self.ggrads = [torch.empty_like(p) for p in gp]
-        self.mgrads = [torch.empty_like(p) for p in mp]
+        # persistent parameter gradients (handed to the parameters as .grad; overwritten every step),
+        # views of one flat buffer per group (the data-parallel all-reduce runs on it in place)
+        self.gflat, self.ggrads = _flat_views(gp)
+        self.mflat, self.mgrads = _flat_views(mp)
         self.params = gp + mp
         self.grads = self.ggrads + self.mgrads
         self._mp_arr = (P_ * len(mp))(*[p.data_ptr() for p in mp])
@@ -126,8 +131,10 @@ class NativeStep:
         a.g_xyz, a.g_dc, a.g_rest, a.g_scaling, a.g_rotation, a.g_opacity = (g.data_ptr() for g in self.ggrads)
         self.key = key
 
-    def __call__(self, cam, gt_image, background, warm=True, ast_noise=0.0, lambda_dssim=0.2, deferred_count=False):
-        """-> (loss (0-d tensor), render package as render() returns it, overflowed)."""
+    def __call__(self, cam, gt_image, background, warm=True, ast_noise=0.0, lambda_dssim=0.2, deferred_count=False,
+                 phase=0):
+        """-> (loss (0-d tensor), render package as render() returns it, overflowed). phase 0: the whole
+        step; 1: up to the Gaussian gradients (network_backward() issues the rest)."""
         H, W = int(cam.image_height), int(cam.image_width)
         self._ensure(H, W)
         a, b, lib = self.args, self.buf, self.lib
@@ -156,6 +163,8 @@ class NativeStep:
         loss3 = torch.empty((3,), dtype=torch.float32, device=dev)
         a.image, a.loss3 = image.data_ptr(), loss3.data_ptr()
         a.deferred_count = 1 if deferred_count else 0
+        a.phase = phase
+        self._warm = warm
         over, nr = I_(0), I_(0)
         _lib.check(lib.dgs_train_step(ctypes.byref(a), ctypes.byref(over), ctypes.byref(nr), _lib.stream_ptr(dev)),
                    "train_step")
@@ -169,3 +178,54 @@ class NativeStep:
                "viewspace_points_densify": _GradHolder(b["d_means2D_densify"]), "visibility_filter": b["visible"],
                "radii": b["radii"], "depth": b["depth"], "num_rendered": int(nr.value)}
         return loss3[0], pkg, bool(over.value)
+
+    def network_backward(self):
+        """Phase 2 of the preceding phase-1 call: the network's dX / dW (nothing in the warm-up)."""
+        if not self._warm:
+            return
+        a = self.args
+        a.phase = 2
+        _lib.check(self.lib.dgs_train_step(ctypes.byref(a), None, None, _lib.stream_ptr(self.params[0].device)),
+                   "train_step")
+
+    def step_data_parallel(self, cam, gt_image, background, warm, ast_noise, lambda_dssim, deferred_count,
+                           agreement, group=None):
+        """One data-parallel step (frame parallelism): phase 1, the rank-agreed redo of
+        an overflowed deferred pair count, the Gaussian gradient all-reduce overlapped with the network
+        backward, the network gradient all-reduce. Collectives are issued in the same order on every rank
+        (warm is the same on every rank: it depends on the iteration only). -> (loss, pkg, redone)."""
+        import torch.distributed as dist
+        from .dist import _avg_op
+        loss, pkg, over = self(cam, gt_image, background, warm, ast_noise, lambda_dssim, deferred_count, phase=1)
+        redone = False
+        if deferred_count:
+            over = agreement(over)
+            if over:
+                redone = True
+                loss, pkg, _ = self(cam, gt_image, background, warm, ast_noise, lambda_dssim, False, phase=1)
+        op = _avg_op(group)
+        # the collective stream waits for the compute stream as of here (the Gaussian gradients are
+        # final), so the all-reduce runs under the network backward issued next
+        works = [dist.all_reduce(self.gflat, op=op, group=group, async_op=True)]
+        if warm:
+            self.network_backward()
+            works.append(dist.all_reduce(self.mflat, op=op, group=group, async_op=True))
+        for w in works:
+            w.wait()  # a stream dependency (RCCL): the optimizer step queued next runs after both
+        if op == dist.ReduceOp.SUM:
+            ws = dist.get_world_size(group)
+            self.gflat.div_(ws)
+            if warm:
+                self.mflat.div_(ws)
+        return loss, pkg, redone
+
+
+def _flat_views(params):
+    """One flat fp32 buffer and a view of it shaped like each parameter."""
+    n = sum(p.numel() for p in params)
+    flat = torch.empty((max(n, 1),), dtype=torch.float32, device=params[0].device)
+    views, off = [], 0
+    for p in params:
+        views.append(flat[off:off + p.numel()].view(p.shape))
+        off += p.numel()
+    return flat[:n], views

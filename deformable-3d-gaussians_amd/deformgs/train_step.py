@@ -52,28 +52,33 @@ def forward_backward(gaussians, deform, cam, gt_image, pipe, background, is_6dof
 
 def train_step(gaussians, deform, cam, gt_image, pipe, background, is_6dof=False, lambda_dssim=0.2, warm=True,
                ast_noise=0.0, deferred_count=True, allreduce=None, agreement=None):
-    """One iteration's compute up to the optimizer. A single rank on render()'s fused training path
-    runs it as one C call (native_step.NativeStep: dgs_train_step, the same kernels in the same order
-    as forward_backward, without the autograd engine; DGS_NATIVE_STEP=0 keeps forward_backward);
+    """One iteration's compute up to the optimizer. On render()'s fused training path it runs as one C
+    call (native_step.NativeStep: dgs_train_step, the same kernels in the same order as
+    forward_backward, without the autograd engine; DGS_NATIVE_STEP=0 keeps forward_backward), or, with
+    several ranks, two calls around the overlapped Gaussian gradient all-reduce (step_data_parallel);
     otherwise forward_backward (deferred pair count unless deferred_count=False), the synchronous redo of a step whose speculative pair capacity overflowed
     (agreed across ranks by `agreement`, a dist.OverflowAgreement, when world > 1), and the gradient
     all-reduce (`allreduce`, an armed dist.OverlappedGradAllReduce, when world > 1).
     Returns (loss, render package, redone)."""
     multi = allreduce is not None and allreduce.world() > 1
-    if not multi and (not dist.is_initialized() or dist.get_world_size() == 1) and \
-            getattr(deform.deform, "is_6dof", False) == bool(is_6dof) and native_step.usable(gaussians, deform, pipe,
-                                                                                             gt_image):
+    if multi and deferred_count and agreement is None:
+        raise RuntimeError("train_step: several ranks with the deferred pair count need an OverflowAgreement")
+    single = not dist.is_initialized() or dist.get_world_size() == 1
+    if (multi or single) and getattr(deform.deform, "is_6dof", False) == bool(is_6dof) and \
+            native_step.usable(gaussians, deform, pipe, gt_image):
         # one C call per step (dgs_train_step): no autograd engine, no per-step allocations but the
-        # image and the loss (deformgs/native_step.py)
+        # image and the loss (deformgs/native_step.py); several ranks: two calls around the
+        # Gaussian gradient all-reduce
         ns = getattr(gaussians, "_dgs_native", None)
         if ns is None or ns.deform is not deform:
             ns = gaussians._dgs_native = native_step.NativeStep(gaussians, deform)
+        if multi:
+            return ns.step_data_parallel(cam, gt_image, background, warm, ast_noise, lambda_dssim, deferred_count,
+                                         agreement, allreduce.group)
         loss, pkg, over = ns(cam, gt_image, background, warm, ast_noise, lambda_dssim, deferred_count)
         if deferred_count and over:
             loss, pkg, _ = ns(cam, gt_image, background, warm, ast_noise, lambda_dssim, False)
         return loss, pkg, bool(deferred_count and over)
-    if multi and deferred_count and agreement is None:
-        raise RuntimeError("train_step: several ranks with the deferred pair count need an OverflowAgreement")
     if multi:
         allreduce.arm()
     loss, pkg = forward_backward(gaussians, deform, cam, gt_image, pipe, background, is_6dof, lambda_dssim, warm,

@@ -103,6 +103,9 @@ int dgs_raster_backward_split_sh(dgs_raster_ctx *ctx, const float *dL_dcolor, co
                                  float *dL_dscales, float *dL_drotations, void *stream);
 
 void dgs_raster_ctx_free(dgs_raster_ctx *ctx);
+/* The pair count of ctx's forward (resolving a deferred count: a host wait for the GPU's read-back);
+ * the count the binning used, i.e. the speculative capacity if it overflowed. -1 on error. */
+int dgs_raster_ctx_num_rendered(dgs_raster_ctx *ctx);
 
 /* Frustum test only (p_view.z > 0.2): visible (P,) uint8. */
 int dgs_mark_visible(int P, const float *means3D, const float *viewmatrix, const float *projmatrix,
@@ -291,7 +294,12 @@ int dgs_select_rows(int nrows, const uint8_t *mask, int njobs, const dgs_row_job
  * ast_noise (train_baseline.py:107-112); t_full (P floats) is needed unless the network is the blender
  * one on the split path (whose kernels read t[0]). deferred_count: as dgs_raster_set_deferred_count for
  * this call; *overflowed = 1 when the speculative pair capacity overflowed (redo the step with 0).
- * *num_rendered = the pair count, -1 when deferred. */
+ * *num_rendered = the pair count (a deferred count is resolved at the end of the call).
+ * phase (data-parallel steps, deformgs/native_step.py): bit 1 = everything up to the Gaussian parameter
+ * gradients (the network's dL/d(output) included), the pair count resolved at its end; bit 2 = the
+ * network backward (dX, dW) of the preceding bit-1 call; 0 = both (one call). Between the two the
+ * caller agrees on an overflow redo and starts the Gaussian gradient all-reduce, which then overlaps
+ * the network backward. */
 typedef struct dgs_train_step_args {
     int P;
     const float *xyz, *f_dc, *f_rest, *scaling, *rotation, *opacity;   /* (P,3) (P,1,3) (P,15,3) (P,3) (P,4) (P,1) */
@@ -314,6 +322,7 @@ typedef struct dgs_train_step_args {
     float *d_means3D, *d_means2D, *d_means2D_densify, *d_opacities, *d_scales, *d_rotations;
     float *g_xyz, *g_dc, *g_rest, *g_scaling, *g_rotation, *g_opacity;  /* parameter gradients */
     int deferred_count;
+    int phase;                           /* 0 (= 3), 1, 2, 3: see above */
 } dgs_train_step_args;
 int dgs_train_step(const dgs_train_step_args *a, int *overflowed, int *num_rendered, void *stream);
 

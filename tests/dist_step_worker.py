@@ -76,7 +76,8 @@ def main():
     optimizer_step(gs, deform, 3000)
     torch.cuda.synchronize()
     params = [p.detach().clone().cpu() for p in params_of(gs, deform)]
-    torch.save({"grads": grads, "params": params, "redone": redone, "loss": float(loss)},
+    torch.save({"grads": grads, "params": params, "redone": redone, "loss": float(loss),
+                "native": getattr(gs, "_dgs_native", None) is not None},
                os.path.join(out_dir, f"rank{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()

@@ -280,3 +280,70 @@ def test_overflow_discard_when_one_rank_missed_the_early_hook():
         torch.testing.assert_close(ag, torch.full((4,), 1.5))
         torch.testing.assert_close(bg, torch.full((3,), 1.5))
         torch.testing.assert_close(cg, torch.full((2,), 3.0))
+
+
+def _warmup_late_case(rank, world):
+    """A warm-up iteration: the late group (the network) has no gradient on any rank; it is not
+    reduced and keeps .grad None (Adam skips it, as on one rank); the early group is reduced."""
+    a = torch.nn.Parameter(torch.zeros(4))
+    c = torch.nn.Parameter(torch.zeros(2))
+    ar = OverlappedGradAllReduce(lambda: [a], lambda: [c])
+    ar.arm()
+    ((rank + 1.0) * a).sum().backward()
+    ar()
+    return a.grad.clone(), c.grad
+
+
+def test_warmup_network_gradients_stay_none():
+    out = _run(_warmup_late_case)
+    for rank in (0, 1):
+        ag, cg = out[rank]
+        torch.testing.assert_close(ag, torch.full((4,), 1.5))
+        assert cg is None
+
+
+def _native_dp_case(rank, world):
+    """NativeStep.step_data_parallel's collective sequence with the C calls stubbed (CPU tensors):
+    phase 1, the rank-agreed redo (rank 1 overflows: BOTH ranks redo phase 1 synchronously), the
+    Gaussian all-reduce, phase 2, the network all-reduce; a warm-up step has no network collective."""
+    from deformgs.dist import OverflowAgreement
+    from deformgs.native_step import NativeStep, _flat_views
+
+    class Stub(NativeStep):
+        def __init__(self):
+            self.calls = []
+            self.gflat, self.gviews = _flat_views([torch.zeros(3, 2), torch.zeros(5)])
+            self.mflat, self.mviews = _flat_views([torch.zeros(4)])
+
+        def __call__(self, cam, gt, bg, warm, noise, lam, deferred, phase=0):
+            self.calls.append(("p1", deferred))
+            self._warm = warm
+            self.gflat.fill_((rank + 1.0) * (10.0 if deferred else 1.0))
+            return torch.tensor(float(rank)), {}, bool(deferred and rank == 1)
+
+        def network_backward(self):
+            self.calls.append(("p2",))
+            self.mflat.copy_(torch.arange(4.0) * (rank + 1))
+
+    ns = Stub()
+    agree = OverflowAgreement()
+    out = []
+    for warm, deferred in ((True, True), (False, False)):
+        ns.calls.clear()
+        ns.mflat.fill_(-1.0)
+        loss, _, redone = ns.step_data_parallel(None, None, None, warm, 0.0, 0.2, deferred, agree)
+        out.append((list(ns.calls), redone, ns.gviews[0].clone(), ns.gviews[1].clone(), ns.mflat.clone()))
+    return out
+
+
+def test_native_data_parallel_step_sequence():
+    out = _run(_native_dp_case)
+    for rank in (0, 1):
+        (c0, r0, g0a, g0b, m0), (c1, r1, g1a, g1b, m1) = out[rank]
+        assert c0 == [("p1", True), ("p1", False), ("p2",)] and r0  # rank 1's overflow: every rank redoes
+        torch.testing.assert_close(g0a, torch.full((3, 2), 1.5))    # the redone (sync) step's gradients
+        torch.testing.assert_close(g0b, torch.full((5,), 1.5))
+        torch.testing.assert_close(m0, 1.5 * torch.arange(4.0))
+        assert c1 == [("p1", False)] and not r1  # warm-up: no phase 2, no network collective
+        torch.testing.assert_close(g1a, torch.full((3, 2), 1.5))
+        torch.testing.assert_close(m1, torch.full((4,), -1.0))

@@ -44,15 +44,19 @@ def _single_rank_grads(six=False):
 
 
 @pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")
+@pytest.mark.parametrize("path", ["native", "autograd"])
 @pytest.mark.parametrize("mode", ["plain", "overflow", "6dof"])
-def test_two_rank_step_averages_gradients(tmp_path, mode):
-    """mode 6dof: config 4's screw deformation head (trex --is_6dof), plain deferred step."""
+def test_two_rank_step_averages_gradients(tmp_path, mode, path):
+    """mode 6dof: config 4's screw deformation head (trex --is_6dof), plain deferred step. path: the
+    native step's two calls around the Gaussian gradient all-reduce (NativeStep.step_data_parallel) or
+    the autograd step with the post-accumulate-grad hooks (DGS_NATIVE_STEP=0)."""
     six = mode == "6dof"
     port = _free_port()
     procs = []
     for r in range(2):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), DGS_DEVICE="0", DGS_DIST_BACKEND="gloo")
+                   MASTER_PORT=str(port), DGS_DEVICE="0", DGS_DIST_BACKEND="gloo",
+                   DGS_NATIVE_STEP="1" if path == "native" else "0")
         procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "dist_step_worker.py"), str(tmp_path),
                                        "plain" if six else mode] + (["6dof"] if six else []), env=env, cwd=ROOT))
     rcs = []
@@ -65,6 +69,7 @@ def test_two_rank_step_averages_gradients(tmp_path, mode):
     assert rcs == [0, 0], rcs
     r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
     r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
+    assert r0["native"] == r1["native"] == (path == "native")
     if mode == "overflow":
         assert r0["redone"] and r1["redone"], "an overflow on one rank must be redone on every rank"
     else:

@@ -72,6 +72,7 @@ def test_native_step_matches_autograd_step(name, N, res, is_blender, is_6dof, as
     torch.cuda.synchronize()
     ref = dict(loss=float(loss_a), image=pkg_a["render"].detach().clone(), depth=pkg_a["depth"].detach().clone(),
                radii=pkg_a["radii"].clone(), vis=pkg_a["visibility_filter"].clone(),
+               nr=int(pkg_a["render"].grad_fn.num_rendered),
                dens=pkg_a["viewspace_points_densify"].grad.clone(),
                grads=[None if p.grad is None else p.grad.clone() for p in _params(gs, deform)])
     drop_grads(gs, deform)
@@ -83,6 +84,7 @@ def test_native_step_matches_autograd_step(name, N, res, is_blender, is_6dof, as
     assert float(loss_n) == ref["loss"]
     assert torch.equal(pkg_n["render"], ref["image"]) and torch.equal(pkg_n["depth"], ref["depth"])
     assert torch.equal(pkg_n["radii"], ref["radii"]) and torch.equal(pkg_n["visibility_filter"], ref["vis"])
+    assert pkg_n["num_rendered"] == ref["nr"] > 0  # also with the deferred count (resolved at the end)
     torch.testing.assert_close(pkg_n["viewspace_points_densify"].grad, ref["dens"], rtol=1e-4,
                                atol=1e-6 * float(ref["dens"].abs().max()))
     for i, (p, want) in enumerate(zip(_params(gs, deform), ref["grads"])):

@@ -27,6 +27,16 @@ for p in $PARTS; do
     tests)
       run 1100 $O/gpu_tests.txt python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread
       tail -3 $O/gpu_tests.txt ;;
+    tests:*)  # tests:<file>,<file>,... (names under tests/, without .py)
+      files=$(echo "${p#tests:}" | tr ',' '\n' | sed 's|^|tests/|; s|$|.py|' | tr '\n' ' ')
+      log=$O/tests_$(echo "${p#tests:}" | tr ',' '_' | cut -c1-60).txt
+      run 1000 $log python -u -m pytest $files -v --timeout 600 --timeout-method thread
+      tail -3 $log ;;
+    ab)  # the segmented blend backward against the serial replay, kernel timings on
+      for s in 0 1; do
+        DGS_BLEND_SEG=$s run 200 $O/ab_seg$s.jsonl python bench.py --no-cpu-baseline --kernel-timing major
+        tail -1 $O/ab_seg$s.jsonl | cut -c1-200
+      done ;;
     smoke)
       run 300 $O/smoke.txt python -c "import __graft_entry__ as g; g.smoke()"
       tail -1 $O/smoke.txt ;;
