@@ -3,7 +3,7 @@
 # its CPU baseline), config-sized bench lines, and a rocprofv3 kernel trace + stats plus the FETCH_SIZE /
 # WRITE_SIZE passes (tools/gpu_prof.sh). Every GPU step has its own time limit; a step that times out,
 # aborts or faults ends the session (a failing test does not). Outputs: gpurun_out/$TAG/.
-#   usage: TAG=r4b [PARTS="tests smoke bench configs prof"] tools/evidence.sh
+#   usage: TAG=r4b [PARTS="tests smoke bench configs prof ab stall tests:<file>,..."] tools/evidence.sh
 set -u
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
@@ -49,6 +49,13 @@ for p in $PARTS; do
         run 300 $O/cfg.log python bench.py --no-cpu-baseline $a && tail -1 $O/cfg.log >> $O/configs.jsonl
       done
       cut -c1-160 $O/configs.jsonl ;;
+    stall)  # wave-state PMC of the blend kernels over a short bench run (both blend backward paths)
+      for s in 0 1; do
+        DGS_BLEND_SEG=$s TAG=${TAG}_seg$s PROG="bench.py --steps 6 --warmup 3 --no-cpu-baseline" PMC_TIMEOUT=150 \
+          KERNELS="blend_fwd=k_blend_fwd,blend_bwd2=k_blend_bwd2<,blend_bwd2s=k_blend_bwd2s" \
+          run 400 $O/stall_seg$s.txt bash tools/stall_pmc.sh
+        tail -30 $O/stall_seg$s.txt
+      done ;;
     prof)
       TAG=$TAG run 1000 $O/prof.log bash tools/gpu_prof.sh
       tail -5 $O/prof.log ;;

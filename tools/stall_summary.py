@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Per-kernel averages of the tools/stall_pmc.sh counter passes (split-bf16 MLP kernels only)."""
+"""Per-kernel averages of the tools/stall_pmc.sh counter passes (default: the split-bf16 MLP kernels;
+KERNELS="name=substring,..." picks others, e.g. KERNELS="fwd=k_blend_fwd,bwd2=k_blend_bwd2<,bwd2s=k_blend_bwd2s")."""
 import csv
 import glob
 import os
@@ -7,6 +8,8 @@ import sys
 from collections import defaultdict
 
 KERNELS = {"k_fwd": "mlps::k_fwd<true", "k_bwd": "mlps::k_bwd<", "k_dws": "mlps::k_dws("}
+if os.environ.get("KERNELS"):
+    KERNELS = dict(kv.split("=", 1) for kv in os.environ["KERNELS"].split(","))
 
 
 def main():
