@@ -220,12 +220,16 @@ class NativeStep:
         return loss, pkg, redone
 
 
+_ALIGN = 64  # floats: every view starts on a 256-byte boundary (the SH gradient rows need >= 16 B)
+
+
 def _flat_views(params):
-    """One flat fp32 buffer and a view of it shaped like each parameter."""
-    n = sum(p.numel() for p in params)
-    flat = torch.empty((max(n, 1),), dtype=torch.float32, device=params[0].device)
-    views, off = [], 0
+    """One flat fp32 buffer and a view of it shaped like each parameter, each view aligned to _ALIGN
+    floats (the padding between views is zero and stays zero: it is all-reduced along, never written)."""
+    offs, n = [], 0
     for p in params:
-        views.append(flat[off:off + p.numel()].view(p.shape))
-        off += p.numel()
+        offs.append(n)
+        n += -(-p.numel() // _ALIGN) * _ALIGN
+    flat = torch.zeros((max(n, 1),), dtype=torch.float32, device=params[0].device)
+    views = [flat[o:o + p.numel()].view(p.shape) for o, p in zip(offs, params)]
     return flat[:n], views

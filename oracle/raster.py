@@ -50,6 +50,8 @@ def lib():
         _lib.or_preprocess_raw.argtypes = [P] * 4
         _lib.or_flip_flags.argtypes = [P, ctypes.c_float, P, P]
         _lib.or_flip_flags.restype = ctypes.c_int
+        _lib.or_preprocess_flags.argtypes = [P, ctypes.c_float, P]
+        _lib.or_preprocess_flags.restype = ctypes.c_int
     return _lib
 
 
@@ -144,6 +146,13 @@ class OracleRaster:
         px = np.zeros((H, W), np.uint8)
         lib().or_flip_flags(self._st, float(eps), _ptr(g), _ptr(px))
         return g.astype(bool), px.astype(bool)
+
+    def preprocess_flags(self, eps):
+        """Per-Gaussian flags of gradient-only preprocess decisions within eps of their threshold: the
+        EWA Jacobian's frustum clamp and the SH colour clamp (raster_ref.c or_preprocess_flags)."""
+        g = np.zeros((self.N,), np.uint8)
+        lib().or_preprocess_flags(self._st, float(eps), _ptr(g))
+        return g.astype(bool)
 
     def backward(self, dL_dcolor, dL_ddepth=None):
         N, M = self.N, self.M

@@ -66,6 +66,7 @@ typedef struct {
     float *radf, *vz, *pxy; /* 3 sqrt(lambda_max) before the ceil; view-space z; pixel centre */
     int *radii, *tiles;
     uint8_t *clamped;
+    float *rgb_raw; /* SH colour + 0.5 before the clamp at 0 (tests: or_preprocess_flags) */
     /* binning */
     uint64_t *keys;
     uint32_t *vals;
@@ -154,7 +155,7 @@ static void cov2d_from(const float *tv, float fx, float fy, float tanx, float ta
     out[2] = cc + 0.3f;
 }
 
-static void sh_to_rgb(int deg, int M, const float *sh, const float *dir, float *rgb, uint8_t *cl) {
+static void sh_to_rgb(int deg, int M, const float *sh, const float *dir, float *rgb, uint8_t *cl, float *raw) {
     float x = dir[0], y = dir[1], z = dir[2];
     for (int c = 0; c < 3; c++) {
 #define S(k) sh[(k) * 3 + c]
@@ -176,6 +177,7 @@ static void sh_to_rgb(int deg, int M, const float *sh, const float *dir, float *
         }
 #undef S
         r += 0.5f;
+        if (raw) raw[c] = r;
         cl[c] = r < 0.f;
         rgb[c] = r < 0.f ? 0.f : r;
     }
@@ -211,6 +213,7 @@ int or_forward(const ORSettings *s, int N, int M, const float *means3D, const fl
     st->radii = (int *)calloc(N, sizeof(int));
     st->tiles = (int *)calloc(N, sizeof(int));
     st->clamped = (uint8_t *)calloc((size_t)N * 3, 1);
+    st->rgb_raw = (float *)calloc((size_t)N * 3, sizeof(float));
     st->radf = (float *)calloc(N, sizeof(float));
     st->vz = (float *)calloc(N, sizeof(float));
     st->pxy = (float *)calloc((size_t)N * 2, sizeof(float));
@@ -258,7 +261,8 @@ int or_forward(const ORSettings *s, int N, int M, const float *means3D, const fl
             float d[3] = {p[0] - s->campos[0], p[1] - s->campos[1], p[2] - s->campos[2]};
             float n = sqrtf(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
             d[0] /= n; d[1] /= n; d[2] /= n;
-            sh_to_rgb(s->sh_degree, M, st->shs + (size_t)i * M * 3, d, st->rgb + 3 * i, st->clamped + 3 * i);
+            sh_to_rgb(s->sh_degree, M, st->shs + (size_t)i * M * 3, d, st->rgb + 3 * i, st->clamped + 3 * i,
+                      st->rgb_raw + 3 * i);
         }
         st->depth[i] = pv[2];
         st->radii[i] = rad;
@@ -715,7 +719,7 @@ void or_free(void *p) {
     if (!st) return;
     free(st->means3D); free(st->shs); free(st->colors_in); free(st->opac); free(st->scales);
     free(st->rots); free(st->cov_in); free(st->depth); free(st->xy); free(st->conic_o);
-    free(st->rgb); free(st->cov3D); free(st->radii); free(st->tiles); free(st->clamped);
+    free(st->rgb); free(st->cov3D); free(st->radii); free(st->tiles); free(st->clamped); free(st->rgb_raw);
     free(st->keys); free(st->vals); free(st->range_lo); free(st->range_hi); free(st->final_T);
     free(st->n_contrib); free(st->radf); free(st->vz); free(st->pxy);
     free(st);
@@ -813,4 +817,29 @@ int or_flip_flags(void *p, float eps, uint8_t *gflag, uint8_t *pflag) {
             }
     }
     return flagged;
+}
+
+/* Near-threshold decisions of the preprocess that only switch a Gaussian's GRADIENT (its forward
+   value is continuous across them), for the rendered Gaussians (tests): the frustum clamp of the EWA
+   Jacobian (|t.x / t.z| within eps limx of limx = 1.3 tan(fovx / 2), or y: the x / y gradient of the
+   view-space mean is zeroed past it) and the SH colour clamp at 0 (|SH colour + 0.5| <= eps: the
+   colour's gradient is zeroed below it). gflag |= 1 for such Gaussians. Returns their number. */
+int or_preprocess_flags(void *p, float eps, uint8_t *gflag) {
+    ORState *st = (ORState *)p;
+    const ORSettings *s = &st->s;
+    const float limx = 1.3f * s->tanfovx, limy = 1.3f * s->tanfovy;
+    int n = 0;
+    for (int i = 0; i < st->N; i++) {
+        if (st->radii[i] <= 0) continue;
+        float tv[3];
+        xform43(s->viewmatrix, st->means3D + 3 * i, tv);
+        int near = fabsf(fabsf(tv[0] / tv[2]) - limx) <= eps * limx || fabsf(fabsf(tv[1] / tv[2]) - limy) <= eps * limy;
+        if (!st->colors_in)
+            for (int c = 0; c < 3; c++) near |= fabsf(st->rgb_raw[3 * i + c]) <= eps;
+        if (near) {
+            gflag[i] = 1;
+            n++;
+        }
+    }
+    return n;
 }

@@ -188,9 +188,11 @@ def check_integer_outputs(o, radii_gpu, nr_gpu, stats=None):
 
 def tail_flags(o, amb=None, eps=1e-4):
     """Gaussians (and pixels) whose gradient (value) may legitimately differ from the oracle's by
-    more than rounding: a near-threshold blend decision in their pixel (oracle or_flip_flags), or a
-    fp32-ambiguous radius / rectangle / cull (integer_ambiguity)."""
+    more than rounding: a near-threshold blend decision in their pixel (oracle or_flip_flags), a
+    near-threshold gradient mask of their own preprocess (the EWA frustum clamp, the SH colour clamp:
+    or_preprocess_flags), or a fp32-ambiguous radius / rectangle / cull (integer_ambiguity)."""
     g, px = o.flip_flags(eps)
+    g = g | o.preprocess_flags(eps)
     if amb is not None:
         g = g | amb["rad_amb"] | amb["rect_amb"] | amb["cull_amb"]
         H, W = px.shape
