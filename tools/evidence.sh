@@ -50,12 +50,15 @@ for p in $PARTS; do
       done
       cut -c1-160 $O/configs.jsonl ;;
     stall)  # wave-state PMC of the blend kernels over a short bench run (both blend backward paths)
-      for s in 0 1; do
+      for s in ${STALL_SEG:-0 1}; do
         DGS_BLEND_SEG=$s TAG=${TAG}_seg$s PROG="bench.py --steps 6 --warmup 3 --no-cpu-baseline" PMC_TIMEOUT=150 \
           KERNELS="blend_fwd=k_blend_fwd,blend_bwd2=k_blend_bwd2<,blend_bwd2s=k_blend_bwd2s" \
           run 400 $O/stall_seg$s.txt bash tools/stall_pmc.sh
         tail -30 $O/stall_seg$s.txt
       done ;;
+    outlier)  # tools/step_outlier.py on the composed-step case OUTLIER (default blender-cfg2)
+      run 300 $O/outlier.txt python tools/step_outlier.py ${OUTLIER:-blender-cfg2}
+      tail -30 $O/outlier.txt ;;
     prof)
       TAG=$TAG run 1000 $O/prof.log bash tools/gpu_prof.sh
       tail -5 $O/prof.log ;;
