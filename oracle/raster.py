@@ -52,6 +52,8 @@ def lib():
         _lib.or_flip_flags.restype = ctypes.c_int
         _lib.or_preprocess_flags.argtypes = [P, ctypes.c_float, P]
         _lib.or_preprocess_flags.restype = ctypes.c_int
+        _lib.or_pixel_gaussians.argtypes = [P, P, P]
+        _lib.or_pixel_gaussians.restype = ctypes.c_int
     return _lib
 
 
@@ -152,6 +154,14 @@ class OracleRaster:
         EWA Jacobian's frustum clamp and the SH colour clamp (raster_ref.c or_preprocess_flags)."""
         g = np.zeros((self.N,), np.uint8)
         lib().or_preprocess_flags(self._st, float(eps), _ptr(g))
+        return g.astype(bool)
+
+    def pixel_gaussians(self, pmask):
+        """Per-Gaussian flags of the Gaussians blended in the pixels of pmask (H, W) (raster_ref.c
+        or_pixel_gaussians)."""
+        m = np.ascontiguousarray(pmask, np.uint8)
+        g = np.zeros((self.N,), np.uint8)
+        lib().or_pixel_gaussians(self._st, _ptr(m), _ptr(g))
         return g.astype(bool)
 
     def backward(self, dL_dcolor, dL_ddepth=None):

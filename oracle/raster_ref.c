@@ -843,3 +843,36 @@ int or_preprocess_flags(void *p, float eps, uint8_t *gflag) {
     }
     return n;
 }
+
+/* Gaussians that contribute to the pixels in pmask (tests): every Gaussian listed in such a pixel's
+   tile up to and including its stop that passes the power / alpha tests there. Used for pixels whose
+   loss gradient itself sits at a decision (the L1 term's sign where the image equals the target within
+   the image tolerance): the gradient of every Gaussian blended there can move by that pixel's share.
+   gflag |= 1; returns the number of Gaussians newly flagged. */
+int or_pixel_gaussians(void *p, const uint8_t *pmask, uint8_t *gflag) {
+    ORState *st = (ORState *)p;
+    const int H = st->s.image_height, W = st->s.image_width;
+    int n = 0;
+    for (int py = 0; py < H; py++)
+        for (int px = 0; px < W; px++) {
+            if (!pmask[py * W + px]) continue;
+            const int t = (py / BY) * st->grid_x + px / BX;
+            const float pfx = (float)px, pfy = (float)py;
+            float Tt = 1.f;
+            for (int j = st->range_lo[t]; j < st->range_hi[t]; j++) {
+                int g = st->vals[j];
+                float dx = st->xy[2 * g] - pfx, dy = st->xy[2 * g + 1] - pfy;
+                const float *co = st->conic_o + 4 * g;
+                float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                if (power > 0.f) continue;
+                float alpha = fminf(0.99f, co[3] * expf(power));
+                if (alpha < 1.f / 255.f) continue;
+                if (!gflag[g]) n++;
+                gflag[g] = 1;
+                float testT = Tt * (1.f - alpha);
+                if (testT < 0.0001f) break;
+                Tt = testT;
+            }
+        }
+    return n;
+}

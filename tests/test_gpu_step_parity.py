@@ -18,7 +18,8 @@
 Tolerances (floating point, fp32 kernels vs an fp64/fp32 oracle): loss within 2e-6 relative; image
 and integer outputs as test_gpu_raster; Gaussian gradients: >= 99.5 % of elements within 2e-3 of the
 tensor's max + 1e-3 relative and every element outside that on a Gaussian with a near-threshold
-decision; MLP gradients (sums over all points): max error within 2e-3 of the tensor's max. The MLP
+decision (the rasterizer's, or the L1 term's sign: a pixel where the GPU's and the oracle's images lie
+on different sides of the target flags the Gaussians blended there); MLP gradients (sums over all points): max error within 2e-3 of the tensor's max. The MLP
 oracle's backward uses the kernel's own relu' masks (a pre-activation within an ulp of 0 can take
 either sign in fp32), and every mask that differs from the oracle's own z > 0 is checked to sit on a
 pre-activation within 2e-5 of its layer's max |z| of zero.
@@ -184,7 +185,18 @@ def test_training_step_vs_oracle_chain(name, N, res, is_blender, is_6dof, ast_no
         amb = check_integer_outputs(o, pkg["radii"].cpu().numpy(), nr_gpu, stats)
         gflag, pflag = tail_flags(o, amb)
         tight = {e: tail_flags(o, amb, float(e))[0] for e in ("1e-5", "1e-6")}  # recorded only
-        check_image(pkg["render"].detach().cpu().numpy(), o, pflag, stats)
+        img_gpu = pkg["render"].detach().cpu().numpy()
+        check_image(img_gpu, o, pflag, stats)
+        # the L1 term's gradient is sign(image - gt): where the GPU's and the oracle's images lie on
+        # different sides of the target (|image - gt| below their difference), dL/dpixel differs by
+        # 2 (1 - lambda) / (3 H W) there, and so does the gradient of every Gaussian blended in it
+        gt_np = gt.cpu().numpy()
+        l1_flip = (np.sign(img_gpu - gt_np) != np.sign(o.color - gt_np)).any(0)
+        stats["l1_sign_flip_px"] = int(l1_flip.sum())
+        if l1_flip.any():
+            lf = o.pixel_gaussians(l1_flip)
+            gflag = gflag | lf
+            tight = {e: f | lf for e, f in tight.items()}
         params = {"_xyz": gs._xyz, "_scaling": gs._scaling, "_rotation": gs._rotation, "_opacity": gs._opacity,
                   "_features_dc": gs._features_dc, "_features_rest": gs._features_rest}
         params.update({"mlp." + k: p for k, p in deform.deform.named_parameters()})
