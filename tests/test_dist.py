@@ -323,7 +323,7 @@ def _native_dp_case(rank, world):
 
         def network_backward(self):
             self.calls.append(("p2",))
-            self.mflat.copy_(torch.arange(4.0) * (rank + 1))
+            self.mviews[0].copy_(torch.arange(4.0) * (rank + 1))
 
     ns = Stub()
     agree = OverflowAgreement()
@@ -332,7 +332,7 @@ def _native_dp_case(rank, world):
         ns.calls.clear()
         ns.mflat.fill_(-1.0)
         loss, _, redone = ns.step_data_parallel(None, None, None, warm, 0.0, 0.2, deferred, agree)
-        out.append((list(ns.calls), redone, ns.gviews[0].clone(), ns.gviews[1].clone(), ns.mflat.clone()))
+        out.append((list(ns.calls), redone, ns.gviews[0].clone(), ns.gviews[1].clone(), ns.mviews[0].clone()))
     return out
 
 
