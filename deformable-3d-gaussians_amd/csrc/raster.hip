@@ -626,8 +626,16 @@ __global__ __launch_bounds__(256) void k_blend_fwd(const uint2 *__restrict__ ran
             s_cd[sl.x] = rgbd[id];
             s_pos[sl.x] = prog;
         }
+        // the batch is padded to a multiple of 4 with inert entries (zero conic and opacity: power 0,
+        // alpha 0, never used), so the loop below tests for its early exit once per 4 Gaussians
+        const int n = sl.y, n4 = (sl.y + 3) & ~3;
+        if (tid >= n && tid < n4) {
+            s_xy[tid] = make_float2(0.f, 0.f);
+            s_co[tid] = make_float4(0.f, 0.f, 0.f, 0.f);
+            s_cd[tid] = make_float4(0.f, 0.f, 0.f, 0.f);
+            s_pos[tid] = 0;
+        }
         __syncthreads();
-        const int n = sl.y;
         // checkpoints (segmented backward): the state before positions 256 r + 128 and 256 (r + 1); the
         // first half of the batch (threads 0..127 = waves 0, 1) staged jmid kept Gaussians
         const int jmid = CK ? (int)(s_wcnt[0] + s_wcnt[1]) : -1;
@@ -644,33 +652,37 @@ __global__ __launch_bounds__(256) void k_blend_fwd(const uint2 *__restrict__ ran
         // contributor is tracked as a batch index and mapped to its list position once per batch
         // (12 -> 10 LDS cycles per Gaussian and wave: blend_fwd -3.5 %)
         int lastj = 0;  // batch index + 1 of this batch's last contributor (0: none)
-        for (int j = 0; j < n; j++) {
-            if constexpr (CK) {
-                if (j == jmid) {
-                    put_ckpt(r * TILE_PIX + SEG);
-                    mid_done = true;
-                }
-            }
+        for (int j0 = 0; j0 < n4; j0 += 4) {
             if (__ballot(!done) == 0ull) break;
-            const int pos1 = j + 1;
-            const float2 g = s_xy[j];
-            const float4 q = s_co[j];
-            const float4 cd = s_cd[j];
-            const float dx = g.x - pfx, dy = g.y - pfy;
-            const float power = q_power(q, dx, dy);
-            const float alpha = fminf(0.99f, q.w * __builtin_amdgcn_exp2f(power));
-            const float testT = T * (1.f - alpha);
-            bool use = !done && !(power > 0.f) && !(alpha < 1.f / 255.f);
-            const bool stop = use && testT < 0.0001f;
-            done = done || stop;
-            use = use && !stop;
-            const float w = use ? alpha * T : 0.f;
-            C0 += cd.x * w;
-            C1 += cd.y * w;
-            C2 += cd.z * w;
-            Dd += cd.w * w;
-            T = use ? testT : T;
-            lastj = use ? pos1 : lastj;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int j = j0 + u;
+                if constexpr (CK) {
+                    if (j == jmid) {
+                        put_ckpt(r * TILE_PIX + SEG);
+                        mid_done = true;
+                    }
+                }
+                const int pos1 = j + 1;
+                const float2 g = s_xy[j];
+                const float4 q = s_co[j];
+                const float4 cd = s_cd[j];
+                const float dx = g.x - pfx, dy = g.y - pfy;
+                const float power = q_power(q, dx, dy);
+                const float alpha = fminf(0.99f, q.w * __builtin_amdgcn_exp2f(power));
+                const float testT = T * (1.f - alpha);
+                bool use = !done && !(power > 0.f) && !(alpha < 1.f / 255.f);
+                const bool stop = use && testT < 0.0001f;
+                done = done || stop;
+                use = use && !stop;
+                const float w = use ? alpha * T : 0.f;
+                C0 += cd.x * w;
+                C1 += cd.y * w;
+                C2 += cd.z * w;
+                Dd += cd.w * w;
+                T = use ? testT : T;
+                lastj = use ? pos1 : lastj;
+            }
         }
         if (lastj) last = (uint32_t)s_pos[lastj - 1] + 1u;  // list position + 1 (n_contrib of the full list)
         if constexpr (CK) {  // (a wave that left the batch early: its pixels are done, their state is final)
