@@ -11,7 +11,7 @@ gradients live in persistent buffers handed to the parameters as .grad, overwrit
 
 Used by train_step() on the fused path (DGS_NATIVE_STEP=0 turns it off). Data-parallel steps
 (`step_data_parallel`) split the call in two: phase 1 runs up to the Gaussian parameter gradients and
-resolves the pair count; the ranks agree on an overflow redo (dist.OverflowAgreement); ONE async
+resolves the pair count (an overflow is redone by that rank alone, before any collective); ONE async
 all-reduce of the Gaussian gradients (a flat buffer the parameters' .grad tensors are views of: no
 concatenation, no copy back) is started and overlaps phase 2, the network backward; then the network
 gradients' all-reduce. The autograd path's hooks (dist.OverlappedGradAllReduce) do the same
@@ -189,20 +189,25 @@ class NativeStep:
                    "train_step")
 
     def step_data_parallel(self, cam, gt_image, background, warm, ast_noise, lambda_dssim, deferred_count,
-                           agreement, group=None):
-        """One data-parallel step (frame parallelism): phase 1, the rank-agreed redo of
+                           agreement=None, group=None):
+        """One data-parallel step (frame parallelism): phase 1, this rank's own redo of
         an overflowed deferred pair count, the Gaussian gradient all-reduce overlapped with the network
         backward, the network gradient all-reduce. Collectives are issued in the same order on every rank
-        (warm is the same on every rank: it depends on the iteration only). -> (loss, pkg, redone)."""
+        (warm is the same on every rank: it depends on the iteration only). -> (loss, pkg, redone).
+
+        No rank agreement is needed (`agreement` is accepted and unused): the pair count is resolved at
+        the end of phase 1, BEFORE this step issues any collective, so a rank whose speculative capacity
+        overflowed redoes its own phase 1 synchronously and then joins the same collectives as every
+        other rank (which simply wait for it inside the all-reduce). Only the autograd path, whose hooks
+        may start the early collective before the count is known, needs dist.OverflowAgreement: the
+        native path has no per-step host collective at all."""
         import torch.distributed as dist
         from .dist import _avg_op
         loss, pkg, over = self(cam, gt_image, background, warm, ast_noise, lambda_dssim, deferred_count, phase=1)
         redone = False
-        if deferred_count:
-            over = agreement(over)
-            if over:
-                redone = True
-                loss, pkg, _ = self(cam, gt_image, background, warm, ast_noise, lambda_dssim, False, phase=1)
+        if deferred_count and over:
+            redone = True
+            loss, pkg, _ = self(cam, gt_image, background, warm, ast_noise, lambda_dssim, False, phase=1)
         op = _avg_op(group)
         # the collective stream waits for the compute stream as of here (the Gaussian gradients are
         # final), so the all-reduce runs under the network backward issued next

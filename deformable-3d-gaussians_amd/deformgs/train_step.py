@@ -55,14 +55,13 @@ def train_step(gaussians, deform, cam, gt_image, pipe, background, is_6dof=False
     """One iteration's compute up to the optimizer. On render()'s fused training path it runs as one C
     call (native_step.NativeStep: dgs_train_step, the same kernels in the same order as
     forward_backward, without the autograd engine; DGS_NATIVE_STEP=0 keeps forward_backward), or, with
-    several ranks, two calls around the overlapped Gaussian gradient all-reduce (step_data_parallel);
+    several ranks, two calls around the overlapped Gaussian gradient all-reduce (step_data_parallel: an
+    overflowed pair count is redone by its rank alone, no agreement);
     otherwise forward_backward (deferred pair count unless deferred_count=False), the synchronous redo of a step whose speculative pair capacity overflowed
     (agreed across ranks by `agreement`, a dist.OverflowAgreement, when world > 1), and the gradient
     all-reduce (`allreduce`, an armed dist.OverlappedGradAllReduce, when world > 1).
     Returns (loss, render package, redone)."""
     multi = allreduce is not None and allreduce.world() > 1
-    if multi and deferred_count and agreement is None:
-        raise RuntimeError("train_step: several ranks with the deferred pair count need an OverflowAgreement")
     single = not dist.is_initialized() or dist.get_world_size() == 1
     if (multi or single) and getattr(deform.deform, "is_6dof", False) == bool(is_6dof) and \
             native_step.usable(gaussians, deform, pipe, gt_image):
@@ -79,6 +78,8 @@ def train_step(gaussians, deform, cam, gt_image, pipe, background, is_6dof=False
         if deferred_count and over:
             loss, pkg, _ = ns(cam, gt_image, background, warm, ast_noise, lambda_dssim, False)
         return loss, pkg, bool(deferred_count and over)
+    if multi and deferred_count and agreement is None:
+        raise RuntimeError("train_step: several ranks with the deferred pair count need an OverflowAgreement")
     if multi:
         allreduce.arm()
     loss, pkg = forward_backward(gaussians, deform, cam, gt_image, pipe, background, is_6dof, lambda_dssim, warm,

@@ -304,9 +304,9 @@ def test_warmup_network_gradients_stay_none():
 
 def _native_dp_case(rank, world):
     """NativeStep.step_data_parallel's collective sequence with the C calls stubbed (CPU tensors):
-    phase 1, the rank-agreed redo (rank 1 overflows: BOTH ranks redo phase 1 synchronously), the
-    Gaussian all-reduce, phase 2, the network all-reduce; a warm-up step has no network collective."""
-    from deformgs.dist import OverflowAgreement
+    phase 1, the redo of an overflowed pair count by that rank ALONE (rank 1: no agreement, no host
+    collective), the Gaussian all-reduce, phase 2, the network all-reduce; a warm-up step has no
+    network collective."""
     from deformgs.native_step import NativeStep, _flat_views
 
     class Stub(NativeStep):
@@ -326,12 +326,11 @@ def _native_dp_case(rank, world):
             self.mviews[0].copy_(torch.arange(4.0) * (rank + 1))
 
     ns = Stub()
-    agree = OverflowAgreement()
     out = []
     for warm, deferred in ((True, True), (False, False)):
         ns.calls.clear()
         ns.mflat.fill_(-1.0)
-        loss, _, redone = ns.step_data_parallel(None, None, None, warm, 0.0, 0.2, deferred, agree)
+        loss, _, redone = ns.step_data_parallel(None, None, None, warm, 0.0, 0.2, deferred)
         out.append((list(ns.calls), redone, ns.gviews[0].clone(), ns.gviews[1].clone(), ns.mviews[0].clone()))
     return out
 
@@ -340,9 +339,12 @@ def test_native_data_parallel_step_sequence():
     out = _run(_native_dp_case)
     for rank in (0, 1):
         (c0, r0, g0a, g0b, m0), (c1, r1, g1a, g1b, m1) = out[rank]
-        assert c0 == [("p1", True), ("p1", False), ("p2",)] and r0  # rank 1's overflow: every rank redoes
-        torch.testing.assert_close(g0a, torch.full((3, 2), 1.5))    # the redone (sync) step's gradients
-        torch.testing.assert_close(g0b, torch.full((5,), 1.5))
+        if rank == 1:  # its overflow is redone (synchronously) by this rank alone
+            assert c0 == [("p1", True), ("p1", False), ("p2",)] and r0
+        else:
+            assert c0 == [("p1", True), ("p2",)] and not r0
+        torch.testing.assert_close(g0a, torch.full((3, 2), 6.0))  # mean of rank 0's 10 and rank 1's redone 2
+        torch.testing.assert_close(g0b, torch.full((5,), 6.0))
         torch.testing.assert_close(m0, 1.5 * torch.arange(4.0))
         assert c1 == [("p1", False)] and not r1  # warm-up: no phase 2, no network collective
         torch.testing.assert_close(g1a, torch.full((3, 2), 1.5))
