@@ -928,12 +928,11 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
                                                    const uint32_t *__restrict__ n_contrib,
                                                    const float *__restrict__ dL_dpix, const float *__restrict__ dL_ddepth,
                                                    float *__restrict__ acc) {
-    __shared__ float2 s_xy[B2];
+    __shared__ float4 s_q[B2];   // staged conic in exponent form + opacity
+    __shared__ float4 s_xyc[B2]; // mean2D x, y, list position (bits), -: one 16-B stride with s_q
     __shared__ float4 s_co[B2];
-    __shared__ float4 s_q[B2];
     __shared__ float4 s_cd[B2];
     __shared__ uint32_t s_id[B2];
-    __shared__ int s_pos[B2];
     __shared__ uint32_t s_wcnt[B2 / 64];
     __shared__ uint32_t s_maxlast;
     const int tile = blockIdx.x;
@@ -1002,26 +1001,31 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
         const int2 sl = compact_slot_n<B2 / 64>(keep, tid, s_wcnt);
         if (keep) {
             s_id[sl.x] = id;
-            s_xy[sl.x] = gl;
+            // the position in the full list, staged as bits beside the mean
+            s_xyc[sl.x] = make_float4(gl.x, gl.y, __uint_as_float((uint32_t)(todo_total - 1 - prog)), 0.f);
             s_co[sl.x] = cl;
             s_q[sl.x] = conic_q(cl);
             s_cd[sl.x] = rgbd[id];
-            s_pos[sl.x] = prog;
         }
         __syncthreads();
         const int n = sl.y;
         for (int j = 0; j < n; j++) {
-            const uint32_t contributor = (uint32_t)(todo_total - 1 - s_pos[j]);  // position in the full list
-            const float2 g = s_xy[j];
+            const float4 xc = s_xyc[j];
             const float4 q = s_q[j];
-            const f2 dx = g.x - pfx;
-            const float dy = g.y - pfy;
+            const uint32_t contributor = __float_as_uint(xc.z);  // position in the full list
+            const f2 dx = xc.x - pfx;
+            const float dy = xc.y - pfy;
             const f2 power = f2{q_power(q, dx.x, dy), q_power(q, dx.y, dy)};
             const f2 G = f2{__builtin_amdgcn_exp2f(power.x), __builtin_amdgcn_exp2f(power.y)};
             const f2 alpha = f2{fminf(0.99f, q.w * G.x), fminf(0.99f, q.w * G.y)};
-            const bool act0 = in0 && contributor < last0 && power.x <= 0.f && alpha.x >= 1.f / 255.f;
-            const bool act1 = in1 && contributor < last1 && power.y <= 0.f && alpha.y >= 1.f / 255.f;
-            if (__ballot(act0 || act1) == 0ull) continue;  // wave-uniform
+            // a pixel takes the Gaussian iff it lies within the pixel's contributors (last = 0 outside
+            // the image), power <= 0 and alpha >= 1/255: the alpha gated by the first two decides, and
+            // the wave's skip test is ONE compare on the larger of the pair (a ballot of a plain
+            // compare is its lane mask; of a combined predicate the compiler materialises it first)
+            const float ga0 = (contributor < last0 && power.x <= 0.f) ? alpha.x : 0.f;
+            const float ga1 = (contributor < last1 && power.y <= 0.f) ? alpha.y : 0.f;
+            if (__ballot(fmaxf(ga0, ga1) >= 1.f / 255.f) == 0ull) continue;  // wave-uniform
+            const bool act0 = ga0 >= 1.f / 255.f, act1 = ga1 >= 1.f / 255.f;
             const float4 cd = s_cd[j];
             const float4 co = s_co[j];
             // an inactive pixel of the pair runs with alpha = 0 and G = 0: T (1 / (1 - 0) = 1), its
