@@ -73,11 +73,14 @@ constexpr int G_XE = 0, G_TE = 8, G_H = 12, G_TIN = 44, G_FWD = 48;
 constexpr int G_BH = 0, G_BG = 32, G_BWD = 36;
 // fp32 staging rows (inside the H region): XE 0..63 | TE 64..95 | TIN 96..111
 constexpr int ST_TE = 64, ST_TIN = 96;
-// relu' mask tiles: [64-point block][row / 16][64 lanes] u16 = 2 * nmask u32 words per block
+// relu' masks per 64-point block (2 * nmask u32 words): the trunk's as [layer pair][row / 16][64 lanes]
+// u32 (layer 2l in the low, 2l + 1 in the high 16 bits: one dword store per two layers), then the
+// timenet TH tiles as [row / 16][64 lanes] u16 at tile MR_TH
 constexpr int MR_TH = M_TH / 16;
 
 static_assert(G_TE == G_XE + 8 && G_H == G_TE + 4, "XE|TE|H must be contiguous");
-static_assert(G_FWD * UG * 16 + (8 * 256 + 16) * 4 <= 160 * 1024 && G_BWD * UG * 16 <= 160 * 1024, "LDS (k_fwd: + trunk biases)");
+static_assert(G_FWD * UG * 16 + (8 * 256 + 16) * 4 + NTHR * 4 + 128 <= 160 * 1024 && G_BWD * UG * 16 <= 160 * 1024,
+              "LDS (k_fwd: + trunk biases, pending relu' bits, hand-off counters)");
 static_assert(112 * BM * 4 <= 32 * UG * 16, "fp32 staging must fit the H region");
 
 // ------------------------------------------------------------------------------------------------
@@ -498,7 +501,7 @@ __global__ __launch_bounds__(256) void k_timenet(FwdArgs a) {
 // block's relu'-mask slot.
 template <bool SAVE, int NQB, bool FOLD>
 __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_t *hwr, uint32_t *hrd, const float4 *sb,
-                                          int p0, int slot) {
+                                          uint32_t *s_mpend, int p0, int slot) {
     constexpr int BMB = 16 * NQB;  // points of this block (the LDS images keep the BM-point stride)
     float *lf = reinterpret_cast<float *>(lds);
     float *stage = lf + G_H * UG * 4;  // fp32 [112][BM] feature staging (H region, before the trunk)
@@ -514,8 +517,19 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
     const size_t Ns = a.Ns;
     const __amdgpu_buffer_rsrc_t mrsrc = __builtin_amdgcn_make_buffer_rsrc(
         a.mask + (SAVE ? (size_t)slot * 2 * F.nmask : 0), 0, 0x7fffffff, 0x00020000);
-    auto store_mask = [&](uint32_t w, int mr) {  // mask tile mr (= row / 16)
+    auto store_mask = [&](uint32_t w, int mr) {  // u16 mask tile mr (= row / 16): the timenet's TH
         __builtin_amdgcn_raw_buffer_store_b16((unsigned short)w, mrsrc, lane * 2, mr * 128, 0);
+    };
+    // the trunk's: layer L's bits wait in LDS (this thread's own word) until layer L + 1 (odd) stores
+    // both as one dword: half the mask stores, and k_bwd loads one dword per two layers
+    // (tools/mlp_time.py A/B: k_fwd -0.8 %, k_bwd -2 %, profiles/r4j_mlp_mask_pairs_ab.txt)
+    auto trunk_mask = [&](uint32_t w, int L) {
+        if ((L & 1) == 0) {
+            s_mpend[64 * r + lane] = w;
+        } else {
+            __builtin_amdgcn_raw_buffer_store_b32(s_mpend[64 * r + lane] | (w << 16), mrsrc, lane * 4,
+                                                  (16 * (L >> 1) + r) * 256, 0);
+        }
     };
     DGS_STAMP(0);
     // frame-uniform t: all points of the block carry k_timenet's t0 (every wave checks the same
@@ -670,7 +684,7 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
         DGS_WSTAMP(22, L);  // per wave: GEMM end (layer 3)
         bias_relu(c, bv, true);
         if (SAVE) {
-            store_mask(relu_bits(c), 16 * L + r);
+            trunk_mask(relu_bits(c), L);
             tile16(a.saved, Ns, s_h(L) + 16 * r, p0, lane).store(c);
         }
         if (L == 3 && r == 0) DGS_STAMP(54);
@@ -718,6 +732,7 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
     // k_timenet), one float4 per (layer, 4 rows), the heads' 16 rows last; the first block's staging
     // barriers publish them
     __shared__ float4 s_bias[8 * 64 + 4];
+    __shared__ uint32_t s_mpend[NTHR];  // relu' bits of an even trunk layer, per thread (fwd_block)
     for (int i = threadIdx.x; i < 8 * 64 + 4; i += NTHR) {
         const int L = i >> 6;
         const float *bias = L == 8                ? a.fp + a.bHd
@@ -730,8 +745,8 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
     for (int b = blockIdx.x;;) {
         int nx = 0;
         if (a.queue && threadIdx.x == 0) nx = queue_take(a.queue);
-        if (b < a.nfull) fwd_block<SAVE, NQ, FOLD>(a, lds, hwr, hrd, s_bias, b * BM, b);
-        else fwd_block<SAVE, 1, FOLD>(a, lds, hwr, hrd, s_bias, a.nfull * BM + (b - a.nfull) * 16, b);
+        if (b < a.nfull) fwd_block<SAVE, NQ, FOLD>(a, lds, hwr, hrd, s_bias, s_mpend, b * BM, b);
+        else fwd_block<SAVE, 1, FOLD>(a, lds, hwr, hrd, s_bias, s_mpend, a.nfull * BM + (b - a.nfull) * 16, b);
         if (!a.queue) break;
         if (threadIdx.x == 0) s_next = nx;
         __syncthreads();  // also: the next block's staging overwrites LDS this one's heads read
@@ -760,7 +775,16 @@ struct BwdArgs {
     int nblk;
 };
 
-// relu' bits of the layer input for this wave's 16 x 64 tile, loaded ahead of the GEMM
+// relu' bits of a trunk layer's output tile (the [layer pair][row / 16][64 lanes] u32 layout),
+// loaded ahead of the GEMM
+struct MaskPre32 {
+    uint32_t *mk;
+    const uint32_t *word;  // &mask[block][layer pair][row / 16][0]
+    int shift, lane;
+    __device__ void operator()() const { *mk = word[lane] >> shift; }
+};
+
+// relu' bits of the layer input for this wave's 16 x 64 tile (u16 tiles: TH), loaded ahead of the GEMM
 struct MaskPre {
     uint32_t *mk;
     const unsigned short *tile;  // &mask[block][mr][0]
@@ -785,6 +809,10 @@ __device__ __forceinline__ void bwd_block(const BwdArgs &a, bf16x8 *lds, uint32_
     const size_t Ns = a.Ns;
     const unsigned short *mtiles = reinterpret_cast<const unsigned short *>(a.mask + (size_t)slot * 2 * F.nmask);
     auto mask_tile = [&](int mr) { return mtiles + (size_t)mr * 64; };
+    const uint32_t *mwords = a.mask + (size_t)slot * 2 * F.nmask;
+    auto trunk_pre = [&](uint32_t *mk, int L) {  // layer L's output tile of this wave (MaskPre32)
+        return MaskPre32{mk, mwords + (size_t)(16 * (L >> 1) + r) * 64, 16 * (L & 1), lane};
+    };
     if (tid < 8) {
         hwr[tid] = 0;
         hrd[tid] = 0;
@@ -815,7 +843,7 @@ __device__ __forceinline__ void bwd_block(const BwdArgs &a, bf16x8 *lds, uint32_
     {
         uint32_t mk;
         zero_tiles(c);
-        gemm<1, NQB>(a.img + (size_t)(a.tHd + r) * KSLOT, lds, G_BG, 0, lane, c, MaskPre{&mk, mask_tile(16 * 7 + r), lane});
+        gemm<1, NQB>(a.img + (size_t)(a.tHd + r) * KSLOT, lds, G_BG, 0, lane, c, trunk_pre(&mk, 7));
         mask_apply(c, mk);
         tile16(a.dz, Ns, Z_L0 + 7 * 256 + 16 * r, p0, lane).store(c);
 #pragma unroll
@@ -834,7 +862,7 @@ __device__ __forceinline__ void bwd_block(const BwdArgs &a, bf16x8 *lds, uint32_
         uint32_t mk;
         zero_tiles(c);
         gemm<8, NQB>(a.img + (size_t)(a.tL[L] + (tile0 + r) * 8) * KSLOT, lds, G_BH, 0, lane, c,
-                    MaskPre{&mk, mask_tile(16 * (L - 1) + r), lane}, HGate{hwr, hrd, 0, 2u * step, true, lane});
+                    trunk_pre(&mk, L - 1), HGate{hwr, hrd, 0, 2u * step, true, lane});
         mask_apply(c, mk);
         tile16(a.dz, Ns, Z_L0 + (L - 1) * 256 + 16 * r, p0, lane).store(c);
         lds_wait_ge(hrd + (r >> 1), 16u * step, lds_peek(hrd + (r >> 1)));
