@@ -276,10 +276,18 @@ __device__ inline void gemm(const bf16x8 *__restrict__ Aw, const bf16x8 *lds, in
     static_assert(NK >= 1, "empty GEMM");
     const int kq = lane >> 4, col = lane & 15;
     const bf16x8 *Ap = Aw + lane;
-    const bf16x8 *Bp = lds + (g0 + kq) * UG + 16 * q0 + col;
+    const int bunit = (g0 + kq) * UG + 16 * q0 + col;  // this lane's B unit at k-step 0
     constexpr int AK = KSLOT;
     constexpr int BK = KG * UG;
     auto bofs = [](int k) { return (k + (k >= SKIP ? 1 : 0)) * BK; };  // compile-time per unrolled k
+    // the B fragments of k-step k from a base formed once per k-step (the unit index is opaque to the
+    // compiler): the image spans > 64 KB, so a single base would need one address add per ds_read
+    // (a DS immediate offset is 16 bits); from the k-step base every fragment is an immediate offset
+    auto kbase = [&](int k) {
+        int u = bunit + bofs(k);
+        asm volatile("" : "+v"(u));
+        return lds + u;
+    };
     constexpr int RING = 2;
     AFrag ring[RING];
 #pragma unroll
@@ -287,7 +295,8 @@ __device__ inline void gemm(const bf16x8 *__restrict__ Aw, const bf16x8 *lds, in
         if (k < NK) ring[k] = load_a(Ap + k * AK);
     pre();
     gate.need(0, gate.peek(0));
-    AFrag b = load_b(Bp, 0);
+    const bf16x8 *Bk = kbase(0);
+    AFrag b = load_b(Bk, 0);
     f32x4 lo[NQ_];
 #pragma unroll
     for (int q = 0; q < NQ_; q++) lo[q] = zero4();
@@ -300,10 +309,11 @@ __device__ inline void gemm(const bf16x8 *__restrict__ Aw, const bf16x8 *lds, in
         for (int q = 0; q < NQ_; q++) {
             // the next tile's B fragment (or the next k-step's first) is in flight during this tile's MFMAs
             AFrag nb;
-            if (q + 1 < NQ_) nb = load_b(Bp + bofs(k), q + 1);
+            if (q + 1 < NQ_) nb = load_b(Bk, q + 1);
             else if (k + 1 < NK) {
                 gate.need(k + 1, seen);
-                nb = load_b(Bp + bofs(k + 1), 0);
+                Bk = kbase(k + 1);
+                nb = load_b(Bk, 0);
             }
             mma6(ring[k % RING], b, acc[q], lo[q]);
             if (q + 1 < NQ_ || k + 1 < NK) b = nb;
