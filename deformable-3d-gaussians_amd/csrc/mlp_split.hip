@@ -317,6 +317,10 @@ __device__ inline void gemm(const bf16x8 *__restrict__ Aw, const bf16x8 *lds, in
             }
             mma6(ring[k % RING], b, acc[q], lo[q]);
             if (q + 1 < NQ_ || k + 1 < NK) b = nb;
+            // pin the order per column tile: the next fragment's reads stay ahead of this tile's six
+            // MFMAs (left to itself the scheduler, at the 128-VGPR cap, pulls each read down to its
+            // first use and waits on it: lgkmcnt(0) in front of most MFMAs)
+            __builtin_amdgcn_sched_barrier(0);
         }
         if (k + RING < NK) ring[k % RING] = load_a(Ap + (k + RING) * AK);
         __builtin_amdgcn_sched_barrier(0);
