@@ -130,3 +130,32 @@ def test_known_answer_skip_threshold():
     assert o.color.max() == 0.0
     T, n = o.pixel_state()
     assert (T == 1.0).all() and (n == 0).all()
+
+
+def test_trace_flags_known_answers():
+    """The oracle's near-threshold reporting used by the parity tests (tests/helpers.py tail_flags):
+    or_flip_flags flags a pixel whose o G sits exactly on the 0.99 clamp; or_preprocess_flags flags a
+    Gaussian whose SH colour + 0.5 is exactly 0 (the colour clamp) and not one far from it;
+    or_pixel_gaussians flags the Gaussians blended in a masked pixel and nothing for a pixel they miss."""
+    o = _single(0.99, 3.0)  # o G = 0.99 exactly at the centre pixel (G = 1 there)
+    g, px = o.flip_flags(1e-4)
+    assert px[16, 16] and g[0]
+    far = _single(0.8, 3.0)
+    g2, px2 = far.flip_flags(1e-4)
+    assert px2[16, 16]  # power == 0 exactly at the mean's pixel: the power > 0 skip is on its threshold
+    assert not px2[16, 19] and not px2[5, 16]  # o G well inside (0, 0.99), power well below 0
+    assert not far.preprocess_flags(1e-4)[0]  # colour 1.0, straight ahead: no clamp near
+    m = np.zeros((33, 33), bool)
+    m[16, 16] = True
+    assert far.pixel_gaussians(m).tolist() == [True]
+    m[:] = False
+    m[0, 0] = True  # alpha 0.8 exp(-(16^2 + 16^2) / 18) < 1/255: not blended there
+    assert far.pixel_gaussians(m).tolist() == [False]
+    # colour channels exactly at the clamp (SH colour + 0.5 == 0)
+    s = far.s
+    sh = np.full((1, 1, 3), -0.5 / 0.28209479177387814, np.float32)
+    sh[0, 0, 0] = (1.0 - 0.5) / 0.28209479177387814
+    from oracle.raster import OracleRaster as OR
+    z = OR(s, np.array([[0, 0, 2.0]], np.float32), shs=sh, opacities=np.array([0.8], np.float32),
+           scales=np.full((1, 3), 0.2, np.float32), rotations=np.array([[1, 0, 0, 0]], np.float32))
+    assert z.preprocess_flags(1e-4)[0]
