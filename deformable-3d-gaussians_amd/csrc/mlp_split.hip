@@ -374,7 +374,14 @@ __device__ inline uint32_t relu_bits(const f32x4 (&v)[NQ_]) {
 #pragma unroll
     for (int q = 0; q < NQ_; q++)
 #pragma unroll
-        for (int i = 0; i < 4; i++) w |= (uint32_t)min(max(__float_as_int(v[q][i]), 0), 1) << (4 * q + i);
+        for (int i = 0; i < 4; i++) {
+            // v_med3_i32 + v_lshl_or_b32: 2 VALU per value (the compiler's own v_cmp + v_cndmask +
+            // v_lshl + v_or3 take ~2.4)
+            uint32_t m;
+            asm("v_med3_i32 %0, %1, 0, 1" : "=v"(m) : "v"(__float_as_int(v[q][i])));
+            if (q == 0 && i == 0) w = m;
+            else asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(w) : "v"(m), "i"(4 * q + i), "v"(w));
+        }
     return w;
 }
 
@@ -383,8 +390,13 @@ __device__ inline void mask_apply(f32x4 (&v)[NQ_], uint32_t bits) {
 #pragma unroll
     for (int q = 0; q < NQ_; q++)
 #pragma unroll
-        for (int i = 0; i < 4; i++)
-            v[q][i] = __int_as_float(__float_as_int(v[q][i]) & __builtin_amdgcn_sbfe((int)bits, 4 * q + i, 1));
+        for (int i = 0; i < 4; i++) {
+            // v_bfe_i32 + v_and (2 VALU): left to itself the compiler turns the sign-extended bit into
+            // v_and + v_cmp + v_cndmask (3 VALU per value)
+            int m;
+            asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(m) : "v"(bits), "i"(4 * q + i));
+            v[q][i] = __int_as_float(__float_as_int(v[q][i]) & m);
+        }
 }
 
 // this lane's 4 rows (16r + 4kq .. +3) of a padded bias vector
@@ -396,10 +408,7 @@ template <int NQ_>
 __device__ inline void bias_relu(f32x4 (&v)[NQ_], float4 b, bool relu) {
 #pragma unroll
     for (int q = 0; q < NQ_; q++) {
-        v[q][0] += b.x;
-        v[q][1] += b.y;
-        v[q][2] += b.z;
-        v[q][3] += b.w;
+        v[q] += f32x4{b.x, b.y, b.z, b.w};  // two v_pk_add_f32
         if (relu)
 #pragma unroll
             for (int i = 0; i < 4; i++) v[q][i] = fmaxf(v[q][i], 0.f);

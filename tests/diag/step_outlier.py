@@ -3,7 +3,7 @@ test_training_step_vs_oracle_chain): for every Gaussian outside the tolerance wi
 decision, print the GPU and oracle gradients and the oracle's per-Gaussian preprocess values, then
 re-run the GPU rasterizer ALONE on the oracle chain's own render inputs (cast to fp32) and the
 oracle's dL/dimage, to tell a raster difference from a difference in the inputs the MLP / glue fed it.
-usage: python tools/step_outlier.py [name]   (a VARIANTS name, default blender-cfg2)"""
+usage: python tests/diag/step_outlier.py [name]   (a VARIANTS name, default blender-cfg2)"""
 import math
 import os
 import sys
@@ -11,7 +11,7 @@ import sys
 import numpy as np
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(ROOT, "tests"), ROOT, os.path.join(ROOT, "deformable-3d-gaussians_amd")]
 
 from helpers import integer_ambiguity, mlp_relu_masks, tail_flags  # noqa: E402

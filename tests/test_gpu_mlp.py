@@ -10,7 +10,7 @@ the split path's error to within 2x the exact-fp32 path's error (plus 1e-6 absol
 
 Oracle gradients at N >= 1000 use the kernel's own relu' masks (helpers.mlp_relu_masks): among
 ~10^7 pre-activations a few sit within an fp32 ulp of 0 and take either sign in any fp32 forward
-(tools/mlp_diag.py found one such flip at N = 4099), which swaps a whole dZ row; the forward outputs
+(tests/diag/mlp_diag.py found one such flip at N = 4099), which swaps a whole dZ row; the forward outputs
 are still compared with the oracle's own masks, and the golden tests use the reference's.
 """
 import numpy as np

@@ -56,8 +56,8 @@ for p in $PARTS; do
           run 400 $O/stall_seg$s.txt bash tools/stall_pmc.sh
         tail -30 $O/stall_seg$s.txt
       done ;;
-    outlier)  # tools/step_outlier.py on the composed-step case OUTLIER (default blender-cfg2)
-      run 300 $O/outlier.txt python tools/step_outlier.py ${OUTLIER:-blender-cfg2}
+    outlier)  # tests/diag/step_outlier.py on the composed-step case OUTLIER (default blender-cfg2)
+      run 300 $O/outlier.txt python tests/diag/step_outlier.py ${OUTLIER:-blender-cfg2}
       tail -30 $O/outlier.txt ;;
     prof)
       TAG=$TAG run 1000 $O/prof.log bash tools/gpu_prof.sh
