@@ -25,14 +25,16 @@ def test_fused_loss_golden(golden_dir):
 
 @pytest.mark.parametrize("shape", [(3, 800, 800), (3, 61, 83), (1, 16, 16), (3, 5, 200)])
 def test_fused_loss_vs_torch(shape):
+    # the torch mirror runs on the CPU: on the GPU its conv2d goes through MIOpen, whose 1-channel
+    # backward once aborted the whole test process on a fresh box (r4v); the HIP loss is what is tested
     torch.manual_seed(0)
-    a = torch.rand(shape, device="cuda")
-    b = torch.rand(shape, device="cuda")
+    a = torch.rand(shape)
+    b = torch.rand(shape)
     x1 = a.clone().requires_grad_(True)
     ref = 0.8 * l1_loss(x1, b) + 0.2 * (1.0 - ssim(x1, b))
     (3.0 * ref).backward()
-    x2 = a.clone().requires_grad_(True)
-    loss, _, _ = l1_ssim_loss(x2, b, 0.2)
+    x2 = a.cuda().requires_grad_(True)
+    loss, _, _ = l1_ssim_loss(x2, b.cuda(), 0.2)
     (3.0 * loss).backward()
     assert abs(loss.item() - ref.item()) < 2e-6
     gr, gg = x1.grad.cpu().numpy(), x2.grad.cpu().numpy()
