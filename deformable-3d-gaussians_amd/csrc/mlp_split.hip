@@ -1565,7 +1565,6 @@ __device__ __forceinline__ void dws_run(const WJob &J, size_t Ns, const float *_
     float *slab = slabs + (size_t)blockIdx.x * SLAB;
     if (COL) {
         // bias row sums: the 8 lanes staging a row hold its partial sums (fixed xor-tree order)
-        // bias row sums: the 8 lanes staging a row hold its partial sums (fixed xor-tree order)
 #pragma unroll
         for (int f = 0; f < NSF; f++) {
             float v = bsum[f];
