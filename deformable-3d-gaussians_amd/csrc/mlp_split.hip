@@ -315,6 +315,11 @@ __device__ inline void gemm(const bf16x8 *__restrict__ Aw, const bf16x8 *lds, in
                 Bk = kbase(k + 1);
                 nb = load_b(Bk, 0);
             }
+            // the reads stay ahead of ALL six MFMAs of this tile: without this barrier the scheduler,
+            // short of registers, sank them below the tile's first four MFMAs (reusing the current
+            // fragment's registers), so the next tile's first MFMAs waited on them (k_fwd -1.4 %,
+            // profiles/r5f_mlp_bread_pin_ab.txt)
+            __builtin_amdgcn_sched_barrier(0);
             mma6(ring[k % RING], b, acc[q], lo[q]);
             if (q + 1 < NQ_ || k + 1 < NK) b = nb;
             // pin the order per column tile: the next fragment's reads stay ahead of this tile's six
