@@ -1009,9 +1009,17 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
         }
         __syncthreads();
         const int n = sl.y;
+        // the next Gaussian's mean / position and conic are read while this one is processed: the
+        // loop's first LDS reads otherwise waited out their latency at the top of every iteration
+        // (blend_bwd -3.3 % at 86 VGPRs, occupancy 6 -> 5; also prefetching the colour and conic
+        // read after the skip test was slower: profiles/r5j_blend_bwd_prefetch_ab.txt)
+        float4 xc_n = s_xyc[0], q_n = s_q[0];
         for (int j = 0; j < n; j++) {
-            const float4 xc = s_xyc[j];
-            const float4 q = s_q[j];
+            const float4 xc = xc_n;
+            const float4 q = q_n;
+            const int jn = min(j + 1, B2 - 1);  // (the batch's last iteration reads a spare slot)
+            xc_n = s_xyc[jn];
+            q_n = s_q[jn];
             const uint32_t contributor = __float_as_uint(xc.z);  // position in the full list
             const f2 dx = xc.x - pfx;
             const float dy = xc.y - pfy;
