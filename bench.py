@@ -378,8 +378,9 @@ def main():
                    + (" (raw-init heads)" if args.raw_init else " (heads at 1/100 init: steady-state deltas)"),
                    "global_batch": world, "includes_adam": not args.no_adam, "pairs_per_render": P_pairs,
                    "pair_capacity": pair_cap, "redone_steps": state["redos"],
-                   "parallelism": f"dp{world} (frame-parallel, "
-                   + ("RCCL" if world == 1 or dist.get_backend() == "nccl" else dist.get_backend()) + " grad all-reduce)"},
+                   "parallelism": "dp1 (one rank, no collective)" if world == 1 else
+                   f"dp{world} (frame-parallel, "
+                   + ("RCCL" if dist.get_backend() == "nccl" else dist.get_backend()) + " grad all-reduce)"},
         "roofline": roofline,
         # average timed launch x launches per step (every launch ran, every `period`-th was timed)
         "kernels_ms_per_step": {k: v[0] / v[1] * v[2] / args.steps for k, v in kernels.items()},

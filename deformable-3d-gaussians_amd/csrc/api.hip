@@ -142,3 +142,43 @@ extern "C" void dgs_timing_sample(int period) {
     std::lock_guard<std::mutex> lk(dgs::g_tmu);
     dgs::g_period = period < 1 ? 1 : period;
 }
+
+// ------------------------------------------------------------------------------------------------
+// Stand-in for the data-parallel step's gradient all-reduce (tools/overlap_probe.py):
+// the one-GPU box cannot run RCCL with two ranks, so the question "does a collective get compute
+// units while the persistent MLP grid runs phase 2" is asked with a kernel shaped like an RCCL ring
+// all-reduce: `nwg` workgroups of 256 threads (RCCL's channel count) streaming `passes` read-modify-
+// write sweeps over the gradient buffer (a ring all-reduce reads and writes each element about twice:
+// reduce-scatter, all-gather). Values: x <- 0.5 x + 0.5 x = x per sweep (the buffer is left unchanged
+// up to rounding, so a probe can run it on live gradients).
+// ------------------------------------------------------------------------------------------------
+namespace dgs {
+namespace {
+__global__ __launch_bounds__(256) void k_collective_standin(float4 *__restrict__ buf, long long n4, int passes) {
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (int p = 0; p < passes; p++)
+        for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+            float4 v = buf[i];
+            v.x = 0.5f * v.x + 0.5f * v.x;
+            v.y = 0.5f * v.y + 0.5f * v.y;
+            v.z = 0.5f * v.z + 0.5f * v.z;
+            v.w = 0.5f * v.w + 0.5f * v.w;
+            buf[i] = v;
+        }
+}
+}  // namespace
+}  // namespace dgs
+
+extern "C" int dgs_debug_collective_standin(float *buf, long long n, int nwg, int passes, void *stream_) {
+    if (!buf || n < 0 || nwg <= 0 || nwg > 4096 || passes <= 0 || (reinterpret_cast<uintptr_t>(buf) & 15)) {
+        dgs::set_error("dgs_debug_collective_standin: bad argument (16-byte aligned buffer, 0 < nwg <= 4096)");
+        return DGS_ERR_ARGS;
+    }
+    hipStream_t stream = (hipStream_t)stream_;
+    const long long n4 = n / 4;
+    if (n4 == 0) return DGS_OK;
+    hipLaunchKernelGGL(dgs::k_collective_standin, dim3(nwg), dim3(256), 0, stream,
+                       reinterpret_cast<float4 *>(buf), n4, passes);
+    DGS_LAUNCH_CHECK("k_collective_standin", false, stream);
+    return DGS_OK;
+}

@@ -38,6 +38,8 @@
 //    deterministic.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -1811,12 +1813,14 @@ static int *pack_map_for(const Plan &P, int flags) {
 // (the folded t_emb's 64-column ROW shape: 1.89 us per chunk vs 4.64 for a full tile, the head 1.59:
 // profiles/r3s_mlp_clock_fold.json)
 static const double kDwsShapeCost[5] = {1.0, 0.34, 0.58, 0.30, 0.41};
-static WPlan split_wplan(const Flags &F) {
+// target: workgroups of the plan (256, one per CU; the slab scratch is sized for it; fewer with
+// reserved CUs)
+static WPlan split_wplan(const Flags &F, int target = 256) {
     static const bool model = [] {  // A/B only: the MFMA-tile cost model
         const char *e = getenv("DGS_DWS_TILE_MODEL");
         return e && *e == '1';
     }();
-    return make_wplan(F, 256, 1.5, 4.0, model ? nullptr : kDwsShapeCost);
+    return make_wplan(F, target, 1.5, 4.0, model ? nullptr : kDwsShapeCost);
 }
 static int dw_split(const Flags &F, size_t Ns, const float *dz, const float *saved, float *slabs, float *const *grads,
                     hipStream_t stream);
@@ -1845,6 +1849,23 @@ static int cu_count() {
     cache[dev] = v;
     return v;
 }
+// CUs the MLP kernels leave free for concurrent work (the data-parallel step's gradient all-reduce runs
+// on its own stream under the network backward): the persistent k_fwd / k_bwd grids
+// launch cu_count() - reserve workgroups (one per CU) and k_dws's plan spans 256 - reserve workgroups.
+// dgs_mlp_set_reserved_cus / DGS_MLP_RESERVE_CUS; default 0.
+static std::atomic<int> g_reserve_cus{-1};
+static int reserved_cus() {
+    int v = g_reserve_cus.load();
+    if (v < 0) {
+        const char *e = getenv("DGS_MLP_RESERVE_CUS");
+        int want = e ? atoi(e) : 0;
+        want = want < 0 ? 0 : want > 64 ? 64 : want;
+        g_reserve_cus.compare_exchange_strong(v, want);
+        v = g_reserve_cus.load();
+    }
+    return v;
+}
+static int mlp_cus() { return std::max(1, cu_count() - reserved_cus()); }
 static Blocks block_split(int N) {
     const int nb = div_up(N, BM);
     static const bool off = [] {
@@ -1852,7 +1873,7 @@ static Blocks block_split(int N) {
         return e && e[0] == '1';
     }();
     if (off || nb == 0) return {nb, 0};
-    const int ncu = cu_count();
+    const int ncu = mlp_cus();
     const int rounds = div_up(nb, ncu), last = nb - ncu * (rounds - 1);
     if (rounds < 2 || last > TAIL_MAX_LAST || 4 * last > ncu) return {nb, 0};
     return {nb - last, 4 * last};
@@ -1893,7 +1914,7 @@ static float *timenet_scratch(hipStream_t stream) {
     if (!b && hipMalloc(&b, TC_FLOATS * sizeof(float)) != hipSuccess) b = nullptr;
     return b;
 }
-static int persistent_grid(int nblk, const uint32_t *queue) { return queue ? std::min(nblk, cu_count()) : nblk; }
+static int persistent_grid(int nblk, const uint32_t *queue) { return queue ? std::min(nblk, mlp_cus()) : nblk; }
 
 static size_t mask_words(const Flags &F, size_t Ns) {
     const size_t nb = Ns / BM;
@@ -2075,7 +2096,7 @@ static int dw_split_once(const Flags &F, size_t Ns, const float *dz, const float
                          float *const *grads, hipStream_t stream) {
     if ((size_t)WT * Ns * 4 >= 0x7fffffffull)  // 32-bit byte offsets of a 256-row operand
         return mlp::dw_fp32(F, Ns, dz, saved, slabs, grads, stream);
-    const WPlan W = split_wplan(F);
+    const WPlan W = split_wplan(F, std::max(32, 256 - reserved_cus()));
     for (int q = 0; q < W.jobs.n; q++) {  // the shapes k_dws instantiates
         const WJob &j = W.jobs.j[q];
         const bool ok = (j.krows == 256 && (j.nrows == 256 || j.nrows == 32)) ||
@@ -2142,6 +2163,9 @@ extern "C" int dgs_debug_clock(int k, int n, unsigned long long *out) {
     return 0;
 }
 #endif
+
+extern "C" void dgs_mlp_set_reserved_cus(int k) { mlps::g_reserve_cus.store(k < 0 ? 0 : k > 64 ? 64 : k); }
+extern "C" int dgs_mlp_reserved_cus(void) { return mlps::reserved_cus(); }
 
 extern "C" long long dgs_debug_guard_expiries(void) {
     uint32_t v = 0;

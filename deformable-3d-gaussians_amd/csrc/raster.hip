@@ -2334,6 +2334,7 @@ extern "C" void dgs_debug_set_pair_cap(int device, int cap) {
 extern "C" int dgs_debug_pair_cap(int device) { return pair_cap_get(device); }
 
 extern "C" void dgs_debug_set_blend_seg(int on) { g_blend_seg.store(on ? 1 : 0); }
+extern "C" int dgs_debug_get_blend_seg(void) { return blend_segmented() ? 1 : 0; }
 
 extern "C" void dgs_debug_set_binning(int mode) { g_binning.store(mode == 1 ? 1 : 0); }
 

@@ -62,6 +62,10 @@ _SIGS = {
     "dgs_raster_deferred_overflows": ([], ctypes.c_longlong),
     "dgs_debug_set_binning": ([I], None),
     "dgs_debug_set_blend_seg": ([I], None),
+    "dgs_debug_get_blend_seg": ([], I),
+    "dgs_mlp_set_reserved_cus": ([I], None),
+    "dgs_mlp_reserved_cus": ([], I),
+    "dgs_debug_collective_standin": ([P, ctypes.c_longlong, I, I, P], I),
     "dgs_timing_enable": ([I], None),
     "dgs_timing_query": ([ctypes.c_char_p, ctypes.POINTER(I)], ctypes.c_double),
     "dgs_timing_reset": ([], None),

@@ -8,6 +8,7 @@ multi-tensor HIP kernel; a CPU-only optimizer (host-side tests of densification)
 `step_all(opt_a, opt_b, ...)` updates several optimizers in the same single launch.
 """
 import math
+import weakref
 
 import torch
 
@@ -93,8 +94,22 @@ class Adam(torch.optim.Adam):
 # step_all's launch tables for a fixed set of (parameter, gradient) buffers: a training step with the
 # native step (deformgs/native_step.py) keeps the same gradient buffers every iteration, so after the
 # first step only the step counts and the per-tensor bias corrections change (~40 us of host time
-# instead of ~200 us of per-parameter Python)
-_FAST = {}
+# instead of ~200 us of per-parameter Python). The cache lives on the first optimizer of the set
+# (`_dgs_fast`) and refers to the others weakly, so it never keeps parameters or Adam moments alive
+# after training; `clear_fast_cache` drops it explicitly.
+
+
+def _fast_get(hip, key):
+    fast = getattr(hip[0], "_dgs_fast", None)
+    if fast is None or fast["key"] != key or any(r() is not o for r, o in zip(fast["refs"], hip)):
+        return None
+    return fast
+
+
+def clear_fast_cache(*optimizers):
+    for o in optimizers:
+        if hasattr(o, "_dgs_fast"):
+            o._dgs_fast = None
 
 
 def _signature(optimizers):
@@ -105,8 +120,8 @@ def _signature(optimizers):
                 g, st = p.grad, opt.state.get(p)
                 m = st.get("exp_avg") if st else None
                 v = st.get("exp_avg_sq") if st else None
-                sig.append((p.data_ptr(), None if g is None else g.data_ptr(), None if m is None else m.data_ptr(),
-                            None if v is None else v.data_ptr()))
+                sig.append((p.data_ptr(), p.numel(), None if g is None else g.data_ptr(),
+                            None if m is None else m.data_ptr(), None if v is None else v.data_ptr()))
     return tuple(sig)
 
 
@@ -122,7 +137,7 @@ def step_all(*optimizers):
         return
     key = tuple(id(o) for o in hip)
     sig = _signature(hip)
-    fast = _FAST.get(key)
+    fast = _fast_get(hip, key)
     stream = _lib.stream_ptr()
     if fast is not None and fast["sig"] == sig and all(float(t) == c for t, c in fast["steps"]):
         counts = {}
@@ -152,7 +167,7 @@ def step_all(*optimizers):
         arr = (_lib.AdamTensor * len(ds))(*ds)
         launch.append(((b1, b2, eps), arr))
         _lib.check(lib.dgs_adam_step(len(ds), arr, b1, b2, eps, stream), "adam_step")
-    _FAST.pop(key, None)
+    clear_fast_cache(*hip)
     if not keep and all(p.grad is not None for o in hip for g in o.param_groups for p in g["params"]):
         # cacheable: every parameter stepped with its own contiguous gradient; the tables follow the
         # entry order of _collect (group by group, parameter by parameter)
@@ -170,7 +185,6 @@ def step_all(*optimizers):
             pos[cfg].append(ents[i])
         for (cfg, arr) in launch:
             tables.append((arr, pos[cfg]))
-        _FAST.clear()  # one cached set (the running training loop); holds its optimizers alive
-        _FAST[key] = {"sig": _signature(hip), "steps": [(t, float(t)) for t in steps.values()], "tables": tables,
-                      "launch": launch, "refs": hip}
+        hip[0]._dgs_fast = {"key": key, "sig": _signature(hip), "steps": [(t, float(t)) for t in steps.values()],
+                            "tables": tables, "launch": launch, "refs": [weakref.ref(o) for o in hip]}
     del keep

@@ -94,6 +94,15 @@ class NativeStep:
         if key == self.key:
             return
         lib, dev, N = self.lib, gp[0].device, gp[0].shape[0]
+        # release the previous set first (densification / opacity resets would otherwise briefly hold
+        # two sets of the several-KB-per-Gaussian MLP buffers); the parameters' .grad views of the old
+        # flat buffers are dropped with them (the next step hands out the new ones)
+        if self.key is not None:
+            for p in getattr(self, "params", []):
+                if p.grad is not None and any(p.grad is g for g in self.grads):
+                    p.grad = None
+        self.buf = self.gflat = self.mflat = self.ggrads = self.mgrads = self.grads = self.args = None
+        self.key = None
         e = lambda *s: torch.empty(s, dtype=torch.float32, device=dev)  # noqa: E731
         from .deform_network import FLAG_EXACT_FP32
         flags = net.flags | (FLAG_EXACT_FP32 if net.exact_fp32 else 0)

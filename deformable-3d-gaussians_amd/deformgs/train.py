@@ -211,6 +211,9 @@ def training(dataset, opt, pipe, testing_iterations, saving_iterations, scene, g
     finally:
         set_fused(True)
         gaussians.row_select = None
+        # the one-launch Adam's cached tables refer to the optimizers' groups: drop them with the loop
+        from .adam import clear_fast_cache
+        clear_fast_cache(getattr(gaussians, "optimizer", None), getattr(deform, "optimizer", None))
 
 
 class SyntheticScene:

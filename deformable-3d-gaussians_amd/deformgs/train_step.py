@@ -63,8 +63,13 @@ def train_step(gaussians, deform, cam, gt_image, pipe, background, is_6dof=False
     Returns (loss, render package, redone)."""
     multi = allreduce is not None and allreduce.world() > 1
     single = not dist.is_initialized() or dist.get_world_size() == 1
-    if (multi or single) and getattr(deform.deform, "is_6dof", False) == bool(is_6dof) and \
-            native_step.usable(gaussians, deform, pipe, gt_image):
+    if multi and gt_image.is_cuda and not gt_image.is_contiguous():
+        gt_image = gt_image.contiguous()  # a per-step input: never a reason for ranks to take different paths
+    local = (multi or single) and getattr(deform.deform, "is_6dof", False) == bool(is_6dof) and \
+        native_step.usable(gaussians, deform, pipe, gt_image)
+    if multi:
+        local = agreed_native_path(local, gaussians, deform, pipe, gt_image, is_6dof, allreduce.group)
+    if local:
         # one C call per step (dgs_train_step): no autograd engine, no per-step allocations but the
         # image and the loss (deformgs/native_step.py); several ranks: two calls around the
         # Gaussian gradient all-reduce
@@ -101,6 +106,39 @@ def train_step(gaussians, deform, cam, gt_image, pipe, background, is_6dof=False
     if multi:
         allreduce()
     return loss, pkg, redone
+
+
+_AGREED = {"key": None, "native": None}
+
+
+def agreed_native_path(local, gaussians, deform, pipe, gt_image, is_6dof, group=None):
+    """The native-vs-autograd choice of a data-parallel step, the same on every rank (the two paths
+    issue different collectives: ranks split between them would hang in RCCL or fail in gloo).
+
+    The ranks MIN-reduce their local `native_step.usable` flag whenever a RANK-INVARIANT key changes —
+    the Gaussian count, the image size, the network's configuration, the pipe / renderer switches —
+    so every rank issues that 1-int collective at the same step; between such changes the agreed
+    choice is reused with no collective. A rank that cannot take an agreed native path without a
+    key change (a condition only it sees, e.g. a misaligned parameter) raises instead of issuing
+    mismatched collectives; a rank that could but the others cannot simply takes the autograd path."""
+    from .renderer import _FUSED, _HONOR_OVERRIDE, _SPLIT_SH
+    net = deform.deform
+    H, W = (int(gt_image.shape[-2]), int(gt_image.shape[-1])) if gt_image.dim() >= 2 else (0, 0)
+    key = (int(gaussians._xyz.shape[0]), H, W, bool(is_6dof), getattr(net, "flags", None),
+           bool(getattr(net, "exact_fp32", False)), native_step.enabled(), bool(_FUSED["on"]), bool(_SPLIT_SH),
+           bool(_HONOR_OVERRIDE["on"]), bool(getattr(pipe, "compute_cov3D_python", False)),
+           bool(getattr(pipe, "convert_SHs_python", False)), bool(getattr(pipe, "debug", False)),
+           int(gaussians._features_rest.shape[1]))
+    if key != _AGREED["key"]:
+        dev = gt_image.device if (gt_image.is_cuda and dist.get_backend(group) == "nccl") else "cpu"
+        flag = torch.tensor([1 if local else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+        _AGREED["key"], _AGREED["native"] = key, bool(flag.item())
+    if _AGREED["native"] and not local:
+        raise RuntimeError(f"rank {dist.get_rank()}: the native training step is not usable on this rank while the "
+                           "ranks agreed on it (a rank-local condition changed without a change of the Gaussian "
+                           "count / image size / configuration): the ranks' collectives would not match")
+    return _AGREED["native"]
 
 
 def deferred_overflowed():

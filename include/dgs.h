@@ -137,6 +137,8 @@ long long dgs_debug_binning_redos(void);
  * 0 = one serial back-to-front replay per tile (k_blend_bwd2). Default from DGS_BLEND_SEG. Applies to
  * forwards issued after the call. */
 void dgs_debug_set_blend_seg(int on);
+/* The blend-backward mode in effect (DGS_BLEND_SEG or the last dgs_debug_set_blend_seg): 1 = segmented. */
+int dgs_debug_get_blend_seg(void);
 /* host nanoseconds spent waiting for num_rendered (and the number of waits) since process start */
 long long dgs_debug_count_wait_ns(long long *waits);
 /* dL/dscales convention. 0 (default) = the upstream CUDA op's: the gradient w.r.t. the modified scale
@@ -147,6 +149,17 @@ void dgs_raster_set_exact_scale_grad(int on);
  * current device since process start: must be 0; a non-zero count means MLP outputs / gradients of
  * some launch are invalid (GPU tests assert it stays 0). -1 if the counter could not be read. */
 long long dgs_debug_guard_expiries(void);
+/* CUs the deformation-MLP kernels leave free for concurrent work on other streams (the data-parallel
+ * step's gradient all-reduce under the network backward): the persistent k_fwd / k_bwd
+ * grids launch (CUs - k) workgroups and k_dws's plan spans (256 - k). 0..64; default
+ * DGS_MLP_RESERVE_CUS or 0. No reference counterpart (the reference is single-GPU). */
+void dgs_mlp_set_reserved_cus(int k);
+int dgs_mlp_reserved_cus(void);
+/* Diagnostic: a stand-in for an RCCL ring all-reduce on `stream` (nwg workgroups of 256 threads,
+ * `passes` read-modify-write sweeps over n floats of a 16-byte aligned buffer; values unchanged up to
+ * rounding), for measuring on one GPU whether a collective overlaps the network backward
+ * (tools/overlap_probe.py). */
+int dgs_debug_collective_standin(float *buf, long long n, int nwg, int passes, void *stream);
 /* The binning's stable LSD radix sort on device buffers (tests only): sorts n (key, value) pairs by
  * key bits [0, end_bit) (32-bit keys when key_bytes == 4, 16-bit when 2; end_bit <= 8 * key_bytes)
  * using (k1, v1) as scratch; the result is left in (k0, v0). Stream-ordered. */

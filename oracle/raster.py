@@ -177,7 +177,8 @@ class OracleRaster:
         rc = lib().or_backward(self._st, _ptr(dc), _ptr(dd), _ptr(g["means3D"]), _ptr(g["means2D"]),
                                _ptr(g["means2D_densify"]), _ptr(g["colors"]), _ptr(g["opacities"]),
                                _ptr(g["cov3D"]), _ptr(g["shs"]), _ptr(g["scales"]), _ptr(g["rotations"]))
-        assert rc == 0
+        if rc != 0:
+            raise MemoryError("oracle raster backward: host allocation failed")
         return g
 
     def __del__(self):

@@ -397,6 +397,7 @@ int or_backward(void *p, const float *dL_dpix, const float *dL_ddepth, float *dL
     int NCH = T < 32 ? (T > 0 ? T : 1) : 32;
     while (NCH > 1 && (size_t)NCH * N * NF * sizeof(float) > ((size_t)768 << 20)) NCH /= 2;
     float *chunk_acc = (float *)calloc((size_t)NCH * N * NF + 1, sizeof(float));
+    if (!chunk_acc) return -1; /* out of host memory: the caller raises */
     const float hx = 0.5f * W, hy = 0.5f * H;
 #pragma omp parallel for schedule(dynamic, 1)
     for (int ch = 0; ch < NCH; ch++) {
@@ -473,6 +474,10 @@ int or_backward(void *p, const float *dL_dpix, const float *dL_ddepth, float *dL
     float *g_op = (float *)calloc((size_t)N + 1, sizeof(float));
     float *g_col = (float *)calloc((size_t)N * 3 + 1, sizeof(float));
     float *g_dep = (float *)calloc((size_t)N + 1, sizeof(float));
+    if (!g_m2 || !g_dens || !g_con || !g_op || !g_col || !g_dep) {
+        free(chunk_acc); free(g_m2); free(g_dens); free(g_con); free(g_op); free(g_col); free(g_dep);
+        return -1;
+    }
 #pragma omp parallel for schedule(static)
     for (int i = 0; i < N; i++) {
         float r[NF] = {0};
@@ -813,7 +818,11 @@ int or_flip_flags(void *p, float eps, uint8_t *gflag, uint8_t *pflag) {
                 flagged++;
                 if (pflag) pflag[py * W + px] = 1;
                 int end = stop + 1 < hi ? stop + 1 : hi - 1;
-                for (int j = first; j <= end; j++) gflag[st->vals[j]] = 1; /* benign race: all write 1 */
+                for (int j = first; j <= end; j++) {
+                    /* several threads may flag one Gaussian: an atomic store (all store 1) */
+#pragma omp atomic write
+                    gflag[st->vals[j]] = 1;
+                }
             }
     }
     return flagged;

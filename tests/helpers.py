@@ -186,7 +186,7 @@ def check_integer_outputs(o, radii_gpu, nr_gpu, stats=None):
     return amb
 
 
-def tail_flags(o, amb=None, eps=1e-4):
+def tail_flags(o, amb=None, eps=1e-5):
     """Gaussians (and pixels) whose gradient (value) may legitimately differ from the oracle's by
     more than rounding: a near-threshold blend decision in their pixel (oracle or_flip_flags), a
     near-threshold gradient mask of their own preprocess (the EWA frustum clamp, the SH colour clamp:
@@ -201,41 +201,76 @@ def tail_flags(o, amb=None, eps=1e-4):
     return g, px
 
 
-def check_image(img, o, pflag, stats=None, name="image"):
+# The tail sets: the checks ASSERT against the near-threshold decisions within a relative 1e-5 of
+# their threshold (1e-4 flagged ~47 % of the Gaussians at the bench size, while every
+# recorded outlier already sat within 1e-5); the 1e-4 and 1e-6 sets are computed too and their flagged
+# and unexplained counts recorded beside it (how close to their thresholds the outliers sit).
+ASSERT_EPS = 1e-5
+RECORD_EPS = (1e-4, 1e-5, 1e-6)
+# Pixel VALUES are held to the 1e-4 set: a pixel's transmittance carries the relative error of every
+# (1 - alpha) factor in front of it, which is the alpha's error times alpha / (1 - alpha) (up to 99x at
+# the 0.99 clamp), so the T (1 - alpha) < 1e-4 stop of two fp32 implementations can differ for inputs
+# 1e-5 .. 1e-4 from the threshold (measured: at 55k-100k @ 800^2, 1-5 of the 6-14 pixels off by > 1e-4
+# sit there; none outside the 1e-4 set). The gradients are held to the 1e-5 set.
+IMAGE_EPS = 1e-4
+
+
+def tail_sets(o, amb=None):
+    """{eps: (gflag, pflag)} for RECORD_EPS."""
+    return {e: tail_flags(o, amb, e) for e in RECORD_EPS}
+
+
+def check_image(img, o, sets, stats=None, name="image"):
     """mean |err| <= 1e-5, >= 99.9 % of values within 1e-4, and every value off by more than 1e-4 at
-    a pixel with a near-threshold decision."""
+    a pixel with a near-threshold decision (sets[IMAGE_EPS])."""
     err = np.abs(np.asarray(img) - o.color)
     bad = (err > 1e-4).any(0)
+    pflag = sets[IMAGE_EPS][1]
     if stats is not None:
         stats[name] = dict(mean=float(err.mean()), bad_px=int(bad.sum()), unexplained=int((bad & ~pflag).sum()),
                            flagged_px=int(pflag.sum()))
+        for e, (_, pf) in sets.items():
+            stats[name][f"flagged_px@{e:g}"] = int(pf.sum())
+            stats[name][f"unexplained@{e:g}"] = int((bad & ~pf).sum())
     assert err.mean() <= 1e-5 and (err <= 1e-4).mean() >= 0.999, err.mean()
     assert not (bad & ~pflag).any(), ("image values off by > 1e-4 at pixels without a near-threshold decision",
                                       np.argwhere(bad & ~pflag)[:10])
 
 
-def check_gaussian_grad(a, b, gflag, name, stats=None, atol_frac=2e-3, rtol=1e-3, tighter=None):
-    """Per-Gaussian gradient rows a (GPU) vs b (oracle): >= 99.5 % of elements within atol_frac of
-    the tensor's max + rtol relative, and every element outside that on a flagged Gaussian
-    (tail_flags). tighter: {label: flags} of narrower flag sets whose unexplained counts are only
-    recorded in stats (how close the outliers sit to their thresholds)."""
+def check_gaussian_grad(a, b, sets, name, stats=None, atol_frac=2e-3, rtol=1e-3, max_bad_frac=1e-4, min_bad=4,
+                        max_ratio=10.0):
+    """Per-Gaussian gradient rows a (GPU) vs b (oracle), tolerance atol_frac of the tensor's max +
+    rtol relative (float32 kernels vs the oracle). Asserted (bars at what is measured):
+      - at most max_bad_frac (1e-4) of the elements outside the tolerance (at least min_bad = 4
+        elements allowed, so a single near-threshold Gaussian of a few-thousand-Gaussian case counts
+        as what it is: one Gaussian);
+      - every element outside the tolerance on a Gaussian of the 1e-5 tail set (sets[ASSERT_EPS]);
+      - no element off by more than max_ratio (10) times its tolerance, flagged or not (a single
+        alpha / transmittance decision moves a gradient by a bounded amount; measured <= 2.9).
+    sets: {eps: (gflag, pflag)} (tail_sets); flagged and unexplained counts recorded for every eps."""
+    gflag = sets[ASSERT_EPS][0]
     N = gflag.shape[0]
     a = np.asarray(a, np.float64).reshape(N, -1)
     b = np.asarray(b, np.float64).reshape(N, -1)
     tol = atol_frac * max(np.abs(b).max(), 1e-30) + rtol * np.abs(b)
-    bad = np.abs(a - b) > tol
+    ratio = np.abs(a - b) / tol
+    bad = ratio > 1.0
     bad_g = bad.any(1)
     unexplained = bad_g & ~gflag
+    nbad = int(bad.sum())
+    worst = float(ratio.max())
     if stats is not None:
-        worst = float((np.abs(a - b) / tol)[unexplained].max()) if unexplained.any() else 0.0
-        stats[name] = dict(bad_frac=float(bad.mean()), bad_gauss=int(bad_g.sum()),
-                           flagged=int(gflag.sum()), unexplained=int(unexplained.sum()), worst_unexplained=worst,
-                           worst_ratio=float((np.abs(a - b) / tol).max()), rel=rel_err(a, b))
-        for label, fl in (tighter or {}).items():
-            stats[name]["unexplained@" + label] = int((bad_g & ~fl).sum())
-    assert 1.0 - bad.mean() >= 0.995, (name, rel_err(a, b))
+        stats[name] = dict(bad_frac=float(bad.mean()), bad_elems=nbad, bad_gauss=int(bad_g.sum()),
+                           flagged=int(gflag.sum()), unexplained=int(unexplained.sum()),
+                           worst_unexplained=float(ratio[unexplained].max()) if unexplained.any() else 0.0,
+                           worst_ratio=worst, rel=rel_err(a, b))
+        for e, (gf, _) in sets.items():
+            stats[name][f"flagged@{e:g}"] = int(gf.sum())
+            stats[name][f"unexplained@{e:g}"] = int((bad_g & ~gf).sum())
+    assert nbad <= max(max_bad_frac * bad.size, min_bad), (name, nbad, bad.size, rel_err(a, b))
     assert not unexplained.any(), (name, "gradient outside tolerance on Gaussians with no near-threshold decision",
                                    np.nonzero(unexplained)[0][:10])
+    assert worst <= max_ratio, (name, "gradient off by more than 10x its tolerance", worst)
 
 
 def write_stats(tag, stats):

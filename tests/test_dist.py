@@ -349,3 +349,82 @@ def test_native_data_parallel_step_sequence():
         assert c1 == [("p1", False)] and not r1  # warm-up: no phase 2, no network collective
         torch.testing.assert_close(g1a, torch.full((3, 2), 1.5))
         torch.testing.assert_close(m1, torch.full((4,), -1.0))
+
+
+def _path_agreement_case(rank, world):
+    """train_step's native-vs-autograd choice with several ranks: the ranks MIN-reduce
+    their local native_step.usable flag when a rank-invariant key changes (Gaussian count, image size,
+    configuration) and reuse it otherwise; a rank forced onto the fallback pulls every rank onto the
+    autograd path (matching collectives) instead of splitting them; a rank that loses the native path
+    without a key change raises instead of issuing mismatched collectives. C calls stubbed (CPU)."""
+    from deformgs import native_step, train_step as ts
+    usable = {"v": rank == 0}
+    calls = []
+    native_step.usable = lambda *a, **k: usable["v"]
+
+    class StubNative:
+        def __init__(self, gs, deform):
+            self.deform = deform
+
+        def step_data_parallel(self, *a, **k):
+            calls.append("native")
+            return torch.tensor(0.0), {}, False
+
+    native_step.NativeStep = StubNative
+
+    def stub_fb(*a, **k):
+        calls.append("autograd")
+        return torch.tensor(0.0), {}
+
+    ts.forward_backward = stub_fb
+
+    class AR:
+        group = None
+
+        def world(self):
+            return world
+
+        def arm(self):
+            pass
+
+        def __call__(self):
+            pass
+
+    net = types.SimpleNamespace(is_6dof=False, flags=0, exact_fp32=False)
+    deform = types.SimpleNamespace(deform=net)
+    gt = torch.zeros(3, 8, 8)
+
+    def gaussians(n):
+        return types.SimpleNamespace(_xyz=torch.zeros(n, 3), _features_rest=torch.zeros(n, 15, 3))
+
+    gs = gaussians(10)
+    out = []
+    for _ in range(2):  # rank 1 cannot: both take the autograd path; the second step reuses the choice
+        ts.train_step(gs, deform, None, gt, types.SimpleNamespace(), None, deferred_count=False, allreduce=AR())
+    out.append(list(calls))
+    calls.clear()
+    usable["v"] = True  # both could now, but the key is unchanged: the agreed choice stays
+    ts.train_step(gs, deform, None, gt, types.SimpleNamespace(), None, deferred_count=False, allreduce=AR())
+    out.append(list(calls))
+    calls.clear()
+    gs = gaussians(12)  # densification (same count on every rank): agreed again, both native
+    ts.train_step(gs, deform, None, gt, types.SimpleNamespace(), None, deferred_count=False, allreduce=AR())
+    out.append(list(calls))
+    calls.clear()
+    usable["v"] = rank == 0  # rank 1 loses the path without a key change: it raises
+    try:
+        ts.train_step(gs, deform, None, gt, types.SimpleNamespace(), None, deferred_count=False, allreduce=AR())
+        out.append(list(calls))
+    except RuntimeError as e:
+        out.append("raised" if "collectives would not match" in str(e) else repr(e))
+    return out
+
+
+def test_native_path_choice_is_agreed_across_ranks():
+    out = _run(_path_agreement_case)
+    for rank in (0, 1):
+        a, b, c, d = out[rank]
+        assert a == ["autograd", "autograd"]
+        assert b == ["autograd"]
+        assert c == ["native"]
+        assert d == (["native"] if rank == 0 else "raised")

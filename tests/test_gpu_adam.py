@@ -77,7 +77,7 @@ def test_adam_two_optimizers_one_launch():
 def test_adam_persistent_gradient_buffers_fast_path():
     """The native training step keeps each parameter's gradient in the same buffer every iteration;
     step_all then reuses its launch tables and only updates the step counts and bias corrections
-    (deformgs/adam.py _FAST). With the learning rates changing every step and the gradients rewritten
+    (deformgs/adam.py: the tables cached on the optimizer, `_dgs_fast`). With the learning rates changing every step and the gradients rewritten
     in place, the result must still be torch.optim.Adam's; a replaced parameter (densification)
     drops back to the full path."""
     from deformgs import adam as adam_mod
@@ -96,14 +96,17 @@ def test_adam_persistent_gradient_buffers_fast_path():
             buf.copy_(torch.randn(a.shape, generator=gen).to(dev))
             a.grad = buf
             b.grad = buf.clone()
-        before = [id(v) for v in adam_mod._FAST.values()]
+        before = getattr(ours, "_dgs_fast", None)
         step_all(ours)
-        hits += int(bool(before) and before == [id(v) for v in adam_mod._FAST.values()])
+        hits += int(before is not None and getattr(ours, "_dgs_fast", None) is before)
         ref.step()
         for go, gr in zip(ours.param_groups, ref.param_groups):
             go["lr"] *= 0.9
             gr["lr"] *= 0.9
     assert hits >= 6, hits  # every step after the first reused the tables
+    # the cache refers to the optimizer's own groups only; clearing it (end of training()) drops it
+    adam_mod.clear_fast_cache(ours)
+    assert ours._dgs_fast is None
     torch.cuda.synchronize()
     for a, b in zip(pa, pb):
         torch.testing.assert_close(a.detach(), b.detach(), rtol=1e-5, atol=1e-6)

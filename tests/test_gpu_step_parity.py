@@ -15,11 +15,16 @@
                   (gaussian_renderer/__init__.py:71-76), gradient into the non-detached xyz too;
       config 5:   NeRF-DS non-blender network (no timenet, 21-channel t PE) with a non-zero ast_noise
                   added to the frame time (train_baseline.py:107-112), 55k @ 800^2.
-Tolerances (floating point, fp32 kernels vs an fp64/fp32 oracle): loss within 2e-6 relative; image
-and integer outputs as test_gpu_raster; Gaussian gradients: >= 99.5 % of elements within 2e-3 of the
-tensor's max + 1e-3 relative and every element outside that on a Gaussian with a near-threshold
-decision (the rasterizer's, or the L1 term's sign: a pixel where the GPU's and the oracle's images lie
-on different sides of the target flags the Gaussians blended there); MLP gradients (sums over all points): max error within 2e-3 of the tensor's max. The MLP
+      bench-100k: the configuration bench.py times (synth-100k, 800^2, its camera and target).
+Every variant runs through BOTH the native step driver (train_step -> dgs_train_step, what bench.py
+times) and the autograd path.
+Tolerances (floating point, fp32 kernels vs an fp64/fp32 oracle): loss within 2e-6 relative plus twice
+the reference's own fp32 rounding of the loss on the oracle's image (bench-100k: ~1e-5); image
+and integer outputs as test_gpu_raster; Gaussian gradients: tolerance 2e-3 of the tensor's max + 1e-3
+relative, at most 1e-4 of the elements outside it, each on a Gaussian with a decision within 1e-5 of
+its threshold (the rasterizer's, or the L1 term's sign: a pixel where the GPU's and the oracle's images
+lie on different sides of the target flags the Gaussians blended there), none beyond 10x the
+tolerance; MLP gradients (sums over all points): max error within 5e-4 of the tensor's max. The MLP
 oracle's backward uses the kernel's own relu' masks (a pre-activation within an ulp of 0 can take
 either sign in fp32), and every mask that differs from the oracle's own z > 0 is checked to sit on a
 pre-activation within 2e-5 of its layer's max |z| of zero.
@@ -32,7 +37,7 @@ import torch
 
 from conftest import gpu_available
 from helpers import (check_gaussian_grad, check_image, check_integer_outputs, mlp_relu_masks, oracle_run, rel_err,
-                     scene, tail_flags, write_stats)
+                     scene, tail_sets, write_stats)
 
 pytestmark = pytest.mark.gpu
 
@@ -132,21 +137,33 @@ VARIANTS = [
     ("blender-cfg3", 55000, 800, True, False, 0.0),
     ("6dof-cfg4", 78600, 800, True, True, 0.0),
     ("nonblender-cfg5", 55000, 800, False, False, 0.0137),
+    # the configuration bench.py times: synth-100k (seed 0) at 800^2, blender network, heads at 1/100,
+    # one of its cameras, its target (that camera's initial render + N(0, 0.02), clamped)
+    ("bench-100k", 100_000, 800, True, False, 0.0),
 ]
+PATHS = ["native", "autograd"]
 
 
 @pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("name,N,res,is_blender,is_6dof,ast_noise", VARIANTS, ids=[v[0] for v in VARIANTS])
-def test_training_step_vs_oracle_chain(name, N, res, is_blender, is_6dof, ast_noise):
+def test_training_step_vs_oracle_chain(name, N, res, is_blender, is_6dof, ast_noise, path):
+    """path "native": train_step() -> NativeStep -> dgs_train_step (csrc/step.hip), the path bench.py
+    times (asserted: the GaussianModel carries its NativeStep); "autograd": forward_backward through the
+    PyTorch autograd engine. Both with the deferred pair count, after one synchronous step that teaches
+    the speculative capacity."""
+    from deformgs import native_step
     from deformgs.arguments import OptimizationParams, PipelineParams
     from deformgs.deform_model import DeformModelBaseline
     from deformgs.gaussian_model import GaussianModel
+    from deformgs.renderer import render
     from deformgs.synthetic import synth_camera, synth_gaussians
-    from deformgs.train_step import deferred_overflowed, drop_grads, forward_backward
+    from deformgs.train_step import deferred_overflowed, drop_grads, forward_backward, train_step
     from oracle import mlp_ref
     from weights import mlp_weights
     dev = torch.device("cuda", 0)
-    g = synth_gaussians(N, seed=2, device=dev)
+    bench = name == "bench-100k"
+    g = synth_gaussians(N, seed=0 if bench else 2, device=dev)
     gs = GaussianModel(3)
     gs.from_tensors(g["xyz"], g["features_dc"], g["features_rest"], g["scaling"], g["rotation"], g["opacity"])
     gs.training_setup(OptimizationParams())
@@ -157,9 +174,18 @@ def test_training_step_vs_oracle_chain(name, N, res, is_blender, is_6dof, ast_no
             w[k] = (w[k] * 0.01).astype(np.float32)
     deform.deform.load_state_dict({k: torch.from_numpy(v) for k, v in w.items()})
     deform.train_setting(OptimizationParams())
-    cam = synth_camera(res, res, index=1, fid=0.37, device=dev)
-    gt = torch.rand((3, res, res), generator=torch.Generator().manual_seed(9)).to(dev)
     pipe, bg = PipelineParams(), torch.zeros(3, device=dev)
+    if bench:  # bench.py's second camera (index 1, fid 1/30) and its kind of target
+        cam = synth_camera(res, res, index=1, fid=1.0 / 30.0, device=dev)
+        with torch.no_grad():
+            d = deform.step(gs.get_xyz.detach(), cam.fid.unsqueeze(0).expand(N, -1))
+            img0 = render(cam, gs, pipe, bg, d[0], d[1], d[2], is_6dof)["render"]
+            noise = torch.randn(img0.shape, generator=torch.Generator().manual_seed(101)).to(dev)
+            gt = (img0 + 0.02 * noise).clamp_(0.0, 1.0).contiguous()
+            del d, img0
+    else:
+        cam = synth_camera(res, res, index=1, fid=0.37, device=dev)
+        gt = torch.rand((3, res, res), generator=torch.Generator().manual_seed(9)).to(dev)
     noise = torch.full((1, 1), ast_noise, device=dev) if ast_noise else 0.0
     # the frame time the network sees: fp32 fid + fp32 noise (train_step adds them on the device)
     t_value = float((cam.fid.unsqueeze(0) + (noise if ast_noise else 0.0)).reshape(-1)[0].item())
@@ -169,24 +195,50 @@ def test_training_step_vs_oracle_chain(name, N, res, is_blender, is_6dof, ast_no
     del raw
     # a synchronous step teaches the speculative pair capacity (and gives the exact pair count),
     # then the deferred one is checked
-    _, pkg0 = forward_backward(gs, deform, cam, gt, pipe, bg, is_6dof=is_6dof, ast_noise=noise)
-    nr_gpu = int(pkg0["render"].grad_fn.num_rendered)
-    del pkg0
-    drop_grads(gs, deform)
-    loss, pkg = forward_backward(gs, deform, cam, gt, pipe, bg, is_6dof=is_6dof, ast_noise=noise,
-                                 deferred_count=True)
-    assert not deferred_overflowed()
+    if path == "native":
+        assert native_step.enabled() and native_step.usable(gs, deform, pipe, gt)
+        _, pkg0, _ = train_step(gs, deform, cam, gt, pipe, bg, is_6dof, ast_noise=noise, deferred_count=False)
+        assert getattr(gs, "_dgs_native", None) is not None, "train_step did not take the native step"
+        nr_gpu = int(pkg0["num_rendered"])
+        del pkg0
+        drop_grads(gs, deform)
+        loss, pkg, redone = train_step(gs, deform, cam, gt, pipe, bg, is_6dof, ast_noise=noise, deferred_count=True)
+        assert not redone
+        assert int(pkg["num_rendered"]) == nr_gpu
+    else:
+        _, pkg0 = forward_backward(gs, deform, cam, gt, pipe, bg, is_6dof=is_6dof, ast_noise=noise)
+        assert getattr(gs, "_dgs_native", None) is None
+        nr_gpu = int(pkg0["render"].grad_fn.num_rendered)
+        del pkg0
+        drop_grads(gs, deform)
+        loss, pkg = forward_backward(gs, deform, cam, gt, pipe, bg, is_6dof=is_6dof, ast_noise=noise,
+                                     deferred_count=True)
+        assert not deferred_overflowed()
     torch.cuda.synchronize()
     want_loss, want, o, c = _oracle_step(w, g, cam, gt, N, res, res, masks, is_blender, is_6dof, t_value)
-    stats = dict(N=N, res=res, loss_rel=abs(float(loss) - want_loss) / abs(want_loss))
+    # the loss bar: 2e-6 relative plus twice the reference's own fp32 rounding of the loss on this image
+    # (its fp32 L1 + SSIM of the oracle's image vs the float64 value): against a target close to the
+    # render (bench-100k) the SSIM variances E[I^2] - mu^2 cancel, and any fp32 evaluation, the
+    # reference's included, lands ~1e-5 relative from the float64 loss
+    from deformgs.loss import l1_loss, ssim
+    img32 = torch.from_numpy(o.color.astype(np.float32))
+    gt32 = gt.cpu().float()
+    loss32 = float(0.8 * l1_loss(img32, gt32) + 0.2 * (1.0 - ssim(img32, gt32)))
+    fp32_dev = abs(loss32 - want_loss)
+    stats = dict(N=N, res=res, path=path, loss_rel=abs(float(loss) - want_loss) / abs(want_loss),
+                 ref_fp32_loss_rel=fp32_dev / abs(want_loss))
+    img_gpu = pkg["render"].detach().cpu().numpy()
+    # the reference's fp32 loss of the GPU's own image: separates the loss kernel from the image
+    imgg = torch.from_numpy(img_gpu)
+    l1g, ssg = float(l1_loss(imgg, gt32)), float(ssim(imgg, gt32))
+    l1o, sso = float(l1_loss(img32, gt32)), float(ssim(img32, gt32))
+    stats.update(loss_gpu=float(loss), loss_oracle=want_loss, ref_fp32_of_gpu_image=0.8 * l1g + 0.2 * (1 - ssg),
+                 l1_gpu_img=l1g, l1_oracle_img=l1o, ssim_gpu_img=ssg, ssim_oracle_img=sso)
     try:
-        assert abs(float(loss) - want_loss) <= 2e-6 * abs(want_loss), (float(loss), want_loss)
         _check_masks(masks, c, is_blender, stats)
         amb = check_integer_outputs(o, pkg["radii"].cpu().numpy(), nr_gpu, stats)
-        gflag, pflag = tail_flags(o, amb)
-        tight = {e: tail_flags(o, amb, float(e))[0] for e in ("1e-5", "1e-6")}  # recorded only
-        img_gpu = pkg["render"].detach().cpu().numpy()
-        check_image(img_gpu, o, pflag, stats)
+        sets = tail_sets(o, amb)
+        check_image(img_gpu, o, sets, stats)
         # the L1 term's gradient is sign(image - gt): where the GPU's and the oracle's images lie on
         # different sides of the target (|image - gt| below their difference), dL/dpixel differs by
         # 2 (1 - lambda) / (3 H W) there, and so does the gradient of every Gaussian blended in it
@@ -195,8 +247,7 @@ def test_training_step_vs_oracle_chain(name, N, res, is_blender, is_6dof, ast_no
         stats["l1_sign_flip_px"] = int(l1_flip.sum())
         if l1_flip.any():
             lf = o.pixel_gaussians(l1_flip)
-            gflag = gflag | lf
-            tight = {e: f | lf for e, f in tight.items()}
+            sets = {e: (gf | lf, pf) for e, (gf, pf) in sets.items()}
         params = {"_xyz": gs._xyz, "_scaling": gs._scaling, "_rotation": gs._rotation, "_opacity": gs._opacity,
                   "_features_dc": gs._features_dc, "_features_rest": gs._features_rest}
         params.update({"mlp." + k: p for k, p in deform.deform.named_parameters()})
@@ -207,13 +258,17 @@ def test_training_step_vs_oracle_chain(name, N, res, is_blender, is_6dof, ast_no
             if k.startswith("mlp."):
                 a, b = a.reshape(-1), b.reshape(-1)
                 mlp_rel[k] = rel_err(a, b)
-                assert np.abs(a - b).max() <= 2e-3 * max(np.abs(b).max(), 1e-12), (k, rel_err(a, b))
             else:
-                check_gaussian_grad(a, b, gflag, k, stats, tighter=tight)
+                check_gaussian_grad(a, b, sets, k, stats)
         stats["mlp_worst_rel"] = max(mlp_rel.values())
+        # MLP gradients (sums over all points): max error within 5e-4 of each tensor's max (measured
+        # worst 2.5e-4 over the five configurations, round 4)
+        for k, r in mlp_rel.items():
+            assert r <= 5e-4, (k, r)
+        assert abs(float(loss) - want_loss) <= 2e-6 * abs(want_loss) + 2.0 * fp32_dev, (float(loss), want_loss, loss32)
         _guard_ok()
     finally:
-        write_stats(f"step_vs_oracle[{name}]", stats)
+        write_stats(f"step_vs_oracle[{name},{path}]", stats)
 
 
 @pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")

@@ -172,23 +172,32 @@ def test_config3_loop_at_size_matches_torch_glue():
 
 
 @pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")
-def test_loop_generalises_to_held_out_views():
+@pytest.mark.parametrize("is_blender", [True, False], ids=["blender", "nonblender-ast-noise"])
+def test_loop_generalises_to_held_out_views(is_blender):
     """Held-out signal for the loop (the stand-in for config 5's test PSNR, train_baseline.py:210-267):
     3000 iterations on a 20k-Gaussian scene at 400x400 whose ground truth deforms smoothly in position
     and time, with test cameras interleaved between the train views and frame times
     (deformgs/train.py SyntheticScene). Reference defaults otherwise (densify every 100 from 500, reset
     at 3000), warm-up 500. The test PSNR must rise: by 1 dB from the end of the static warm-up to the
     end of the run (the deformation network is what it learns after the warm-up) and above the first
-    iteration's."""
+    iteration's. Both networks: the blender one (timenet) and config 5's NeRF-DS one (is_blender=False:
+    no timenet, 21-channel t PE, and the ast_noise of train_baseline.py:107-112 on the frame time after
+    the warm-up), with densification on."""
     from deformgs.arguments import ModelParams, OptimizationParams, PipelineParams
     from deformgs.gaussian_model import GaussianModel
     from deformgs.train import SyntheticScene, training
+    from helpers import write_stats
     scene = SyntheticScene(20_000, 400, 400, n_train=30, n_test=5, seed=5, device="cuda")
     g = scene.init_gaussians(GaussianModel(3))
     torch.manual_seed(0)
     opt = OptimizationParams(iterations=3000, warm_up=500)
-    hist = training(ModelParams(is_blender=True), opt, PipelineParams(), [1, 500, 3000], [], scene, g, seed=0)
+    hist = training(ModelParams(is_blender=is_blender), opt, PipelineParams(), [1, 500, 3000], [], scene, g, seed=0)
     rep = hist["report"]
     p1, p500, p3000 = (rep[k]["test"][1] for k in (1, 500, 3000))
-    print("test PSNR", p1, p500, p3000, "train", [rep[k]["train"][1] for k in (1, 500, 3000)])
+    train = [rep[k]["train"][1] for k in (1, 500, 3000)]
+    print("test PSNR", p1, p500, p3000, "train", train)
+    write_stats(f"heldout_loop[{'blender' if is_blender else 'nonblender'}]",
+                dict(test_psnr=[p1, p500, p3000], train_psnr=train, n_final=hist["n"][-1],
+                     n_after_first_densify=hist["n"][600], redone=int(sum(hist["redone"]))))
+    assert hist["n"][600] != hist["n"][400], "densification must change the Gaussian count"
     assert p3000 > p500 + 1.0 and p3000 > p1, (p1, p500, p3000)

@@ -1,0 +1,150 @@
+// Host audit of the SSIM kernels' index arithmetic (csrc/ssim.hip; VERDICT r4 "close the r4v abort
+// from the evidence in hand"). Every thread of every workgroup of k_ssim_fwd / k_ssim_final /
+// k_ssim_bwd is replayed on the CPU with the kernels' own index expressions (copied term for term,
+// constants from ssim.hip) and every global and LDS address each thread forms is checked against the
+// extent of its buffer: the input planes (C*H*W), the scratch (3*C*H*W maps + 2*nb partials, as
+// dgs_l1_ssim_scratch_floats sizes it), the gradient, and the LDS arrays sx / sm [NM][S][SP], hq
+// [NM][S][HP], red. Usage: ssim_index_audit C H W [C H W ...]; exit 0 = every address in bounds.
+// Built and run by tests/test_ssim_index_audit.py for the shapes of tests/test_gpu_loss.py.
+#include <cstdio>
+#include <cstdlib>
+#include <cstddef>
+
+namespace {
+constexpr int T = 32, R = 5, S = T + 2 * R, SP = S + 1, HP = T + 1, HX = 8, VY = 4;
+
+long long g_checks = 0;
+int g_fail = 0;
+
+void chk(const char *what, long long idx, long long n, int c, int bx, int by, int tid) {
+    ++g_checks;
+    if (idx < 0 || idx >= n) {
+        if (g_fail++ < 20)
+            std::fprintf(stderr, "OUT OF BOUNDS %s: index %lld not in [0, %lld) (c %d block %d,%d thread %d)\n", what,
+                         idx, n, c, bx, by, tid);
+    }
+}
+
+int div_up(int a, int b) { return (a + b - 1) / b; }
+
+// load_tile<NM>: element e of the 42x42 halo tile, global read src[q][p] only when `in`; src[q] =
+// buffer + base[q], checked against the region the map lives in (region_n)
+void audit_load_tile(int NM, const long long *base, long long region_n, int H, int W, int x0, int y0, int c, int bx,
+                     int by) {
+    const int NIT = (S * S + 255) / 256;
+    for (int tid = 0; tid < 256; tid++)
+        for (int it = 0; it < NIT; it++) {
+            const int e = tid + 256 * it;
+            const int ly = e / S, lx = e - ly * S;
+            const int gy = y0 + ly - R, gx = x0 + lx - R;
+            const bool in = e < S * S && gy >= 0 && gy < H && gx >= 0 && gx < W;
+            const long long p = in ? (long long)gy * W + gx : 0;
+            if (in)
+                for (int q = 0; q < NM; q++) chk("load_tile global", base[q] + p, region_n, c, bx, by, tid);
+            if (e < S * S)
+                for (int q = 0; q < NM; q++) chk("load_tile LDS", ((long long)q * S + ly) * SP + lx, (long long)NM * S * SP, c, bx, by, tid);
+        }
+}
+
+// row pass (fwd: 2 input maps -> 5 row-filtered; bwd: 3 -> 3)
+void audit_row_pass(int NIN, int NOUT, int c, int bx, int by) {
+    for (int tid = 0; tid < 256; tid++) {
+        if (!(tid < S * (T / HX))) continue;
+        const int ly = tid / (T / HX), lx0 = (tid % (T / HX)) * HX;
+        for (int m = 0; m < NIN; m++)
+            for (int k = 0; k < HX + 10; k++)
+                chk("row pass LDS read", ((long long)m * S + ly) * SP + lx0 + k, (long long)NIN * S * SP, c, bx, by, tid);
+        for (int m = 0; m < NOUT; m++)
+            for (int j = 0; j < HX; j++)
+                chk("row pass LDS write", ((long long)m * S + ly) * HP + lx0 + j, (long long)NOUT * S * HP, c, bx, by, tid);
+        // the row index must stay inside a row of the padded array (no wrap into the next row)
+        if (lx0 + HX + 10 - 1 >= SP) chk("row pass read within row", lx0 + HX + 9, SP, c, bx, by, tid);
+        if (lx0 + HX - 1 >= HP) chk("row pass write within row", lx0 + HX - 1, HP, c, bx, by, tid);
+    }
+}
+
+void audit_col_pass(int NM, int c, int bx, int by) {
+    for (int tid = 0; tid < 256; tid++) {
+        const int lx = tid % T, ly0 = (tid / T) * VY;
+        for (int m = 0; m < NM; m++)
+            for (int k = 0; k < VY + 10; k++) {
+                chk("column pass LDS read", ((long long)m * S + ly0 + k) * HP + lx, (long long)NM * S * HP, c, bx, by, tid);
+                chk("column pass row", ly0 + k, S, c, bx, by, tid);
+            }
+    }
+}
+
+int audit(int C, int H, int W) {
+    const long long plane = (long long)H * W;
+    const int gx = div_up(W, T), gy = div_up(H, T);
+    const long long nb = (long long)C * gx * gy;
+    const long long scratch_n = 3LL * C * H * W + 2 * nb;  // dgs_l1_ssim_scratch_floats
+    const long long img_n = (long long)C * plane;
+    for (int c = 0; c < C; c++)
+        for (int by = 0; by < gy; by++)
+            for (int bx = 0; bx < gx; bx++) {
+                const int x0 = bx * T, y0 = by * T;
+                // ---- k_ssim_fwd ----
+                // src planes I + c*plane, G + c*plane: global index = c*plane + p
+                const long long fb[2] = {c * plane, c * plane};  // I + c*plane, G + c*plane
+                audit_load_tile(2, fb, img_n, H, W, x0, y0, c, bx, by);
+                audit_row_pass(2, 5, c, bx, by);
+                audit_col_pass(5, c, bx, by);
+                for (int tid = 0; tid < 256; tid++) {
+                    const int lx = tid % T, ly0 = (tid / T) * VY;
+                    const int x = x0 + lx;
+                    for (int j = 0; j < VY; j++) {
+                        const int y = y0 + ly0 + j;
+                        if (x < W && y < H) {
+                            const long long p = (long long)y * W + x;
+                            for (int m = 0; m < 3; m++) chk("fwd maps write", (3LL * c + m) * plane + p, scratch_n, c, bx, by, tid);
+                            chk("fwd maps region", (3LL * c + 2) * plane + p, 3LL * C * H * W, c, bx, by, tid);
+                            chk("fwd l1 LDS read", ((long long)0 * S + ly0 + j + R) * SP + lx + R, 2LL * S * SP, c, bx, by, tid);
+                            chk("fwd l1 LDS read G", ((long long)1 * S + ly0 + j + R) * SP + lx + R, 2LL * S * SP, c, bx, by, tid);
+                        }
+                    }
+                    const int wv = tid >> 6;
+                    if ((tid & 63) == 0) chk("fwd red", wv, 4, c, bx, by, tid);
+                }
+                const long long b = ((long long)c * gy + by) * gx + bx;
+                chk("fwd partial write", 3LL * C * H * W + 2 * b + 1, scratch_n, c, bx, by, 0);
+                // ---- k_ssim_bwd ----
+                const long long bb[3] = {3LL * c * plane, (3LL * c + 1) * plane, (3LL * c + 2) * plane};  // maps
+                audit_load_tile(3, bb, 3LL * C * H * W, H, W, x0, y0, c, bx, by);
+                audit_row_pass(3, 3, c, bx, by);
+                audit_col_pass(3, c, bx, by);
+                for (int tid = 0; tid < 256; tid++) {
+                    const int lx = tid % T, ly0 = (tid / T) * VY;
+                    const int x = x0 + lx;
+                    for (int j = 0; j < VY; j++) {
+                        const int y = y0 + ly0 + j;
+                        if (x >= W || y >= H) continue;
+                        const long long p = c * plane + (long long)y * W + x;
+                        chk("bwd I/G read, grad write", p, img_n, c, bx, by, tid);
+                    }
+                }
+            }
+    // ---- k_ssim_final: one workgroup of 1024, reads partial[2 i + 1] for i < nblocks ----
+    for (int t = 0; t < 1024; t++) {
+        for (long long i = t; i < nb; i += 1024) chk("final partial read", 3LL * C * H * W + 2 * i + 1, scratch_n, -1, 0, 0, t);
+        if ((t & 63) == 0) chk("final red", t >> 6, 16, -1, 0, 0, t);
+    }
+    return g_fail;
+}
+}  // namespace
+
+int main(int argc, char **argv) {
+    if (argc < 4 || (argc - 1) % 3) {
+        std::fprintf(stderr, "usage: %s C H W [C H W ...]\n", argv[0]);
+        return 2;
+    }
+    for (int a = 1; a + 2 < argc; a += 3) {
+        const int C = std::atoi(argv[a]), H = std::atoi(argv[a + 1]), W = std::atoi(argv[a + 2]);
+        const long long before = g_checks;
+        const int f0 = g_fail;
+        audit(C, H, W);
+        std::printf("shape (%d,%d,%d): %lld addresses checked, %d out of bounds\n", C, H, W, g_checks - before,
+                    g_fail - f0);
+    }
+    return g_fail ? 1 : 0;
+}
