@@ -470,7 +470,11 @@ struct FwdArgs {
 // The reference feeds every Gaussian the same frame time (train_baseline.py:107-110), so the
 // timenet (time_utils.py:74-76, 13 -> 256 -> 30) has one value per launch: evaluated here once in
 // fp32 (one workgroup); a k_fwd block whose points all carry that t broadcasts TE / TH.
-__global__ __launch_bounds__(256) void k_timenet(FwdArgs a) {
+// fpv(off): the value at offset `off` of the packed fp32 region (k_timenet reads the region k_pack
+// wrote; k_pack_tn's timenet workgroup gathers the same values from the parameters, so the two are
+// bitwise equal)
+template <class FPV>
+__device__ __forceinline__ void timenet_body(const FwdArgs &a, FPV fpv) {
     __shared__ float tin[16], th[256], te[32];
     const int j = threadIdx.x;
     const float t0 = a.t[0];
@@ -489,10 +493,10 @@ __global__ __launch_bounds__(256) void k_timenet(FwdArgs a) {
     if (j == 0) a.tc[TC_T] = t0;
     __syncthreads();
     {
-        const float *w = a.fp + a.wT1 + j * 16;
-        float acc = a.fp[a.bT1 + j];
+        const int w = a.wT1 + j * 16;
+        float acc = fpv(a.bT1 + j);
 #pragma unroll
-        for (int f = 0; f < 16; f++) acc = fmaf(w[f], tin[f], acc);
+        for (int f = 0; f < 16; f++) acc = fmaf(fpv(w + f), tin[f], acc);
         acc = fmaxf(acc, 0.f);
         th[j] = acc;
         a.tc[TC_TH + j] = acc;
@@ -500,30 +504,36 @@ __global__ __launch_bounds__(256) void k_timenet(FwdArgs a) {
     __syncthreads();
     {  // TE[k], k < 32 (rows 30, 31 are zero padding): 8 lanes per output, 32 features each
         const int k = j >> 3, q = j & 7;
-        const float *w = a.fp + a.wT2 + k * 256 + 32 * q;
+        const int w = a.wT2 + k * 256 + 32 * q;
         float acc = 0.f;
 #pragma unroll
-        for (int f = 0; f < 32; f++) acc = fmaf(w[f], th[32 * q + f], acc);
+        for (int f = 0; f < 32; f++) acc = fmaf(fpv(w + f), th[32 * q + f], acc);
         acc += __shfl_xor(acc, 1);
         acc += __shfl_xor(acc, 2);
         acc += __shfl_xor(acc, 4);
         if (q == 0) {
-            a.tc[TC_TE + k] = acc + a.fp[a.bT2 + k];
-            te[k] = k < 30 ? acc + a.fp[a.bT2 + k] : 0.f;
+            const float b = fpv(a.bT2 + k);
+            a.tc[TC_TE + k] = acc + b;
+            te[k] = k < 30 ? acc + b : 0.f;
         }
     }
     __syncthreads();
     {  // C0 / C5: the biases of linear.0 / linear.5 with the t_emb columns folded in (k_fwd, uniform t)
-        const float *w0 = a.fp + a.w0te + j * 32, *w5 = a.fp + a.w5te + j * 32;
-        float c0 = a.fp[a.bL[0] + j], c5 = a.fp[a.bL[5] + j];
+        const int w0 = a.w0te + j * 32, w5 = a.w5te + j * 32;
+        float c0 = fpv(a.bL[0] + j), c5 = fpv(a.bL[5] + j);
 #pragma unroll
         for (int k = 0; k < 30; k++) {
-            c0 = fmaf(w0[k], te[k], c0);
-            c5 = fmaf(w5[k], te[k], c5);
+            c0 = fmaf(fpv(w0 + k), te[k], c0);
+            c5 = fmaf(fpv(w5 + k), te[k], c5);
         }
         a.tc[TC_C0 + j] = c0;
         a.tc[TC_C5 + j] = c5;
     }
+}
+
+__global__ __launch_bounds__(256) void k_timenet(FwdArgs a) {
+    const float *fp = a.fp;
+    timenet_body(a, [fp](int o) { return fp[o]; });
 }
 
 // One block of NQB 16-point column tiles (NQB = 4: the 64-point blocks; NQB = 1: the 16-point tail
@@ -1754,6 +1764,35 @@ __global__ __launch_bounds__(256) void k_pack(const int *__restrict__ map, PackP
     }
 }
 
+// k_pack plus, in one extra (last) workgroup, k_timenet reading the parameters through the same map:
+// one launch instead of two on the training path (uniform t, blender network, saved activations)
+__global__ __launch_bounds__(256) void k_pack_tn(const int *__restrict__ map, PackPtrs src, __bf16 *__restrict__ img,
+                                                 float *__restrict__ fp, int nimg, int total, FwdArgs a) {
+    if (blockIdx.x == gridDim.x - 1) {
+        const int *fmap = map + nimg;
+        timenet_body(a, [fmap, &src](int o) {
+            const int c = fmap[o];
+            return c < 0 ? 0.f : src.p[c >> PACK_SHIFT][c & ((1 << PACK_SHIFT) - 1)];
+        });
+        return;
+    }
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int c = map[i];
+    const float v = c < 0 ? 0.f : src.p[c >> PACK_SHIFT][c & ((1 << PACK_SHIFT) - 1)];
+    if (i < nimg) {
+        const __bf16 hb = (__bf16)v;
+        const float r = v - (float)hb;
+        const __bf16 mb = (__bf16)r;
+        __bf16 *d = img + (size_t)(i >> 9) * 1536 + (i & 511);  // k-slot: 3 planes of 512 bf16
+        d[0] = hb;
+        d[512] = mb;
+        d[1024] = (__bf16)(r - (float)mb);
+    } else {
+        fp[i - nimg] = v;
+    }
+}
+
 static std::vector<int> build_pack_map(const Plan &P) {
     const size_t nimg = (size_t)P.nslots * 512;
     std::vector<int> map(nimg + P.nf32, -1);
@@ -1975,10 +2014,74 @@ int pack(int flags, const float *const *params, float *packed, hipStream_t strea
     return DGS_OK;
 }
 
+static void fwd_args(const Plan &P, int flags, int N, const float *xyz, const float *t, const float *packed, float *out,
+                     float *saved, FwdArgs &a, hipStream_t stream);
+
+// timenet_done: k_pack_tn already wrote the timenet values (pack_forward)
 int forward(int flags, int N, const float *xyz, const float *t, const float *packed, float *out, float *saved,
-            hipStream_t stream) {
+            hipStream_t stream, bool timenet_done = false) {
     const Plan P = make_plan(flags);
     FwdArgs a{};
+    fwd_args(P, flags, N, xyz, t, packed, out, saved, a, stream);
+    const int grid = persistent_grid(a.nblk, a.queue);
+    if (P.F.blender && (saved || P.F.uniform_t)) {
+        // the folded biases (uniform t) are needed without saved activations too (inference)
+        if (!a.tc) {
+            set_error("dgs_deform_forward: could not allocate the timenet scratch");
+            return DGS_ERR_HIP;
+        }
+        if (!timenet_done) hipLaunchKernelGGL(k_timenet, dim3(1), dim3(256), 0, stream, a);
+    }
+    {
+        ScopedTimer tm("mlp_fwd", stream);  // k_fwd only: the class's FLOP count is the trunk's + heads'
+        const bool fold = P.F.uniform_t;  // t_emb folded into the biases (a.tc is set above)
+        if (saved && fold)
+            hipLaunchKernelGGL((k_fwd<true, true>), dim3(grid), dim3(NTHR), 0, stream, a);
+        else if (saved)
+            hipLaunchKernelGGL((k_fwd<true, false>), dim3(grid), dim3(NTHR), 0, stream, a);
+        else if (fold)
+            hipLaunchKernelGGL((k_fwd<false, true>), dim3(grid), dim3(NTHR), 0, stream, a);
+        else
+            hipLaunchKernelGGL((k_fwd<false, false>), dim3(grid), dim3(NTHR), 0, stream, a);
+    }
+    DGS_LAUNCH_CHECK("k_fwd", false, stream);
+    return DGS_OK;
+}
+
+// The training step's pack + forward (uniform t, blender, saved activations): the timenet runs in
+// the pack launch (k_pack_tn), gathering its weights from the parameters as k_pack does; otherwise
+// pack() then forward().
+int pack_forward(int flags, const float *const *params, int N, const float *xyz, const float *t, float *packed,
+                 float *out, float *saved, hipStream_t stream) {
+    const Plan P = make_plan(flags);
+    if (!(P.F.blender && P.F.uniform_t && saved) || P.nparams > PACK_MAXP || N <= 0) {
+        if (int rc = pack(flags, params, packed, stream)) return rc;
+        return forward(flags, N, xyz, t, packed, out, saved, stream);
+    }
+    PackPtrs src{};
+    for (int k = 0; k < P.nparams; k++) {
+        if (!params[k]) {
+            set_error("dgs_deform_pack: null parameter pointer");
+            return DGS_ERR_ARGS;
+        }
+        src.p[k] = params[k];
+    }
+    const int *map = pack_map_for(P, flags);
+    if (!map) {
+        set_error("dgs_deform_pack: could not allocate the pack map");
+        return DGS_ERR_HIP;
+    }
+    FwdArgs a{};
+    fwd_args(P, flags, N, xyz, t, packed, out, saved, a, stream);
+    const int nimg = P.nslots * 512, total = nimg + P.nf32;
+    hipLaunchKernelGGL(k_pack_tn, dim3(div_up(total, 256) + 1), dim3(256), 0, stream, map, src,
+                       reinterpret_cast<__bf16 *>(packed), packed + P.img_floats(), nimg, total, a);
+    DGS_LAUNCH_CHECK("k_pack_tn", false, stream);
+    return forward(flags, N, xyz, t, packed, out, saved, stream, true);
+}
+
+static void fwd_args(const Plan &P, int flags, int N, const float *xyz, const float *t, const float *packed, float *out,
+                     float *saved, FwdArgs &a, hipStream_t stream) {
     a.N = N;
     a.Ns = padded_points(N);
     a.xyz = xyz; a.t = t; a.out = out; a.saved = saved;
@@ -1995,30 +2098,9 @@ int forward(int flags, int N, const float *xyz, const float *t, const float *pac
     const int nblk = bs.nfull + bs.ntail;
     a.nblk = nblk;
     a.queue = nblk > 0 ? block_queue(stream, 0) : nullptr;
-    const int grid = persistent_grid(nblk, a.queue);
-    if (P.F.blender && (saved || P.F.uniform_t)) {
-        // the folded biases (uniform t) are needed without saved activations too (inference)
+    a.tc = nullptr;
+    if (P.F.blender && (saved || P.F.uniform_t))
         a.tc = saved ? saved + (size_t)P.F.nsaved * a.Ns + mask_words(P.F, a.Ns) : timenet_scratch(stream);
-        if (!a.tc) {
-            set_error("dgs_deform_forward: could not allocate the timenet scratch");
-            return DGS_ERR_HIP;
-        }
-        hipLaunchKernelGGL(k_timenet, dim3(1), dim3(256), 0, stream, a);
-    }
-    {
-        ScopedTimer tm("mlp_fwd", stream);  // k_fwd only: the class's FLOP count is the trunk's + heads'
-        const bool fold = P.F.uniform_t;  // t_emb folded into the biases (a.tc is set above)
-        if (saved && fold)
-            hipLaunchKernelGGL((k_fwd<true, true>), dim3(grid), dim3(NTHR), 0, stream, a);
-        else if (saved)
-            hipLaunchKernelGGL((k_fwd<true, false>), dim3(grid), dim3(NTHR), 0, stream, a);
-        else if (fold)
-            hipLaunchKernelGGL((k_fwd<false, true>), dim3(grid), dim3(NTHR), 0, stream, a);
-        else
-            hipLaunchKernelGGL((k_fwd<false, false>), dim3(grid), dim3(NTHR), 0, stream, a);
-    }
-    DGS_LAUNCH_CHECK("k_fwd", false, stream);
-    return DGS_OK;
 }
 
 int backward(int flags, int N, const float *packed, const float *saved, const float *dout, float *scratch,
@@ -2208,6 +2290,20 @@ extern "C" int dgs_deform_forward(int flags, int N, const float *xyz, const floa
     if (N == 0) return DGS_OK;
     return exact_fp32(flags) ? mlp::forward(net_flags(flags), N, xyz, t, packed, out, saved, stream)
                              : mlps::forward(net_flags(flags), N, xyz, t, packed, out, saved, stream);
+}
+
+extern "C" int dgs_deform_pack_forward(int flags, const float *const *params, int N, const float *xyz, const float *t,
+                                       float *packed, float *out, float *saved, void *stream_) {
+    hipStream_t stream = (hipStream_t)stream_;
+    if (!params || !packed || N < 0 || (N > 0 && (!xyz || !t || !out))) {
+        set_error("dgs_deform_pack_forward: null argument");
+        return DGS_ERR_ARGS;
+    }
+    if (exact_fp32(flags) || N == 0) {
+        if (int rc = dgs_deform_pack(flags, params, packed, stream_)) return rc;
+        return dgs_deform_forward(flags, N, xyz, t, packed, out, saved, stream_);
+    }
+    return mlps::pack_forward(net_flags(flags), params, N, xyz, t, packed, out, saved, stream);
 }
 
 extern "C" int dgs_deform_backward(int flags, int N, const float *packed, const float *saved, const float *dout,

@@ -55,7 +55,6 @@ extern "C" int dgs_train_step(const dgs_train_step_args *a, int *overflowed, int
     long long over0 = dgs_raster_deferred_overflows();
     // ---- deform.step(xyz.detach(), t) (scene/deform_model.py:323-324) with one frame time ----
     if (warm) {
-        if (int rc = dgs_deform_pack(flags, a->mlp_params, a->mlp_packed, stream)) return rc;
         // the split path of a blender network reads t[0] only (k_timenet); every other kernel a column
         const float *t = a->t;
         if (!(a->mlp_flags & DGS_MLP_BLENDER) || (a->mlp_flags & DGS_MLP_EXACT_FP32)) {
@@ -67,7 +66,10 @@ extern "C" int dgs_train_step(const dgs_train_step_args *a, int *overflowed, int
             DGS_LAUNCH_CHECK("k_fill_scalar", false, stream);
             t = a->t_full;
         }
-        if (int rc = dgs_deform_forward(flags, P, a->xyz, t, a->mlp_packed, a->mlp_out, a->mlp_saved, stream)) return rc;
+        // pack + forward (the timenet inside the pack launch)
+        if (int rc = dgs_deform_pack_forward(flags, a->mlp_params, P, a->xyz, t, a->mlp_packed, a->mlp_out,
+                                             a->mlp_saved, stream))
+            return rc;
     }
     // ---- render(): input glue, then the split-SH rasterizer (gaussian_renderer/__init__.py:32-133) ----
     // (6-DoF warm-up: means3D = xyz, gaussian_renderer/__init__.py:71-74: the plain input launch)

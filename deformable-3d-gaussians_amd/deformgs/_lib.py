@@ -78,6 +78,7 @@ _SIGS = {
     "dgs_deform_scratch_floats": ([I, I], SZ),
     "dgs_deform_pack": ([I, P, P, P], I),
     "dgs_deform_forward": ([I, I, P, P, P, P, P, P], I),
+    "dgs_deform_pack_forward": ([I, P, I, P, P, P, P, P, P], I),
     "dgs_deform_backward": ([I, I, P, P, P, P, P, P], I),
     "dgs_deform_outputs": ([I], I),
     "dgs_knn_dist2": ([I, P, P, P], I),

@@ -210,6 +210,11 @@ int dgs_deform_pack(int flags, const float *const *params, float *packed, void *
  * t: (N,1) per-point time. saved may be NULL for inference (no backward). */
 int dgs_deform_forward(int flags, int N, const float *xyz, const float *t, const float *packed,
                        float *out, float *saved, void *stream);
+/* dgs_deform_pack + dgs_deform_forward in one call (the training step's order): with a uniform t, the
+ * blender network and saved activations the timenet runs inside the pack launch (one launch fewer);
+ * results bitwise equal to the two calls. */
+int dgs_deform_pack_forward(int flags, const float *const *params, int N, const float *xyz, const float *t,
+                            float *packed, float *out, float *saved, void *stream);
 /* dout: (N, n_out). grads: device pointers in the same order as params (overwritten).
  * scratch: dgs_deform_scratch_floats(flags, N) floats. */
 int dgs_deform_backward(int flags, int N, const float *packed, const float *saved, const float *dout,
