@@ -470,9 +470,7 @@ struct FwdArgs {
 // The reference feeds every Gaussian the same frame time (train_baseline.py:107-110), so the
 // timenet (time_utils.py:74-76, 13 -> 256 -> 30) has one value per launch: evaluated here once in
 // fp32 (one workgroup); a k_fwd block whose points all carry that t broadcasts TE / TH.
-// fpv(off): the value at offset `off` of the packed fp32 region (k_timenet reads the region k_pack
-// wrote; k_pack_tn's timenet workgroup gathers the same values from the parameters, so the two are
-// bitwise equal)
+// fpv(off): the value at offset `off` of the packed fp32 region k_pack wrote
 template <class FPV>
 __device__ __forceinline__ void timenet_body(const FwdArgs &a, FPV fpv) {
     __shared__ float tin[16], th[256], te[32];
@@ -1764,35 +1762,6 @@ __global__ __launch_bounds__(256) void k_pack(const int *__restrict__ map, PackP
     }
 }
 
-// k_pack plus, in one extra (last) workgroup, k_timenet reading the parameters through the same map:
-// one launch instead of two on the training path (uniform t, blender network, saved activations)
-__global__ __launch_bounds__(256) void k_pack_tn(const int *__restrict__ map, PackPtrs src, __bf16 *__restrict__ img,
-                                                 float *__restrict__ fp, int nimg, int total, FwdArgs a) {
-    if (blockIdx.x == gridDim.x - 1) {
-        const int *fmap = map + nimg;
-        timenet_body(a, [fmap, &src](int o) {
-            const int c = fmap[o];
-            return c < 0 ? 0.f : src.p[c >> PACK_SHIFT][c & ((1 << PACK_SHIFT) - 1)];
-        });
-        return;
-    }
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= total) return;
-    const int c = map[i];
-    const float v = c < 0 ? 0.f : src.p[c >> PACK_SHIFT][c & ((1 << PACK_SHIFT) - 1)];
-    if (i < nimg) {
-        const __bf16 hb = (__bf16)v;
-        const float r = v - (float)hb;
-        const __bf16 mb = (__bf16)r;
-        __bf16 *d = img + (size_t)(i >> 9) * 1536 + (i & 511);  // k-slot: 3 planes of 512 bf16
-        d[0] = hb;
-        d[512] = mb;
-        d[1024] = (__bf16)(r - (float)mb);
-    } else {
-        fp[i - nimg] = v;
-    }
-}
-
 static std::vector<int> build_pack_map(const Plan &P) {
     const size_t nimg = (size_t)P.nslots * 512;
     std::vector<int> map(nimg + P.nf32, -1);
@@ -2017,9 +1986,8 @@ int pack(int flags, const float *const *params, float *packed, hipStream_t strea
 static void fwd_args(const Plan &P, int flags, int N, const float *xyz, const float *t, const float *packed, float *out,
                      float *saved, FwdArgs &a, hipStream_t stream);
 
-// timenet_done: k_pack_tn already wrote the timenet values (pack_forward)
 int forward(int flags, int N, const float *xyz, const float *t, const float *packed, float *out, float *saved,
-            hipStream_t stream, bool timenet_done = false) {
+            hipStream_t stream) {
     const Plan P = make_plan(flags);
     FwdArgs a{};
     fwd_args(P, flags, N, xyz, t, packed, out, saved, a, stream);
@@ -2030,7 +1998,7 @@ int forward(int flags, int N, const float *xyz, const float *t, const float *pac
             set_error("dgs_deform_forward: could not allocate the timenet scratch");
             return DGS_ERR_HIP;
         }
-        if (!timenet_done) hipLaunchKernelGGL(k_timenet, dim3(1), dim3(256), 0, stream, a);
+        hipLaunchKernelGGL(k_timenet, dim3(1), dim3(256), 0, stream, a);
     }
     {
         ScopedTimer tm("mlp_fwd", stream);  // k_fwd only: the class's FLOP count is the trunk's + heads'
@@ -2048,36 +2016,15 @@ int forward(int flags, int N, const float *xyz, const float *t, const float *pac
     return DGS_OK;
 }
 
-// The training step's pack + forward (uniform t, blender, saved activations): the timenet runs in
-// the pack launch (k_pack_tn), gathering its weights from the parameters as k_pack does; otherwise
-// pack() then forward().
+// The training step's pack + forward: pack() then forward() (k_pack, k_timenet, k_fwd). Round 5 tried
+// the timenet inside the pack launch (one extra workgroup gathering its weights through the pack map):
+// 59 us for that launch against 9 + 7 us for the two (rocprofv3, profiles/r5b_pack_tn_regression.txt;
+// the map double-indirection serialised the timenet's loads and its registers lowered the pack's
+// occupancy), so the two launches stay.
 int pack_forward(int flags, const float *const *params, int N, const float *xyz, const float *t, float *packed,
                  float *out, float *saved, hipStream_t stream) {
-    const Plan P = make_plan(flags);
-    if (!(P.F.blender && P.F.uniform_t && saved) || P.nparams > PACK_MAXP || N <= 0) {
-        if (int rc = pack(flags, params, packed, stream)) return rc;
-        return forward(flags, N, xyz, t, packed, out, saved, stream);
-    }
-    PackPtrs src{};
-    for (int k = 0; k < P.nparams; k++) {
-        if (!params[k]) {
-            set_error("dgs_deform_pack: null parameter pointer");
-            return DGS_ERR_ARGS;
-        }
-        src.p[k] = params[k];
-    }
-    const int *map = pack_map_for(P, flags);
-    if (!map) {
-        set_error("dgs_deform_pack: could not allocate the pack map");
-        return DGS_ERR_HIP;
-    }
-    FwdArgs a{};
-    fwd_args(P, flags, N, xyz, t, packed, out, saved, a, stream);
-    const int nimg = P.nslots * 512, total = nimg + P.nf32;
-    hipLaunchKernelGGL(k_pack_tn, dim3(div_up(total, 256) + 1), dim3(256), 0, stream, map, src,
-                       reinterpret_cast<__bf16 *>(packed), packed + P.img_floats(), nimg, total, a);
-    DGS_LAUNCH_CHECK("k_pack_tn", false, stream);
-    return forward(flags, N, xyz, t, packed, out, saved, stream, true);
+    if (int rc = pack(flags, params, packed, stream)) return rc;
+    return forward(flags, N, xyz, t, packed, out, saved, stream);
 }
 
 static void fwd_args(const Plan &P, int flags, int N, const float *xyz, const float *t, const float *packed, float *out,

@@ -24,10 +24,33 @@ def init_from_env(backend=None):
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
             torch.cuda.set_device(local)
+            reserve_cus_for_collectives()
             dist.init_process_group(backend, device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
     return rank, world, local
+
+
+# CUs the network's persistent MLP kernels leave to the gradient all-reduce, and the RCCL channel cap
+# that keeps the collective's workgroups within them (one workgroup per channel). The MLP kernels take
+# a CU's whole register file, so a collective workgroup and an MLP workgroup never share a CU: on one
+# MI355X, a stand-in collective (24 MB read-modify-write sweeps) enqueued where the Gaussian-gradient
+# all-reduce goes cost the step +0.15-0.35 ms with no CUs reserved (k_dws's static plan waited for the
+# CUs it held) and +0.01-0.03 ms with 16 or 32 reserved for 16 or 32 stand-in workgroups, while the
+# reserve itself cost the step 0-2.5 % (tools/overlap_probe.py --sweep --wide,
+# profiles/r5c_overlap_sweep.jsonl; the collective queued after the network backward instead: +0.08-0.2
+# ms). RCCL itself cannot run on a one-GPU box, so its real workgroup count is capped, not measured.
+OVERLAP_CUS = 32
+
+
+def reserve_cus_for_collectives():
+    """Before an RCCL process group is created (several ranks): cap RCCL's channels at OVERLAP_CUS
+    (unless NCCL_MAX_NCHANNELS is set) and make the MLP kernels leave that many CUs free (unless
+    DGS_MLP_RESERVE_CUS is set)."""
+    os.environ.setdefault("NCCL_MAX_NCHANNELS", str(OVERLAP_CUS))
+    if "DGS_MLP_RESERVE_CUS" not in os.environ:
+        from . import _lib
+        _lib.load().dgs_mlp_set_reserved_cus(min(64, int(os.environ["NCCL_MAX_NCHANNELS"])))
 
 
 class GradAllReduce:

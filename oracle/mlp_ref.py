@@ -118,23 +118,32 @@ def _se3_vjp(w_raw, v_raw, gM, eps=1e-6):
     return gw, gv
 
 
-def backward(p, c, out, g, is_blender, is_6dof, fork=False, relu_masks=None):
+def backward(p, c, out, g, is_blender, is_6dof, fork=False, relu_masks=None, abs_sums=None):
     """g: dict of upstream grads for d_xyz / d_rot / d_scale. Returns dict param-name -> grad.
 
     relu_masks (optional): {layer i: bool (N, 256), "th": bool (N, 256)} overriding relu'(z) = z > 0.
     A pre-activation within a few fp32 ulps of 0 can take either sign in an fp32 forward, which flips
     a whole row of dZ; the GPU parity tests pass the kernel's own masks so they check the arithmetic
-    and not that tie (tests/test_gpu_mlp.py)."""
+    and not that tie (tests/test_gpu_mlp.py).
+    abs_sums (optional dict): filled with, per parameter, the sum over points of the absolute values
+    of the terms its gradient sums (|dZ|^T |X|, sum |dZ|): the scale of an fp32 summation's rounding
+    error, which a nearly cancelling gradient sum does not show."""
     relu_masks = relu_masks or {}
     gr = {}
     h = c["hlast"]
     dh = np.zeros_like(h)
 
+    def record(name, dz, x):
+        gr[name + ".weight"] = dz.T @ x
+        gr[name + ".bias"] = dz.sum(0)
+        if abs_sums is not None:
+            abs_sums[name + ".weight"] = np.abs(dz).T @ np.abs(x)
+            abs_sums[name + ".bias"] = np.abs(dz).sum(0)
+
     def head(name, gout):
         nonlocal dh
         gout = np.asarray(gout, np.float64)
-        gr[name + ".weight"] = gout.T @ h
-        gr[name + ".bias"] = gout.sum(0)
+        record(name, gout, h)
         dh = dh + gout @ p[name + ".weight"].astype(np.float64)
 
     if is_6dof:
@@ -157,18 +166,14 @@ def backward(p, c, out, g, is_blender, is_6dof, fork=False, relu_masks=None):
             dte += dh[:, nx:nx + nt]
             dh = dh[:, nx + nt:]
         dz = dh * relu_masks.get(i, c["z"][i] > 0)
-        hin = c["hin"][i]
-        gr[f"linear.{i}.weight"] = dz.T @ hin
-        gr[f"linear.{i}.bias"] = dz.sum(0)
+        record(f"linear.{i}", dz, c["hin"][i])
         dh = dz @ p[f"linear.{i}.weight"].astype(np.float64)
     dte += dh[:, nx:nx + nt]
     if is_blender:
-        gr["timenet.2.weight"] = dte.T @ c["th"]
-        gr["timenet.2.bias"] = dte.sum(0)
+        record("timenet.2", dte, c["th"])
         dth = dte @ p["timenet.2.weight"].astype(np.float64)
         dz = dth * relu_masks.get("th", c["tz0"] > 0)
-        gr["timenet.0.weight"] = dz.T @ c["te_in"]
-        gr["timenet.0.bias"] = dz.sum(0)
+        record("timenet.0", dz, c["te_in"])
     return gr
 
 

@@ -428,3 +428,26 @@ def test_native_path_choice_is_agreed_across_ranks():
         assert b == ["autograd"]
         assert c == ["native"]
         assert d == (["native"] if rank == 0 else "raised")
+
+
+def test_rccl_group_reserves_cus_for_the_collective(monkeypatch):
+    """Before an RCCL group: NCCL_MAX_NCHANNELS defaults to OVERLAP_CUS and the MLP kernels leave that
+    many CUs free (the library knob; a host-side setter, no GPU needed); explicit settings win."""
+    from deformgs import _lib
+    from deformgs.dist import OVERLAP_CUS, reserve_cus_for_collectives
+    lib = _lib.load()
+    monkeypatch.delenv("NCCL_MAX_NCHANNELS", raising=False)
+    monkeypatch.delenv("DGS_MLP_RESERVE_CUS", raising=False)
+    try:
+        reserve_cus_for_collectives()
+        assert os.environ["NCCL_MAX_NCHANNELS"] == str(OVERLAP_CUS)
+        assert lib.dgs_mlp_reserved_cus() == OVERLAP_CUS
+        monkeypatch.setenv("NCCL_MAX_NCHANNELS", "16")
+        reserve_cus_for_collectives()
+        assert lib.dgs_mlp_reserved_cus() == 16
+        lib.dgs_mlp_set_reserved_cus(3)
+        monkeypatch.setenv("DGS_MLP_RESERVE_CUS", "3")
+        reserve_cus_for_collectives()
+        assert lib.dgs_mlp_reserved_cus() == 3  # an explicit reserve is left alone
+    finally:
+        lib.dgs_mlp_set_reserved_cus(0)

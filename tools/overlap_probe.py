@@ -11,7 +11,7 @@ buffer, the shape of an RCCL ring all-reduce) enqueued exactly where the all-red
 the MLP kernels optionally leaving `reserve` CUs free (dgs_mlp_set_reserved_cus).
 
   python tools/overlap_probe.py --mode standin --reserve 0 [--nwg 16 --passes 2]   # one config
-  python tools/overlap_probe.py --sweep                                             # A/B table
+  python tools/overlap_probe.py --sweep [--wide]                                    # A/B table
   python tools/overlap_probe.py --analyze <rocprofv3 kernel_trace.csv>              # overlap from a trace
 
 Each config prints one JSON line: ms per step over --steps timed steps, and (from HIP events on the
@@ -95,6 +95,10 @@ def run(mode, reserve, steps, warmup, nwg, passes, state=None):
         ns.network_backward()
         if mode == "standin":
             comp.wait_stream(side)  # Adam after the collective (as RCCL's wait())
+        elif mode == "serial":  # no overlap: the collective queued after the network backward
+            _lib.check(lib.dgs_debug_collective_standin(ctypes.c_void_p(ns.gflat.data_ptr()), ns.gflat.numel(),
+                                                        nwg, passes, ctypes.c_void_p(comp.cuda_stream)),
+                       "collective_standin")
         optimizer_step(gs, deform, it[0])
         it[0] += 1
 
@@ -150,13 +154,14 @@ def analyze(path):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", choices=["plain", "standin"], default="standin")
+    ap.add_argument("--mode", choices=["plain", "standin", "serial"], default="standin")
     ap.add_argument("--reserve", type=int, default=0)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--nwg", type=int, default=16)
     ap.add_argument("--passes", type=int, default=2)
     ap.add_argument("--sweep", action="store_true")
+    ap.add_argument("--wide", action="store_true", help="with --sweep: stand-in widths 16 / 32, reserves 16 / 32, serial")
     ap.add_argument("--analyze")
     a = ap.parse_args()
     if a.analyze:
@@ -173,9 +178,15 @@ def main():
         return
     state = setup()
     # alternating order, twice, so box drift does not pose as an effect
+    configs = [("plain", 0, a.nwg), ("standin", 0, a.nwg), ("plain", 4, a.nwg), ("standin", 4, a.nwg),
+               ("plain", 8, a.nwg), ("standin", 8, a.nwg)]
+    if a.wide:  # the stand-in's workgroup count against the reserve, and the serial (no-overlap) form
+        configs = [("plain", 0, 16), ("serial", 0, 16), ("serial", 0, 32), ("standin", 0, 16), ("standin", 0, 32),
+                   ("plain", 16, 16), ("standin", 16, 16), ("standin", 16, 32),
+                   ("plain", 32, 32), ("standin", 32, 32), ("standin", 32, 16)]
     for rep in range(2):
-        for mode, reserve in (("plain", 0), ("standin", 0), ("plain", 4), ("standin", 4), ("plain", 8), ("standin", 8)):
-            r = run(mode, reserve, a.steps, a.warmup, a.nwg, a.passes, state)
+        for mode, reserve, nwg in configs:
+            r = run(mode, reserve, a.steps, a.warmup, nwg, a.passes, state)
             r["rep"] = rep
             print(json.dumps(r), flush=True)
 
