@@ -226,14 +226,21 @@ struct ClkStamp {
 __device__ __forceinline__ uint32_t lds_peek(const uint32_t *f) {
     return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+// The first test of `seen` (peeked earlier, usually already satisfied) sits outside the spin loop:
+// as the loop's header it merged with the loop's own fresh peek, so the compiler waited for EVERY
+// outstanding LDS read there (lgkmcnt(0)) — the next tile's just-issued B fragment reads included —
+// once per k-step of every GEMM; outside it, the wait covers the peek only.
 __device__ __forceinline__ void lds_wait_ge(const uint32_t *f, uint32_t target, uint32_t seen) {
-    int guard = 0;
-    for (; __builtin_amdgcn_readfirstlane(seen) < target && guard < (1 << 20); guard++) {
-        __builtin_amdgcn_s_sleep(DGS_SPIN_SLEEP);
-        seen = lds_peek(f);
+    if (__builtin_amdgcn_readfirstlane(seen) < target) {
+        int guard = 0;
+#pragma clang loop unroll(disable)
+        do {
+            __builtin_amdgcn_s_sleep(DGS_SPIN_SLEEP);
+            seen = lds_peek(f);
+        } while (__builtin_amdgcn_readfirstlane(seen) < target && ++guard < (1 << 20));
+        if (guard == (1 << 20) && (threadIdx.x & 63) == 0)
+            __hip_atomic_fetch_add(&dgs_mlps_guard_expired, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (guard == (1 << 20) && __builtin_amdgcn_readfirstlane(seen) < target && (threadIdx.x & 63) == 0)
-        __hip_atomic_fetch_add(&dgs_mlps_guard_expired, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("" ::: "memory");
 }
 __device__ __forceinline__ void lds_signal(uint32_t *f, int lane) {
