@@ -318,7 +318,11 @@ __device__ inline void gemm(const bf16x8 *__restrict__ Aw, const bf16x8 *lds, in
         for (int q = 0; q < NQ_; q++) {
             // the next tile's B fragment (or the next k-step's first) is in flight during this tile's MFMAs
             AFrag nb;
+#ifdef DGS_DIAG_BHALF  // diagnostic only (wrong results): every other tile reuses the previous B fragment
+            if (q + 1 < NQ_) nb = ((q + 1) & 1) ? b : load_b(Bk, q + 1);
+#else
             if (q + 1 < NQ_) nb = load_b(Bk, q + 1);
+#endif
             else if (k + 1 < NK) {
                 gate.need(k + 1, seen);
                 Bk = kbase(k + 1);
