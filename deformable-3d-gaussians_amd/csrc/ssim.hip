@@ -7,13 +7,9 @@
 // 11-tap row pass + 11-tap column pass through LDS (32x32 output tile, 42x42 halo tile; each thread
 // keeps a register window per pass: 18 inputs for 8 row outputs, 14 for 4 column outputs).
 // Forward: 5 maps (mu1, mu2, E[I^2], E[G^2], E[IG]) -> per pixel SSIM and the three coefficient
-// maps A, B, C of dSSIM/d(mu1, E[I^2], E[IG]) -> HBM; per-block partial sums, added in a fixed order
-// by the last workgroup (deterministic, one launch).
+// maps A, B, C of dSSIM/d(mu1, E[I^2], E[IG]) -> HBM; per-block partial sums (deterministic).
 // Backward: dSSIM_sum/dI = w*A + 2 I (w*B) + G (w*C) (window symmetric), plus the L1 sign term.
 #include <hip/hip_runtime.h>
-
-#include <map>
-#include <mutex>
 
 #include "dgs_common.h"
 
@@ -71,12 +67,9 @@ __device__ __forceinline__ void load_tile(float (*sm)[S][SP], const float *const
 // forward: 5 maps (mu1, mu2, E[I^2], E[G^2], E[IG]); the products are formed on the fly from the two
 // input tiles. Row pass: each item = one tile row x 8 columns from 18 inputs held in registers;
 // column pass: each thread slides 14 row-filtered values down one column for 4 outputs.
-// block (tile) partial sums: [blocks][2] = (sum |I-G|, sum ssim); the last workgroup to finish
-// (ticket) adds them in a fixed order into out3 = (loss, mean L1, mean SSIM) (no second launch)
+// block (tile) partial sums: [blocks][2] = (sum |I-G|, sum ssim)
 __global__ __launch_bounds__(256) void k_ssim_fwd(int H, int W, const float *__restrict__ I, const float *__restrict__ G,
-                                                  Win win, float *__restrict__ maps, float *__restrict__ partial,
-                                                  uint32_t *__restrict__ ticket, float n, float lambda,
-                                                  float *__restrict__ out3) {
+                                                  Win win, float *__restrict__ maps, float *__restrict__ partial) {
     __shared__ float sx[2][S][SP];
     __shared__ float hq[5][S][HP];
     __shared__ float red[2][4];
@@ -159,61 +152,46 @@ __global__ __launch_bounds__(256) void k_ssim_fwd(int H, int W, const float *__r
         red[1][wv] = s;
     }
     __syncthreads();
-    // hand-off to the last workgroup (MI355X_MICROARCH.md, inter-workgroup visibility: one lane per
-    // storing workgroup, write-through (sc1) stores drained before an agent-scope ticket add; the
-    // last adder reads them with sc1 loads)
-    __shared__ bool s_last;
-    const uint32_t nb = gridDim.x * gridDim.y * gridDim.z;
     if (tid == 0) {
         size_t b = ((size_t)c * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-        __hip_atomic_store(&partial[2 * b], (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&partial[2 * b + 1], (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = prev == nb - 1;
+        partial[2 * b] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+        partial[2 * b + 1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
     }
-    __syncthreads();
-    if (!s_last) return;
-    // the last workgroup: fixed-order sums in double (thread stride, then a fixed tree) -> out3. Each
-    // thread issues its (l1, ssim) pairs as 8-byte sc1 loads, 8 at a time, before adding any: one
-    // memory round trip per 2048 blocks instead of one per loop iteration (the rolled loop's dependent
-    // loads made this tail ~8 us of the launch, r5b trace)
-    __shared__ double dred[2][4];
-    double da = 0.0, db = 0.0;
-    const unsigned long long *pp = reinterpret_cast<const unsigned long long *>(partial);
-    for (uint32_t i0 = 0; i0 < nb; i0 += 8 * 256) {
-        unsigned long long v[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const uint32_t i = i0 + 256 * k + tid;
-            v[k] = i < nb ? __hip_atomic_load(pp + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-        }
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            da += (double)__uint_as_float((uint32_t)v[k]);
-            db += (double)__uint_as_float((uint32_t)(v[k] >> 32));
-        }
+}
+
+// (Round 5 tried this reduction in k_ssim_fwd's last workgroup — ticket, sc1 partials — to save the
+// launch: fwd + final 0.0378 vs 0.0335 ms per step, bench kernel timers; the single workgroup's tail
+// costs more than the launch boundary. Not kept.)
+// out[0] = loss, out[1] = mean L1, out[2] = mean SSIM; one workgroup of 1024 (16 waves: the partial
+// sums are a latency chain of double adds per thread), fixed order (deterministic)
+__global__ __launch_bounds__(1024) void k_ssim_final(int nblocks, float n, float lambda, const float *__restrict__ partial,
+                                                     float *__restrict__ out) {
+    __shared__ double red[2][16];
+    double a = 0.0, b = 0.0;
+    for (int i = threadIdx.x; i < nblocks; i += 1024) {
+        a += (double)partial[2 * i];
+        b += (double)partial[2 * i + 1];
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
-        da += __shfl_xor(da, o);
-        db += __shfl_xor(db, o);
+        a += __shfl_xor(a, o);
+        b += __shfl_xor(b, o);
     }
-    if ((tid & 63) == 0) {
-        dred[0][wv] = da;
-        dred[1][wv] = db;
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = a;
+        red[1][threadIdx.x >> 6] = b;
     }
     __syncthreads();
-    if (tid == 0) {
-        const double sa = (dred[0][0] + dred[0][1]) + (dred[0][2] + dred[0][3]);
-        const double sb = (dred[1][0] + dred[1][1]) + (dred[1][2] + dred[1][3]);
-        const float l1m = (float)(sa / n), ssm = (float)(sb / n);
-        out3[0] = (1.f - lambda) * l1m + lambda * (1.f - ssm);
-        out3[1] = l1m;
-        out3[2] = ssm;
-        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next launch's
+    if (threadIdx.x == 0) {
+        double sa = 0.0, sb = 0.0;
+        for (int w = 0; w < 16; w++) {
+            sa += red[0][w];
+            sb += red[1][w];
+        }
+        float l1 = (float)(sa / n), ss = (float)(sb / n);
+        out[0] = (1.f - lambda) * l1 + lambda * (1.f - ss);
+        out[1] = l1;
+        out[2] = ss;
     }
 }
 
@@ -276,25 +254,6 @@ __global__ __launch_bounds__(256) void k_ssim_bwd(int H, int W, const float *__r
     }
 }
 
-// the ticket word of k_ssim_fwd's last-workgroup reduction, one per (device, stream) (two losses in
-// flight on two streams must not share one); zeroed at allocation, reset by each launch's last workgroup
-uint32_t *ticket_word(hipStream_t stream) {
-    static std::mutex mu;
-    static std::map<std::pair<int, hipStream_t>, uint32_t *> words;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::lock_guard<std::mutex> lk(mu);
-    uint32_t *&w = words[{dev, stream}];
-    if (!w) {
-        if (hipMalloc(&w, 64) != hipSuccess) {
-            w = nullptr;
-            return nullptr;
-        }
-        if (hipMemsetAsync(w, 0, 64, stream) != hipSuccess) return nullptr;
-    }
-    return w;
-}
-
 Win make_window() {
     // utils/loss_utils.py:30-39: gauss = exp(-(x-5)^2 / (2*1.5^2)), normalised in fp32
     Win w;
@@ -313,33 +272,26 @@ Win make_window() {
 
 using namespace dgs;
 
-// the block partials start 8-byte aligned (the last workgroup reads each (l1, ssim) pair as one word)
-static size_t partial_offset(int C, int H, int W) { return (3ull * C * H * W + 1) & ~1ull; }
-
 extern "C" size_t dgs_l1_ssim_scratch_floats(int C, int H, int W) {
     size_t nb = (size_t)C * div_up(H, ssim::T) * div_up(W, ssim::T);
-    return partial_offset(C, H, W) + 2 * nb;
+    return 3ull * C * H * W + 2 * nb;
 }
 
 extern "C" int dgs_l1_ssim_forward(int C, int H, int W, const float *img, const float *gt, float lambda, float *out3,
                                    float *scratch, void *stream_) {
     hipStream_t stream = (hipStream_t)stream_;
-    if (C <= 0 || H <= 0 || W <= 0 || !img || !gt || !out3 || !scratch || (reinterpret_cast<uintptr_t>(scratch) & 7)) {
-        set_error("dgs_l1_ssim_forward: bad argument (scratch: 8-byte aligned)");
+    if (C <= 0 || H <= 0 || W <= 0 || !img || !gt || !out3 || !scratch) {
+        set_error("dgs_l1_ssim_forward: bad argument");
         return DGS_ERR_ARGS;
     }
     dim3 grid(div_up(W, ssim::T), div_up(H, ssim::T), C);
+    const int nb = grid.x * grid.y * grid.z;
     float *maps = scratch;
-    float *partial = scratch + partial_offset(C, H, W);
-    uint32_t *ticket = ssim::ticket_word(stream);
-    if (!ticket) {
-        set_error("dgs_l1_ssim_forward: could not allocate the ticket word");
-        return DGS_ERR_HIP;
-    }
+    float *partial = scratch + 3ull * C * H * W;
     {
         ScopedTimer tm("ssim_fwd", stream);
-        hipLaunchKernelGGL(ssim::k_ssim_fwd, grid, dim3(256), 0, stream, H, W, img, gt, ssim::make_window(), maps, partial,
-                           ticket, (float)C * H * W, lambda, out3);
+        hipLaunchKernelGGL(ssim::k_ssim_fwd, grid, dim3(256), 0, stream, H, W, img, gt, ssim::make_window(), maps, partial);
+        hipLaunchKernelGGL(ssim::k_ssim_final, dim3(1), dim3(1024), 0, stream, nb, (float)C * H * W, lambda, partial, out3);
     }
     DGS_LAUNCH_CHECK("k_ssim_fwd", false, stream);
     return DGS_OK;

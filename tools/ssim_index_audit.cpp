@@ -1,5 +1,5 @@
 // Host audit of the SSIM kernels' index arithmetic (csrc/ssim.hip; VERDICT r4 "close the r4v abort
-// from the evidence in hand"). Every thread of every workgroup of k_ssim_fwd (with its last-workgroup reduction) /
+// from the evidence in hand"). Every thread of every workgroup of k_ssim_fwd / k_ssim_final /
 // k_ssim_bwd is replayed on the CPU with the kernels' own index expressions (copied term for term,
 // constants from ssim.hip) and every global and LDS address each thread forms is checked against the
 // extent of its buffer: the input planes (C*H*W), the scratch (3*C*H*W maps + 2*nb partials, as
@@ -78,8 +78,7 @@ int audit(int C, int H, int W) {
     const long long plane = (long long)H * W;
     const int gx = div_up(W, T), gy = div_up(H, T);
     const long long nb = (long long)C * gx * gy;
-    const long long poff = (3LL * C * H * W + 1) & ~1LL;    // partial_offset: 8-byte aligned pairs
-    const long long scratch_n = poff + 2 * nb;             // dgs_l1_ssim_scratch_floats
+    const long long scratch_n = 3LL * C * H * W + 2 * nb;  // dgs_l1_ssim_scratch_floats
     const long long img_n = (long long)C * plane;
     for (int c = 0; c < C; c++)
         for (int by = 0; by < gy; by++)
@@ -108,8 +107,7 @@ int audit(int C, int H, int W) {
                     if ((tid & 63) == 0) chk("fwd red", wv, 4, c, bx, by, tid);
                 }
                 const long long b = ((long long)c * gy + by) * gx + bx;
-                chk("fwd partial write", poff + 2 * b + 1, scratch_n, c, bx, by, 0);
-                if ((poff + 2 * b) % 2) chk("fwd partial pair alignment", 1, 0, c, bx, by, 0);
+                chk("fwd partial write", 3LL * C * H * W + 2 * b + 1, scratch_n, c, bx, by, 0);
                 // ---- k_ssim_bwd ----
                 const long long bb[3] = {3LL * c * plane, (3LL * c + 1) * plane, (3LL * c + 2) * plane};  // maps
                 audit_load_tile(3, bb, 3LL * C * H * W, H, W, x0, y0, c, bx, by);
@@ -126,17 +124,10 @@ int audit(int C, int H, int W) {
                     }
                 }
             }
-    // ---- k_ssim_fwd's last workgroup (ticket): 256 threads read the 8-byte pair (partial[2 i], [2 i + 1])
-    // for i = i0 + 256 k + t < nblocks, k < 8, i0 in steps of 2048 ----
-    for (int t = 0; t < 256; t++) {
-        for (long long i0 = 0; i0 < nb; i0 += 8 * 256)
-            for (int k = 0; k < 8; k++) {
-                const long long i = i0 + 256 * k + t;
-                if (i >= nb) continue;
-                chk("final partial read", poff + 2 * i, scratch_n, -1, 0, 0, t);
-                chk("final partial read", poff + 2 * i + 1, scratch_n, -1, 0, 0, t);
-            }
-        if ((t & 63) == 0) chk("final dred", t >> 6, 4, -1, 0, 0, t);
+    // ---- k_ssim_final: one workgroup of 1024, reads partial[2 i + 1] for i < nblocks ----
+    for (int t = 0; t < 1024; t++) {
+        for (long long i = t; i < nb; i += 1024) chk("final partial read", 3LL * C * H * W + 2 * i + 1, scratch_n, -1, 0, 0, t);
+        if ((t & 63) == 0) chk("final red", t >> 6, 16, -1, 0, 0, t);
     }
     return g_fail;
 }
