@@ -929,10 +929,9 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
                                                    const float *__restrict__ dL_dpix, const float *__restrict__ dL_ddepth,
                                                    float *__restrict__ acc) {
     __shared__ float4 s_q[B2];   // staged conic in exponent form + opacity
-    __shared__ float4 s_xyc[B2]; // mean2D x, y, list position (bits), -: one 16-B stride with s_q
+    __shared__ float4 s_xyc[B2]; // mean2D x, y, list position (bits), Gaussian id (bits)
     __shared__ float4 s_co[B2];
     __shared__ float4 s_cd[B2];
-    __shared__ uint32_t s_id[B2];
     __shared__ uint32_t s_wcnt[B2 / 64];
     __shared__ uint32_t s_maxlast;
     const int tile = blockIdx.x;
@@ -1000,19 +999,21 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
         }
         const int2 sl = compact_slot_n<B2 / 64>(keep, tid, s_wcnt);
         if (keep) {
-            s_id[sl.x] = id;
-            // the position in the full list, staged as bits beside the mean
-            s_xyc[sl.x] = make_float4(gl.x, gl.y, __uint_as_float((uint32_t)(todo_total - 1 - prog)), 0.f);
+            // the position in the full list and the Gaussian's id, staged as bits beside the mean
+            // (the atomic lanes used to read the id from a separate LDS array after the reduction,
+            // a wait with the whole wave behind it)
+            s_xyc[sl.x] = make_float4(gl.x, gl.y, __uint_as_float((uint32_t)(todo_total - 1 - prog)), __uint_as_float(id));
             s_co[sl.x] = cl;
             s_q[sl.x] = conic_q(cl);
             s_cd[sl.x] = rgbd[id];
         }
         __syncthreads();
         const int n = sl.y;
-        // the next Gaussian's mean / position and conic are read while this one is processed: the
-        // loop's first LDS reads otherwise waited out their latency at the top of every iteration
+        // the next Gaussian's mean / position / id and conic are read while this one is processed:
+        // the loop's first LDS reads otherwise waited out their latency at the top of every iteration
         // (blend_bwd -3.3 % at 86 VGPRs, occupancy 6 -> 5; also prefetching the colour and conic
-        // read after the skip test was slower: profiles/r5j_blend_bwd_prefetch_ab.txt)
+        // read after the skip test was slower: profiles/r4zj_blend_bwd_prefetch_ab.txt, and again at
+        // 96 VGPRs with the id staged here, occupancy 5 either way: profiles/r5g_blend_bwd_id_ab.txt)
         float4 xc_n = s_xyc[0], q_n = s_q[0];
         for (int j = 0; j < n; j++) {
             const float4 xc = xc_n;
@@ -1073,7 +1074,7 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
                                               fold32(fabsf(mxp.x) + fabsf(mxp.y), fabsf(myp.x) + fabsf(myp.y))));
             if ((lane & 15) == 15) {
                 const int row = lane >> 4;
-                float *dst = acc + (size_t)s_id[j] * ACC_STRIDE + ((row & 1) << 1) + (row >> 1);
+                float *dst = acc + (size_t)__float_as_uint(xc.w) * ACC_STRIDE + ((row & 1) << 1) + (row >> 1);
                 atomicAdd(dst, w0 * sc0);
                 atomicAdd(dst + 4, w1 * sc1);
                 atomicAdd(dst + 8, w2 * sc2);
