@@ -734,7 +734,9 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
         bias_relu(c, bv, true);
         if (SAVE) {
             trunk_mask(relu_bits(c), L);
+#ifndef DGS_DIAG_NOSAVE  // diagnostic only (wrong backward): the trunk's saved-activation stores skipped
             tile16(a.saved, Ns, s_h(L) + 16 * r, p0, lane).store(c);
+#endif
         }
         if (L == 3 && r == 0) DGS_STAMP(54);
         // this wave's rows are H k-step r / 2: every wave must have read it in this layer
@@ -913,7 +915,9 @@ __device__ __forceinline__ void bwd_block(const BwdArgs &a, bf16x8 *lds, uint32_
         gemm<8, NQB>(a.img + (size_t)(a.tL[L] + (tile0 + r) * 8) * KSLOT, lds, G_BH, 0, lane, c,
                     trunk_pre(&mk, L - 1), HGate{hwr, hrd, 0, 2u * step, true, lane});
         mask_apply(c, mk);
+#ifndef DGS_DIAG_NOSAVE  // diagnostic only (wrong dW): the dZ chain's stores skipped
         tile16(a.dz, Ns, Z_L0 + (L - 1) * 256 + 16 * r, p0, lane).store(c);
+#endif
         lds_wait_ge(hrd + (r >> 1), 16u * step, lds_peek(hrd + (r >> 1)));
 #pragma unroll
         for (int q = 0; q < NQB; q++) acc_to_lds(c[q], lds, G_BH, r, q, lane);

@@ -11,6 +11,8 @@
 // Backward: dSSIM_sum/dI = w*A + 2 I (w*B) + G (w*C) (window symmetric), plus the L1 sign term.
 #include <hip/hip_runtime.h>
 
+#include <cstring>
+
 #include "dgs_common.h"
 
 namespace dgs {
@@ -255,15 +257,23 @@ __global__ __launch_bounds__(256) void k_ssim_bwd(int H, int W, const float *__r
 }
 
 Win make_window() {
-    // utils/loss_utils.py:30-39: gauss = exp(-(x-5)^2 / (2*1.5^2)), normalised in fp32
+    // utils/loss_utils.py:30-39 builds the 11-tap Gaussian (sigma 1.5) in fp32 and filters with the
+    // fp32-ROUNDED outer product as a 2-D window; this kernel filters separably, i.e. with the exact
+    // outer product of its 1-D weights, whose total differs from the reference window's: the fp32
+    // 1-D weights sum to 1 + 4e-8, the reference's 121 rounded products to 1 - 6.9e-8. Against a target
+    // close to the render the SSIM variances cancel against C2 and that normalisation reached the loss at
+    // 4.2e-5 relative (the bench step vs the float64 reference, r5h; reproduced by a numpy emulation).
+    // The weights below are the reference's 1-D weights (torch fp32: gaussian(11, 1.5)) with taps 0/10
+    // +1 ulp and 1/9 -4 ulps, chosen so that (sum w)^2 equals the reference window's sum to 6e-11: the
+    // emulated fp32 loss then sits 7e-8 from the float64 reference (the reference's own fp32: 6e-8).
+    // tests/test_host_mirrors.py re-derives both sums from the reference formula.
+    static const uint32_t bits[11] = {0x3a86cab7u, 0x3bf8fefdu, 0x3d13758cu, 0x3ddff87fu, 0x3e5a1e1fu, 0x3e8832b0u,
+                                      0x3e5a1e1fu, 0x3ddff87fu, 0x3d13758cu, 0x3bf8fefdu, 0x3a86cab7u};
     Win w;
-    float s = 0.f;
     for (int k = 0; k < 11; k++) {
-        float v = (float)std::exp(-(double)((k - 5) * (k - 5)) / (2.0 * 1.5 * 1.5));
-        w.w[k] = v;
-        s += v;
+        uint32_t u = bits[k];
+        std::memcpy(&w.w[k], &u, 4);
     }
-    for (int k = 0; k < 11; k++) w.w[k] /= s;
     return w;
 }
 
@@ -313,4 +323,10 @@ extern "C" int dgs_l1_ssim_backward(int C, int H, int W, const float *img, const
     }
     DGS_LAUNCH_CHECK("k_ssim_bwd", false, stream);
     return DGS_OK;
+}
+
+// the fused loss's 11 separable window taps (host-side constant, no GPU needed; tests)
+extern "C" void dgs_l1_ssim_window(float *out11) {
+    const ssim::Win w = ssim::make_window();
+    for (int k = 0; k < 11; k++) out11[k] = w.w[k];
 }

@@ -83,6 +83,7 @@ _SIGS = {
     "dgs_deform_outputs": ([I], I),
     "dgs_knn_dist2": ([I, P, P, P], I),
     "dgs_l1_ssim_scratch_floats": ([I, I, I], SZ),
+    "dgs_l1_ssim_window": ([P], None),
     "dgs_l1_ssim_forward": ([I, I, I, P, P, F, P, P, P], I),
     "dgs_l1_ssim_backward": ([I, I, I, P, P, F, P, P, P, P], I),
     "dgs_adam_step": ([I, ctypes.POINTER(AdamTensor), ctypes.c_double, ctypes.c_double, ctypes.c_double, P], I),

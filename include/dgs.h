@@ -230,6 +230,9 @@ int dgs_l1_ssim_forward(int C, int H, int W, const float *img, const float *gt, 
                         float *scratch, void *stream);
 int dgs_l1_ssim_backward(int C, int H, int W, const float *img, const float *gt, float lambda,
                          const float *scratch, const float *dloss, float *grad, void *stream);
+/* The 11 separable window taps the loss kernels filter with (host-side, no GPU): the reference's 1-D
+ * Gaussian with its outer product's total matched to the reference's fp32 2-D window (ssim.hip). */
+void dgs_l1_ssim_window(float *out11);
 
 /* ---- simple-knn replacement: mean squared distance to the 3 nearest neighbours ---- */
 int dgs_knn_dist2(int P, const float *points, float *dist2, void *stream);

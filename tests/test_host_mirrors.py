@@ -113,3 +113,26 @@ def test_deform_network_state_dict_keys():
         assert len(net.kernel_params()) == len(exp)
     with pytest.raises(NotImplementedError):
         DeformNetworkBaseline(W=128)
+
+
+def test_loss_kernel_window_matches_reference_window_total():
+    """The fused loss filters separably (csrc/ssim.hip make_window): its taps must stay within a few
+    fp32 ulps of the reference's 1-D Gaussian (loss_utils.py:30-39 via deformgs.loss, which mirrors it)
+    and the total of their exact outer product must equal the total of the reference's fp32-rounded
+    2-D window (the SSIM normalisation a near-render target is sensitive to) to 1e-10."""
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    from deformgs import _lib
+    from deformgs.loss import create_window, gaussian
+    out = (ctypes.c_float * 11)()
+    _lib.load().dgs_l1_ssim_window(out)
+    w = np.array(out[:], np.float32)
+    ref1 = gaussian(11, 1.5).numpy().astype(np.float32)
+    ulps = np.abs(w.view(np.int32).astype(np.int64) - ref1.view(np.int32).astype(np.int64))
+    assert ulps.max() <= 4, ulps
+    assert np.array_equal(w, w[::-1])  # symmetric: the backward applies the same taps
+    S2 = create_window(11, 1, torch.device("cpu"), torch.float32).double().sum().item()
+    assert abs(w.astype(np.float64).sum() ** 2 - S2) < 1e-10, (w.astype(np.float64).sum() ** 2, S2)
