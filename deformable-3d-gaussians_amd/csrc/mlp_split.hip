@@ -366,8 +366,11 @@ struct Tile16 {
     __amdgpu_buffer_rsrc_t rsrc;  // base = &dst[row0 * Ns + p0]
     int voff;                     // (4kq * Ns + col) * 4 bytes
     int ns4;                      // Ns * 4 bytes
+#ifndef DGS_TILE_STORE_AUX
+#define DGS_TILE_STORE_AUX 0
+#endif
     __device__ void st(int i, int q, float v) const {
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc, voff + 64 * q, i * ns4, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc, voff + 64 * q, i * ns4, DGS_TILE_STORE_AUX);
     }
     template <int NQ_>
     __device__ void store(const f32x4 (&v)[NQ_], int q0 = 0) const {
