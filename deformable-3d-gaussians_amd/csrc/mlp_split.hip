@@ -366,8 +366,14 @@ struct Tile16 {
     __amdgpu_buffer_rsrc_t rsrc;  // base = &dst[row0 * Ns + p0]
     int voff;                     // (4kq * Ns + col) * 4 bytes
     int ns4;                      // Ns * 4 bytes
+// Cache policy of these stores (the saved activations / dZ: ~0.95 GB per launch, read back only by
+// the dW kernel after the whole launch): nt. A/B r5m against plain stores: k_fwd -1.7 %, k_bwd -3 %,
+// k_dws (their reader) -4..-6 %, step +2.5 %; sc1 (write-through, line dropped from L2) was 3-7 %
+// slower. (Without any of these stores k_fwd / k_bwd ran 7 / 15 % faster, r5j; 16-byte stores after a
+// quad transpose were 5-6 % slower, r5k; the next layer's first A fragment issued ahead of the stores
+// changed nothing, r5l.)
 #ifndef DGS_TILE_STORE_AUX
-#define DGS_TILE_STORE_AUX 0
+#define DGS_TILE_STORE_AUX 2
 #endif
     __device__ void st(int i, int q, float v) const {
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc, voff + 64 * q, i * ns4, DGS_TILE_STORE_AUX);
