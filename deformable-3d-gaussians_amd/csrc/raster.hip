@@ -1014,13 +1014,9 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
         // (blend_bwd -3.3 % at 86 VGPRs, occupancy 6 -> 5; also prefetching the colour and conic
         // read after the skip test was slower: profiles/r4zj_blend_bwd_prefetch_ab.txt, and again at
         // 96 VGPRs with the id staged here, occupancy 5 either way: profiles/r5g_blend_bwd_id_ab.txt)
-        float4 xc_n = s_xyc[0], q_n = s_q[0];
-        for (int j = 0; j < n; j++) {
-            const float4 xc = xc_n;
-            const float4 q = q_n;
-            const int jn = min(j + 1, B2 - 1);  // (the batch's last iteration reads a spare slot)
-            xc_n = s_xyc[jn];
-            q_n = s_q[jn];
+        // two Gaussians per loop trip with alternating register sets: with one per trip the compiler
+        // copied the prefetched mean / conic into the working registers every iteration (4 moves)
+        auto gauss = [&](int j, const float4 &xc, const float4 &q) {
             const uint32_t contributor = __float_as_uint(xc.z);  // position in the full list
             const f2 dx = xc.x - pfx;
             const float dy = xc.y - pfy;
@@ -1033,7 +1029,7 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
             // compare is its lane mask; of a combined predicate the compiler materialises it first)
             const float ga0 = (contributor < last0 && power.x <= 0.f) ? alpha.x : 0.f;
             const float ga1 = (contributor < last1 && power.y <= 0.f) ? alpha.y : 0.f;
-            if (__ballot(fmaxf(ga0, ga1) >= 1.f / 255.f) == 0ull) continue;  // wave-uniform
+            if (__ballot(fmaxf(ga0, ga1) >= 1.f / 255.f) == 0ull) return;  // wave-uniform
             const bool act0 = ga0 >= 1.f / 255.f, act1 = ga1 >= 1.f / 255.f;
             const float4 cd = s_cd[j];
             const float4 co = s_co[j];
@@ -1079,7 +1075,19 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
                 atomicAdd(dst + 4, w1 * sc1);
                 atomicAdd(dst + 8, w2 * sc2);
             }
+        };
+        float4 xa = s_xyc[0], qa = s_q[0], xb, qb;
+        int j = 0;
+        for (; j + 1 < n; j += 2) {
+            xb = s_xyc[j + 1];
+            qb = s_q[j + 1];
+            gauss(j, xa, qa);
+            const int j2 = min(j + 2, B2 - 1);  // (the batch's last trip reads a spare slot)
+            xa = s_xyc[j2];
+            qa = s_q[j2];
+            gauss(j + 1, xb, qb);
         }
+        if (j < n) gauss(j, xa, qa);
     }
 }
 
