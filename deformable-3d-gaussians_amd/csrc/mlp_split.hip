@@ -348,6 +348,75 @@ __device__ inline void gemm(const bf16x8 *__restrict__ Aw, const bf16x8 *lds, in
     for (int q = 0; q < NQ_; q++) acc[q] += lo[q];
 }
 
+// gemm() for TWO n-tiles per wave (the 8-wave k_fwd8): n-tile t's A image at Aw + t * astride units;
+// every B fragment read from LDS feeds both n-tiles' six MFMAs, so the activation image is read by 8
+// waves per layer instead of 16. Each (n-tile, column tile) accumulator sees the same MFMA sequence
+// as in gemm(): outputs bitwise equal to the 16-wave kernel.
+template <int NK, int NQ_, class Pre = NoPre, class Gate = NoGate, int SKIP = (1 << 20)>
+__device__ inline void gemm2(const bf16x8 *__restrict__ Aw, int astride, const bf16x8 *lds, int g0, int q0, int lane,
+                             f32x4 (&acc)[2][NQ_], Pre pre = Pre(), Gate gate = Gate()) {
+    static_assert(NK >= 1, "empty GEMM");
+    const int kq = lane >> 4, col = lane & 15;
+    const bf16x8 *Ap0 = Aw + lane, *Ap1 = Aw + astride + lane;
+    const int bunit = (g0 + kq) * UG + 16 * q0 + col;
+    constexpr int AK = KSLOT;
+    constexpr int BK = KG * UG;
+    auto bofs = [](int k) { return (k + (k >= SKIP ? 1 : 0)) * BK; };
+    auto kbase = [&](int k) {
+        int u = bunit + bofs(k);
+        asm volatile("" : "+v"(u));
+        return lds + u;
+    };
+    constexpr int RING = 2;
+    AFrag ring[RING][2];
+#pragma unroll
+    for (int k = 0; k < RING; k++)
+        if (k < NK) {
+            ring[k][0] = load_a(Ap0 + k * AK);
+            ring[k][1] = load_a(Ap1 + k * AK);
+        }
+    pre();
+    gate.need(0, gate.peek(0));
+    const bf16x8 *Bk = kbase(0);
+    AFrag b = load_b(Bk, 0);
+    f32x4 lo[2][NQ_];
+#pragma unroll
+    for (int t = 0; t < 2; t++)
+#pragma unroll
+        for (int q = 0; q < NQ_; q++) lo[t][q] = zero4();
+#pragma unroll
+    for (int k = 0; k < NK; k++) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (k > 0) gate.done(k - 1);
+        const uint32_t seen = k + 1 < NK ? gate.peek(k + 1) : 0u;
+#pragma unroll
+        for (int q = 0; q < NQ_; q++) {
+            AFrag nb;
+            if (q + 1 < NQ_) nb = load_b(Bk, q + 1);
+            else if (k + 1 < NK) {
+                gate.need(k + 1, seen);
+                Bk = kbase(k + 1);
+                nb = load_b(Bk, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            mma6(ring[k % RING][0], b, acc[0][q], lo[0][q]);
+            mma6(ring[k % RING][1], b, acc[1][q], lo[1][q]);
+            if (q + 1 < NQ_ || k + 1 < NK) b = nb;
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (k + RING < NK) {
+            ring[k % RING][0] = load_a(Ap0 + (k + RING) * AK);
+            ring[k % RING][1] = load_a(Ap1 + (k + RING) * AK);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    gate.done(NK - 1);
+#pragma unroll
+    for (int t = 0; t < 2; t++)
+#pragma unroll
+        for (int q = 0; q < NQ_; q++) acc[t][q] += lo[t][q];
+}
+
 // accumulator tile q (rows 16r + 4kq + i of this wave, point 16q + col) -> its 8-byte half of the
 // split units of group 2r + (kq >> 1) (LDS image from group gbase)
 __device__ inline void acc_to_lds(const f32x4 &v, bf16x8 *lds, int gbase, int r, int q, int lane) {
@@ -817,6 +886,134 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
     CLK_END(0);
 }
 
+
+// The training forward (saved activations, frame-uniform t folded) as 8 waves of two n-tiles
+// (k_fwd8, 512 threads, 2 waves per SIMD, 256 VGPRs): wave w owns rows 32w .. 32w + 31 of every trunk
+// layer = H k-step w, so each k-step has ONE writer (hand-off target L per layer) and 8 readers.
+// Same LDS image, saved-activation / relu'-mask layouts and arithmetic as fwd_block<true, NQB, true>.
+constexpr int NW8 = 8, NTHR8 = NW8 * 64;
+template <int NQB>
+__device__ __forceinline__ void fwd_block8(const FwdArgs &a, bf16x8 *lds, uint32_t *hwr, uint32_t *hrd, const float4 *sb,
+                                           uint32_t *s_mpend, int p0, int slot) {
+    constexpr int BMB = 16 * NQB;
+    float *lf = reinterpret_cast<float *>(lds);
+    float *stage = lf + G_H * UG * 4;
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // rows 32w .. 32w + 31: n-tiles 2w, 2w + 1
+    const int kq = lane >> 4;
+    const int pend = min(a.N, p0 + BMB);
+    const Flags F = make_flags(a.flags);
+    const size_t Ns = a.Ns;
+    const __amdgpu_buffer_rsrc_t mrsrc =
+        __builtin_amdgcn_make_buffer_rsrc(a.mask + (size_t)slot * 2 * F.nmask, 0, 0x7fffffff, 0x00020000);
+    auto trunk_mask = [&](uint32_t m, int L, int nt) {  // as fwd_block's, per n-tile
+        if ((L & 1) == 0) {
+            s_mpend[64 * nt + lane] = m;
+        } else {
+            __builtin_amdgcn_raw_buffer_store_b32(s_mpend[64 * nt + lane] | (m << 16), mrsrc, lane * 4,
+                                                  (16 * (L >> 1) + nt) * 256, 0);
+        }
+    };
+    if (tid < 8) {
+        hwr[tid] = 0;
+        hrd[tid] = 0;
+    }
+    // positional encodings (utils/time_utils.py:42-54), as fwd_block
+    if (tid < 3 * BMB) {
+        const int m = tid / 3, d = tid - 3 * m;
+        stage[d * BM + m] = p0 + m < pend ? a.xyz[3 * (size_t)p0 + tid] : 0.f;
+    }
+    if (tid < BMB) stage[63 * BM + tid] = 0.f;
+    __syncthreads();
+    for (int e = tid; e < BMB * 3 * 10; e += NTHR8) {
+        const int m = e % BMB, rr = e / BMB, d = rr % 3, i = rr / 3;
+        const bool ok = p0 + m < pend;
+        float sv, cv;
+        sincosf(stage[d * BM + m] * (float)(1 << i), &sv, &cv);
+        stage[(3 * (1 + 2 * i) + d) * BM + m] = ok ? sv : 0.f;
+        stage[(3 * (2 + 2 * i) + d) * BM + m] = ok ? cv : 0.f;
+    }
+    __syncthreads();
+    for (int e = tid; e < 64 * BMB; e += NTHR8) {  // saved x_emb rows (folded: dW reads x_emb only)
+        const int f = e / BMB, m = e % BMB;
+        a.saved[(size_t)(S_XE + f) * Ns + p0 + m] = stage[f * BM + m];
+    }
+    for (int u = tid; u < 8 * BMB; u += NTHR8) {
+        const int g = u / BMB, m = u % BMB;
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = stage[(8 * g + j) * BM + m];
+        put_unit8(lds, g, m, v);
+    }
+    lds_barrier();
+    f32x4 c[2][NQB];
+#pragma unroll 1
+    for (int L = 0; L < 8; L++) {
+        const int g0 = (L == 0 || L == 5) ? G_XE : G_H;
+        const int nk = layer_kpad_f(F, L) / 32;
+#pragma unroll
+        for (int t = 0; t < 2; t++) zero_tiles(c[t]);
+        const bf16x8 *Aw = a.img + (size_t)(a.fL[L] + 2 * w * nk) * KSLOT;
+        const int astride = nk * KSLOT;
+        const HGate hg{hwr, hrd, L == 5 ? 2 : 0, 1u * L, true, lane};
+        if (L == 0) gemm2<2, NQB>(Aw, astride, lds, g0, 0, lane, c);
+        else if (L == 5) gemm2<10, NQB, NoPre, HGate, 2>(Aw, astride, lds, g0, 0, lane, c, NoPre(), hg);
+        else gemm2<8, NQB>(Aw, astride, lds, g0, 0, lane, c, NoPre(), hg);
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+            const int nt = 2 * w + t;
+            bias_relu(c[t], sb[64 * L + 4 * nt + kq], true);
+            trunk_mask(relu_bits(c[t]), L, nt);
+            tile16(a.saved, Ns, s_h(L) + 16 * nt, p0, lane).store(c[t]);
+        }
+        // this wave's rows are H k-step w: all 8 waves must have read it in this layer
+        if (L > 0) lds_wait_ge(hrd + w, (uint32_t)NW8 * L, lds_peek(hrd + w));
+#pragma unroll
+        for (int t = 0; t < 2; t++)
+#pragma unroll
+            for (int q = 0; q < NQB; q++) acc_to_lds(c[t][q], lds, G_H, 2 * w + t, q, lane);
+        lds_signal(hwr + w, lane);
+    }
+    // heads on the last NQB waves (one column tile each), once all 8 layers' writers have signalled
+    const int hq = w - (NW8 - NQB);
+    if (hq >= 0) {
+        f32x4 c1[1] = {zero4()};
+        gemm<8, 1>(a.img + (size_t)a.fHd * KSLOT, lds, G_H, hq, lane, c1, NoPre(), HGate{hwr, hrd, 0, 8u, false, lane});
+        const float4 b = sb[8 * 64 + kq];
+        c1[0] += f32x4{b.x, b.y, b.z, b.w};
+        const int p = p0 + 16 * hq + (lane & 15);
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            if (p < pend && 4 * kq + i < F.nout) a.out[(size_t)p * F.nout + 4 * kq + i] = c1[0][i];
+    }
+}
+
+__global__ __launch_bounds__(NTHR8) void k_fwd8(FwdArgs a) {
+    __shared__ bf16x8 lds[G_FWD * UG];
+    __shared__ uint32_t hwr[8], hrd[8];
+    __shared__ int s_next;
+    __shared__ float4 s_bias[8 * 64 + 4];
+    __shared__ uint32_t s_mpend[NTHR];  // [n-tile][64 lanes]
+    for (int i = threadIdx.x; i < 8 * 64 + 4; i += NTHR8) {
+        const int L = i >> 6;
+        const float *bias = L == 8 ? a.fp + a.bHd : L == 0 ? a.tc + TC_C0 : L == 5 ? a.tc + TC_C5 : a.fp + a.bL[L];
+        s_bias[i] = reinterpret_cast<const float4 *>(bias)[i & 63];
+    }
+    for (int b = blockIdx.x;;) {
+        int nx = 0;
+        if (a.queue && threadIdx.x == 0) nx = queue_take(a.queue);
+        if (b < a.nfull) fwd_block8<NQ>(a, lds, hwr, hrd, s_bias, s_mpend, b * BM, b);
+        else fwd_block8<1>(a, lds, hwr, hrd, s_bias, s_mpend, a.nfull * BM + (b - a.nfull) * 16, b);
+        if (!a.queue) break;
+        if (threadIdx.x == 0) s_next = nx;
+        __syncthreads();
+        b = s_next;
+        if (b >= a.nblk) break;
+    }
+    if (a.queue) queue_release(a.queue);
+}
 
 // ------------------------------------------------------------------------------------------------
 // backward (dX chain): dZ_i for every layer -> scratch; deterministic
@@ -2027,7 +2224,13 @@ int forward(int flags, int N, const float *xyz, const float *t, const float *pac
     {
         ScopedTimer tm("mlp_fwd", stream);  // k_fwd only: the class's FLOP count is the trunk's + heads'
         const bool fold = P.F.uniform_t;  // t_emb folded into the biases (a.tc is set above)
-        if (saved && fold)
+        static const bool fwd8 = [] {  // DGS_MLP_FWD8=0: the 16-wave k_fwd (A/B)
+            const char *e = getenv("DGS_MLP_FWD8");
+            return !(e && e[0] == '0');
+        }();
+        if (saved && fold && fwd8)
+            hipLaunchKernelGGL(k_fwd8, dim3(grid), dim3(NTHR8), 0, stream, a);
+        else if (saved && fold)
             hipLaunchKernelGGL((k_fwd<true, true>), dim3(grid), dim3(NTHR), 0, stream, a);
         else if (saved)
             hipLaunchKernelGGL((k_fwd<true, false>), dim3(grid), dim3(NTHR), 0, stream, a);
