@@ -1150,6 +1150,111 @@ __device__ __forceinline__ void bwd_block(const BwdArgs &a, bf16x8 *lds, uint32_
     }
 }
 
+// The dX chain for a frame-uniform t (TE_ROWS = false: every training step) as 8 waves of two n-tiles
+// (k_bwd8, as k_fwd8): wave w writes dZ rows 32w .. 32w + 31 = H k-step w (one writer per k-step and
+// step, 8 readers). Same arithmetic, layouts and outputs as bwd_block<false, NQB>.
+struct MaskPre32x2 {
+    uint32_t *mk;              // [2]
+    const uint32_t *word;      // n-tile 2w's word row; 2w + 1's is 64 words on
+    int shift, lane;
+    __device__ void operator()() const {
+        mk[0] = word[lane] >> shift;
+        mk[1] = word[64 + lane] >> shift;
+    }
+};
+template <int NQB>
+__device__ __forceinline__ void bwd_block8(const BwdArgs &a, bf16x8 *lds, uint32_t *hwr, uint32_t *hrd, int p0, int slot) {
+    constexpr int BMB = 16 * NQB;
+    float *lf = reinterpret_cast<float *>(lds);
+    float *stage = lf + G_BH * UG * 4;
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const Flags F = make_flags(a.flags);
+    const size_t Ns = a.Ns;
+    const uint32_t *mwords = a.mask + (size_t)slot * 2 * F.nmask;
+    auto trunk_pre = [&](uint32_t *mk, int L) {  // layer L's output tiles 2w, 2w + 1
+        return MaskPre32x2{mk, mwords + (size_t)(16 * (L >> 1) + 2 * w) * 64, 16 * (L & 1), lane};
+    };
+    if (tid < 8) {
+        hwr[tid] = 0;
+        hrd[tid] = 0;
+    }
+    for (int e = tid; e < 32 * BMB; e += NTHR8) {  // dOut -> dz rows Z_G and the split G image
+        const int c = e / BMB, m = e % BMB;
+        const int p = p0 + m;
+        const float v = (p < a.N && c < F.nout) ? a.dout[(size_t)p * F.nout + c] : 0.f;
+        a.dz[(size_t)(Z_G + c) * Ns + p] = v;
+        stage[c * BM + m] = v;
+    }
+    __syncthreads();
+    if (tid < 4 * BMB) {
+        const int g = tid / BMB, m = tid % BMB;
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = stage[(8 * g + j) * BM + m];
+        put_unit8(lds, G_BG + g, m, v);
+    }
+    lds_barrier();
+    f32x4 c[2][NQB];
+    {  // heads^T: dH7 = W_h^T dOut (K = 32 from G) -> mask H7 -> dZ7
+        uint32_t mk[2];
+#pragma unroll
+        for (int t = 0; t < 2; t++) zero_tiles(c[t]);
+        gemm2<1, NQB>(a.img + (size_t)(a.tHd + 2 * w) * KSLOT, KSLOT, lds, G_BG, 0, lane, c, trunk_pre(mk, 7));
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+            mask_apply(c[t], mk[t]);
+            tile16(a.dz, Ns, Z_L0 + 7 * 256 + 16 * (2 * w + t), p0, lane).store(c[t]);
+        }
+#pragma unroll
+        for (int t = 0; t < 2; t++)
+#pragma unroll
+            for (int q = 0; q < NQB; q++) acc_to_lds(c[t][q], lds, G_BH, 2 * w + t, q, lane);
+        lds_signal(hwr + w, lane);
+    }
+#pragma unroll 1
+    for (int L = 7; L >= 1; L--) {
+        const uint32_t step = 8 - L;
+        const int tile0 = (L == 5) ? F_H / 16 : 0;
+        uint32_t mk[2];
+#pragma unroll
+        for (int t = 0; t < 2; t++) zero_tiles(c[t]);
+        gemm2<8, NQB>(a.img + (size_t)(a.tL[L] + (tile0 + 2 * w) * 8) * KSLOT, 8 * KSLOT, lds, G_BH, 0, lane, c,
+                      trunk_pre(mk, L - 1), HGate{hwr, hrd, 0, step, true, lane});
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+            mask_apply(c[t], mk[t]);
+            tile16(a.dz, Ns, Z_L0 + (L - 1) * 256 + 16 * (2 * w + t), p0, lane).store(c[t]);
+        }
+        lds_wait_ge(hrd + w, (uint32_t)NW8 * step, lds_peek(hrd + w));
+#pragma unroll
+        for (int t = 0; t < 2; t++)
+#pragma unroll
+            for (int q = 0; q < NQB; q++) acc_to_lds(c[t][q], lds, G_BH, 2 * w + t, q, lane);
+        lds_signal(hwr + w, lane);
+    }
+}
+
+__global__ __launch_bounds__(NTHR8) void k_bwd8(BwdArgs a) {
+    __shared__ bf16x8 lds[G_BWD * UG];
+    __shared__ uint32_t hwr[8], hrd[8];
+    __shared__ int s_next;
+    for (int b = blockIdx.x;;) {
+        int nx = 0;
+        if (a.queue && threadIdx.x == 0) nx = queue_take(a.queue);
+        if (b < a.nfull) bwd_block8<NQ>(a, lds, hwr, hrd, b * BM, b);
+        else bwd_block8<1>(a, lds, hwr, hrd, a.nfull * BM + (b - a.nfull) * 16, b);
+        if (!a.queue) break;
+        if (threadIdx.x == 0) s_next = nx;
+        __syncthreads();
+        b = s_next;
+        if (b >= a.nblk) break;
+    }
+    if (a.queue) queue_release(a.queue);
+}
+
 template <bool TE_ROWS>
 __global__ __launch_bounds__(NTHR) void k_bwd(BwdArgs a) {
     __shared__ bf16x8 lds[G_BWD * UG];
@@ -2302,7 +2407,18 @@ int backward(int flags, int N, const float *packed, const float *saved, const fl
         if (F.blender && !F.uniform_t)
             hipLaunchKernelGGL(k_bwd<true>, dim3(grid), dim3(NTHR), 0, stream, b);
         else
-            hipLaunchKernelGGL(k_bwd<false>, dim3(grid), dim3(NTHR), 0, stream, b);
+        {
+            // DGS_MLP_BWD8=1: the 8-wave k_bwd8 (bitwise equal; A/B r5u: neutral, so the 16-wave kernel
+            // stays the default)
+            static const bool bwd8 = [] {
+                const char *e = getenv("DGS_MLP_BWD8");
+                return e && e[0] == '1';
+            }();
+            if (bwd8)
+                hipLaunchKernelGGL(k_bwd8, dim3(grid), dim3(NTHR8), 0, stream, b);
+            else
+                hipLaunchKernelGGL(k_bwd<false>, dim3(grid), dim3(NTHR), 0, stream, b);
+        }
     }
     DGS_LAUNCH_CHECK("k_bwd", false, stream);
     int rc;
