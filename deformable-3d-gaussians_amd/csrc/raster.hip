@@ -431,11 +431,16 @@ __host__ __device__ inline size_t rect_place_lds(int gx, int gy, bool stage) {
 // the block's output base per tile (tile start + the block's column offset) staged in LDS when it fits
 __host__ __device__ inline bool rect_place_stage(int gx, int gy) { return rect_place_lds(gx, gy, true) <= 65536; }
 
-__global__ __launch_bounds__(256) void k_rect_place(int P, const uint32_t *__restrict__ order, const float2 *__restrict__ xy,
-                                                    const int *__restrict__ radii, int gx, int gy,
-                                                    const uint32_t *__restrict__ cnt, const uint32_t *__restrict__ tile_start,
-                                                    uint32_t cap, uint32_t *__restrict__ vals, int stage) {
-    extern __shared__ uint32_t lds[];
+// The pair positions of one block of depth-ordered Gaussians (one per thread): per wave and tile the
+// lanes' counts packed one byte each, per wave the lanes whose rectangle spans each tile column / row; a
+// pair's position is the tile start + the block's column offset + the waves below + its rank among the
+// wave's lanes. f(g, t, pos) is called per covered tile t in row-major order (k_rect_place writes the
+// list, k_rect_gather sums the deterministic blend backward's per-pair slots).
+template <class F>
+__device__ __forceinline__ void rect_walk(int P, const uint32_t *__restrict__ order, const float2 *__restrict__ xy,
+                                          const int *__restrict__ radii, int gx, int gy,
+                                          const uint32_t *__restrict__ cnt, const uint32_t *__restrict__ tile_start,
+                                          int stage, uint32_t *lds, F &&f) {
     const int T = gx * gy, G = gx + gy;
     // per tile, the four waves' counts packed one byte each (a wave adds at most 64 per tile)
     const int Tp = (T + 1) & ~1;
@@ -471,10 +476,51 @@ __global__ __launch_bounds__(256) void k_rect_place(int P, const uint32_t *__res
             const uint32_t rank = (uint32_t)__popcll(rows & ws[x]);
             // waves below: byte w-1 of the packed inclusive sums (partial sums <= 192, no carries)
             const uint32_t below = w ? ((wc[t] * 0x01010101u) >> (8 * (w - 1))) & 0xffu : 0u;
-            const uint32_t pos = (stage ? base[t] : tile_start[t] + crow[t]) + below + rank;
-            if (pos < cap) vals[pos] = g;
+            f(g, t, (stage ? base[t] : tile_start[t] + crow[t]) + below + rank);
         }
     }
+}
+
+__global__ __launch_bounds__(256) void k_rect_place(int P, const uint32_t *__restrict__ order, const float2 *__restrict__ xy,
+                                                    const int *__restrict__ radii, int gx, int gy,
+                                                    const uint32_t *__restrict__ cnt, const uint32_t *__restrict__ tile_start,
+                                                    uint32_t cap, uint32_t *__restrict__ vals, int stage) {
+    extern __shared__ uint32_t lds[];
+    rect_walk(P, order, xy, radii, gx, gy, cnt, tile_start, stage, lds, [&](uint32_t g, int, uint32_t pos) {
+        if (pos < cap) vals[pos] = g;
+    });
+}
+
+// Deterministic blend backward (dgs_raster_set_deterministic): k_blend_bwd2<DEPTH, true> leaves every
+// pair of the replayed lists two 12-float slots (one per wave of its tile: the wave's reduced sums in the
+// accumulator row's field order, zeros for a pair the wave skipped or the tile culled) instead of
+// adding them into acc with float atomics. This gather walks the same rectangles as k_rect_place, one
+// thread per depth-ordered Gaussian, and sums its pairs' slots in tile row-major order, wave 0 before
+// wave 1: a fixed order, so acc (and every gradient after it) is bitwise reproducible. A pair past the
+// launched capacity or past its tile's replayed prefix (todo) was not replayed and adds nothing,
+// exactly as with the atomics. Every row of acc is written (zeros for a Gaussian without a rectangle).
+__global__ __launch_bounds__(256) void k_rect_gather(int P, const uint32_t *__restrict__ order, const float2 *__restrict__ xy,
+                                                     const int *__restrict__ radii, int gx, int gy,
+                                                     const uint32_t *__restrict__ cnt, const uint32_t *__restrict__ tile_start,
+                                                     const uint2 *__restrict__ ranges, const uint32_t *__restrict__ tile_todo,
+                                                     uint32_t cap, const float4 *__restrict__ slot, float *__restrict__ acc,
+                                                     int stage) {
+    extern __shared__ uint32_t lds[];
+    float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0, s2 = s0;
+    rect_walk(P, order, xy, radii, gx, gy, cnt, tile_start, stage, lds, [&](uint32_t, int t, uint32_t pos) {
+        if (pos >= cap || pos - min(ranges[t].x, cap) >= tile_todo[t]) return;
+        const float4 *q = slot + 6ull * pos;
+        const float4 a0 = q[0], a1 = q[1], a2 = q[2], b0 = q[3], b1 = q[4], b2 = q[5];
+        s0 = s0 + (a0 + b0);
+        s1 = s1 + (a1 + b1);
+        s2 = s2 + (a2 + b2);
+    });
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= P) return;
+    float4 *dst = reinterpret_cast<float4 *>(acc + (size_t)order[j] * ACC_STRIDE);
+    dst[0] = s0;
+    dst[1] = s1;
+    dst[2] = s2;
 }
 
 // L (the pair count) is read on the device and clipped to the launched capacity: an overflowing
@@ -919,15 +965,19 @@ __device__ __forceinline__ f2 sel2(bool a, bool b, f2 x, f2 y) { return f2{a ? x
 
 #define BWD2_OCC
 // DEPTH: the depth output has a gradient (dL_ddepth != nullptr); without one (every training step: the
-// loss reads only the image) the depth terms, the depth colour-behind state and its loads drop out
-template <bool DEPTH>
+// loss reads only the image) the depth terms, the depth colour-behind state and its loads drop out.
+// DET: the deterministic mode (k_rect_gather): each wave writes its reduced sums for list position p
+// to slot[2 p + wave] (12 floats, zeros when it skips the Gaussian; the staging thread zeros both slots
+// of a culled one) and the tile's replayed length to tile_todo, instead of adding into acc
+template <bool DEPTH, bool DET>
 __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restrict__ ranges, const uint32_t *__restrict__ vals,
                                                    uint32_t cap, int W, int H, int gx, const float *bg,
                                                    const float2 *__restrict__ xy, const float4 *__restrict__ conic_o,
                                                    const float4 *__restrict__ rgbd, const float *__restrict__ final_T,
                                                    const uint32_t *__restrict__ n_contrib,
                                                    const float *__restrict__ dL_dpix, const float *__restrict__ dL_ddepth,
-                                                   float *__restrict__ acc) {
+                                                   float *__restrict__ acc, float *__restrict__ slot,
+                                                   uint32_t *__restrict__ tile_todo) {
     __shared__ float4 s_q[B2];   // staged conic in exponent form + opacity
     __shared__ float4 s_xyc[B2]; // mean2D x, y, list position (bits), Gaussian id (bits)
     __shared__ float4 s_co[B2];
@@ -970,6 +1020,7 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
     atomicMax(&s_maxlast, max(last0, last1));
     __syncthreads();
     const int todo_total = (int)s_maxlast;  // Gaussians past every pixel's last contributor are skipped
+    if (DET && tid == 0) tile_todo[tile] = (uint32_t)todo_total;
     const float b0 = bg[0], b1 = bg[1], b2 = bg[2];
     const f2 kbg = -Tfinal * (b0 * dp0 + b1 * dp1 + b2 * dp2);  // dL/dalpha's background term / (1 - alpha)
     const float hx = 0.5f * W, hy = 0.5f * H;
@@ -996,6 +1047,12 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
             gl = xy[id];
             cl = conic_o[id];
             keep = tile_reach(gl, cl, (float)tx0, (float)ty0);
+            if (DET && !keep) {
+                float4 *z = reinterpret_cast<float4 *>(slot + 24ull * (end - prog - 1));
+                const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                for (int i = 0; i < 6; i++) z[i] = z4;
+            }
         }
         const int2 sl = compact_slot_n<B2 / 64>(keep, tid, s_wcnt);
         if (keep) {
@@ -1029,7 +1086,10 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
             // compare is its lane mask; of a combined predicate the compiler materialises it first)
             const float ga0 = (contributor < last0 && power.x <= 0.f) ? alpha.x : 0.f;
             const float ga1 = (contributor < last1 && power.y <= 0.f) ? alpha.y : 0.f;
-            if (__ballot(fmaxf(ga0, ga1) >= 1.f / 255.f) == 0ull) return;  // wave-uniform
+            if (__ballot(fmaxf(ga0, ga1) >= 1.f / 255.f) == 0ull) {  // wave-uniform
+                if (DET && lane < 12) slot[12ull * (2 * ((uint32_t)range.x + contributor) + wv) + lane] = 0.f;
+                return;
+            }
             const bool act0 = ga0 >= 1.f / 255.f, act1 = ga1 >= 1.f / 255.f;
             const float4 cd = s_cd[j];
             const float4 co = s_co[j];
@@ -1070,10 +1130,18 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
                                               fold32(fabsf(mxp.x) + fabsf(mxp.y), fabsf(myp.x) + fabsf(myp.y))));
             if ((lane & 15) == 15) {
                 const int row = lane >> 4;
-                float *dst = acc + (size_t)__float_as_uint(xc.w) * ACC_STRIDE + ((row & 1) << 1) + (row >> 1);
-                atomicAdd(dst, w0 * sc0);
-                atomicAdd(dst + 4, w1 * sc1);
-                atomicAdd(dst + 8, w2 * sc2);
+                const int fo = ((row & 1) << 1) + (row >> 1);
+                if constexpr (DET) {
+                    float *dst = slot + 12ull * (2 * ((uint32_t)range.x + contributor) + wv) + fo;
+                    dst[0] = w0 * sc0;
+                    dst[4] = w1 * sc1;
+                    dst[8] = w2 * sc2;
+                } else {
+                    float *dst = acc + (size_t)__float_as_uint(xc.w) * ACC_STRIDE + fo;
+                    atomicAdd(dst, w0 * sc0);
+                    atomicAdd(dst + 4, w1 * sc1);
+                    atomicAdd(dst + 8, w2 * sc2);
+                }
             }
         };
         float4 xa = s_xyc[0], qa = s_q[0], xb, qb;
@@ -1593,6 +1661,8 @@ struct dgs_raster_ctx {
     // positions, and [work queue (2) | maxtodo | - | tile_todo (T)] (zeroed when (re)allocated; the
     // queue resets itself at the end of every launch, maxtodo is zeroed by k_rect_count)
     DevBuf ckb, segq;
+    // deterministic blend backward (dgs_raster_set_deterministic): [tile_todo (T, padded) | per-pair slots]
+    DevBuf det;
     bool seg_ok = false;  // this forward wrote the checkpoints
     float4 *cfin = nullptr;  // the forward's final (T, C) per pixel (segmented backward)
     bool bwd_done = false;  // a backward already consumed the accumulators (a second one re-zeroes them)
@@ -1647,6 +1717,21 @@ bool blend_segmented() {
         int want = e && e[0] == '1' ? 1 : 0;
         g_blend_seg.compare_exchange_strong(v, want);
         v = g_blend_seg.load();
+    }
+    return v == 1;
+}
+
+// DGS_DETERMINISTIC=1 / dgs_raster_set_deterministic(1): the blend backward (rect binning) writes per-pair
+// slots that k_rect_gather sums in a fixed order instead of float atomics into acc: bitwise reproducible
+// gradients at the cost of the slot traffic (96 B per pair written and read)
+std::atomic<int> g_det{-1};
+bool blend_deterministic() {
+    int v = g_det.load();
+    if (v < 0) {
+        const char *e = getenv("DGS_DETERMINISTIC");
+        int want = e && e[0] == '1' ? 1 : 0;
+        g_det.compare_exchange_strong(v, want);
+        v = g_det.load();
     }
     return v == 1;
 }
@@ -2217,11 +2302,30 @@ static int raster_backward(dgs_raster_ctx *c, const float *dL_dcolor, const floa
     const bool dbg = c->s.debug != 0;
     const int T = c->gx * c->gy;
     float *acc = (float *)c->acc.p;  // [P][12], zeroed by the forward's k_preprocess
+    // deterministic mode: k_rect_gather writes every row of acc (no zeroing needed)
+    const bool det = blend_deterministic() && c->rect_mode && !blend_one_pixel();
     // a second backward through the same forward (retain_graph, or a context kept alive): the blend
     // backward adds into the accumulators, so they are cleared first instead of doubling the gradients
-    if (c->bwd_done) DGS_HIP_CHECK(hipMemsetAsync(acc, 0, 4ull * ACC_STRIDE * P, stream));
+    if (c->bwd_done && !det) DGS_HIP_CHECK(hipMemsetAsync(acc, 0, 4ull * ACC_STRIDE * P, stream));
     c->bwd_done = true;
-    if (cap > 0) {
+    if (cap > 0 && det) {
+        const size_t tpad = ((size_t)T + 63) & ~(size_t)63;
+        if (int rc = c->det.ensure(4ull * tpad + 96ull * cap)) return rc;
+        uint32_t *todo = (uint32_t *)c->det.p;
+        float *slot = (float *)(todo + tpad);
+        {
+            ScopedTimer tm("blend_bwd", stream);
+            hipLaunchKernelGGL((dL_ddepth ? k_blend_bwd2<true, true> : k_blend_bwd2<false, true>), dim3(T), dim3(B2), 0,
+                               stream, c->ranges, c->vals, cap, c->W, c->H, c->gx, c->s.bg, c->xy, c->conic_o, c->rgbd,
+                               c->final_T, c->n_contrib, dL_dcolor, dL_ddepth, acc, slot, todo);
+        }
+        DGS_LAUNCH_CHECK("k_blend_bwd2<det>", dbg, stream);
+        ScopedTimer tm("blend_gather", stream);
+        const bool stage = rect_place_stage(c->gx, c->gy);
+        hipLaunchKernelGGL(k_rect_gather, dim3(div_up(P, 256)), dim3(256), rect_place_lds(c->gx, c->gy, stage), stream, P,
+                           c->order, c->xy, c->radii, c->gx, c->gy, c->rect_cnt, c->rect_start, c->ranges, todo, cap,
+                           (const float4 *)slot, acc, (int)stage);
+    } else if (cap > 0) {
         ScopedTimer tm("blend_bwd", stream);
         if (blend_one_pixel())
             hipLaunchKernelGGL(k_blend_bwd, dim3(T), dim3(TILE_PIX), 0, stream, c->ranges, c->vals, cap, c->W, c->H, c->gx,
@@ -2235,13 +2339,13 @@ static int raster_backward(dgs_raster_ctx *c, const float *dL_dcolor, const floa
                                c->cfin, (const float4 *)c->ckb.p, q + 4, q + 2, q, dL_dcolor, acc);
         } else
             if (dL_ddepth)
-                hipLaunchKernelGGL(k_blend_bwd2<true>, dim3(T), dim3(B2), 0, stream, c->ranges, c->vals, cap, c->W, c->H,
-                                   c->gx, c->s.bg, c->xy, c->conic_o, c->rgbd, c->final_T, c->n_contrib, dL_dcolor,
-                                   dL_ddepth, acc);
+                hipLaunchKernelGGL((k_blend_bwd2<true, false>), dim3(T), dim3(B2), 0, stream, c->ranges, c->vals, cap, c->W,
+                                   c->H, c->gx, c->s.bg, c->xy, c->conic_o, c->rgbd, c->final_T, c->n_contrib, dL_dcolor,
+                                   dL_ddepth, acc, nullptr, nullptr);
             else
-                hipLaunchKernelGGL(k_blend_bwd2<false>, dim3(T), dim3(B2), 0, stream, c->ranges, c->vals, cap, c->W, c->H,
-                                   c->gx, c->s.bg, c->xy, c->conic_o, c->rgbd, c->final_T, c->n_contrib, dL_dcolor,
-                                   nullptr, acc);
+                hipLaunchKernelGGL((k_blend_bwd2<false, false>), dim3(T), dim3(B2), 0, stream, c->ranges, c->vals, cap, c->W,
+                                   c->H, c->gx, c->s.bg, c->xy, c->conic_o, c->rgbd, c->final_T, c->n_contrib, dL_dcolor,
+                                   nullptr, acc, nullptr, nullptr);
     }
     DGS_LAUNCH_CHECK("k_blend_bwd", dbg, stream);
     const float fx = c->W / (2.f * c->s.tanfovx), fy = c->H / (2.f * c->s.tanfovy);
@@ -2323,7 +2427,7 @@ extern "C" void dgs_raster_ctx_free(dgs_raster_ctx *c) {
         g_pool.push_back(c);
     } else {
         c->geom.release(); c->bin.release(); c->img.release(); c->acc.release(); c->tmp.release(); c->rect.release();
-        c->rtot.release(); c->ckb.release(); c->segq.release();
+        c->rtot.release(); c->ckb.release(); c->segq.release(); c->det.release();
         if (c->h_total) (void)hipHostFree(c->h_total);
         delete c;
     }
@@ -2343,6 +2447,8 @@ extern "C" void dgs_debug_set_pair_cap(int device, int cap) {
 extern "C" int dgs_debug_pair_cap(int device) { return pair_cap_get(device); }
 
 extern "C" void dgs_debug_set_blend_seg(int on) { g_blend_seg.store(on ? 1 : 0); }
+extern "C" void dgs_raster_set_deterministic(int on) { g_det.store(on ? 1 : 0); }
+extern "C" int dgs_raster_get_deterministic(void) { return blend_deterministic() ? 1 : 0; }
 extern "C" int dgs_debug_get_blend_seg(void) { return blend_segmented() ? 1 : 0; }
 
 extern "C" void dgs_debug_set_binning(int mode) { g_binning.store(mode == 1 ? 1 : 0); }

@@ -107,6 +107,18 @@ def set_fused(on):
     _FUSED["on"] = bool(on)
 
 
+def set_deterministic(on):
+    """Bitwise-reproducible rasterizer gradients (libdgs: dgs_raster_set_deterministic; also
+    DGS_DETERMINISTIC=1): the blend backward sums every Gaussian's per-tile terms in a fixed order instead
+    of the reference's float atomics. Off by default (it costs the per-pair slot traffic). Returns the
+    previous setting."""
+    from . import _lib
+    lib = _lib.load()
+    before = bool(lib.dgs_raster_get_deterministic())
+    lib.dgs_raster_set_deterministic(1 if on else 0)
+    return before
+
+
 def _fused_deform_rows(pc, d_xyz, d_rotation, d_scaling):
     """The (N, 10) deformation output the three deltas are column views of, 0 for no deformation,
     or None when the deltas have any other form (then the generic torch glue runs)."""

@@ -139,6 +139,13 @@ long long dgs_debug_binning_redos(void);
 void dgs_debug_set_blend_seg(int on);
 /* The blend-backward mode in effect (DGS_BLEND_SEG or the last dgs_debug_set_blend_seg): 1 = segmented. */
 int dgs_debug_get_blend_seg(void);
+/* Deterministic blend backward (rect binning): 1 = every (tile, Gaussian) pair's gradient terms are written
+ * to per-pair slots and summed per Gaussian in a fixed order (k_rect_gather) instead of float atomics, so
+ * repeated backwards of the same forward give bitwise-identical gradients (the upstream renderCUDA backward's
+ * global atomics, SURVEY.md §2 renderCUDA row and §7 risk (c), are order-dependent). Costs the slot traffic; off by
+ * default (DGS_DETERMINISTIC=1 turns it on). Applies to backwards issued after the call. */
+void dgs_raster_set_deterministic(int on);
+int dgs_raster_get_deterministic(void);
 /* host nanoseconds spent waiting for num_rendered (and the number of waits) since process start */
 long long dgs_debug_count_wait_ns(long long *waits);
 /* dL/dscales convention. 0 (default) = the upstream CUDA op's: the gradient w.r.t. the modified scale

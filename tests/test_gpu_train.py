@@ -148,6 +148,27 @@ def test_loop_converges_and_redoes_overflows(scene):
 
 
 @pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")
+def test_deterministic_loop_is_bitwise_reproducible(scene):
+    """With the deterministic blend backward (deformgs.renderer.set_deterministic) the fused loop has no
+    order-dependent sum left (the MLP's split GEMMs, the loss reduction, Adam and densification are
+    deterministic already): two 60-iteration runs (warm-up 20, densify at 20 and 40, an opacity reset at
+    30) give bitwise-identical losses, Gaussian counts, Gaussian tensors and network updates. Without it
+    two runs differ in the last bits from the first backward on (test_loop_converges_and_redoes_overflows)."""
+    from deformgs.renderer import set_deterministic
+    opt = _opt(iterations=60, warm_up=20, densify_from_iter=10, densification_interval=20, opacity_reset_interval=30)
+    before = set_deterministic(True)
+    try:
+        ha, pa = _run(scene, True, opt=opt)
+        hb, pb = _run(scene, True, opt=opt)
+    finally:
+        set_deterministic(before)
+    assert ha["n"] == hb["n"] and ha["n"][19] != ha["n"][18]
+    np.testing.assert_array_equal(np.array(ha["loss"]), np.array(hb["loss"]))
+    for k in pa:
+        assert torch.equal(pa[k], pb[k]), k
+
+
+@pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")
 def test_config3_loop_at_size_matches_torch_glue():
     """Config 3's loop at its size (55k Gaussians @ 800x800, bouncingballs-like; synthetic scene):
     200 iterations across the warm-up boundary (deformation on from iteration 100) and densify_and_prune
