@@ -125,7 +125,7 @@ def kernel_algorithmic(name, N, P, HW, cap=None, T=None):
 
 
 KERNEL_CLASSES = ["mlp_fwd", "mlp_bwd", "mlp_dw", "mlp_dw_reduce", "mlp_tgrad", "preprocess_fwd", "depth_sort", "count", "scan",
-                  "place", "duplicate", "sort", "ranges",
+                  "place", "tile_sort", "duplicate", "sort", "ranges",
                   "blend_fwd", "blend_bwd", "blend_gather", "preprocess_bwd", "ssim_fwd", "ssim_bwd", "inputs_fwd", "inputs_bwd", "adam"]
 
 

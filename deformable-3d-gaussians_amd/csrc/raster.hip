@@ -320,7 +320,7 @@ __global__ __launch_bounds__(256) void k_rect_count(int P, const uint32_t *__res
     __syncthreads();
     const int j = blockIdx.x * 256 + threadIdx.x;
     int4 rc;
-    if (j < P && gauss_rect(order[j], xy, radii, gx, gy, rc))
+    if (j < P && gauss_rect(order ? order[j] : (uint32_t)j, xy, radii, gx, gy, rc))
         for (int y = rc.y; y < rc.w; y++)
             for (int x = rc.x; x < rc.z; x++) atomicAdd(&h[y * gx + x], 1u);
     __syncthreads();
@@ -457,7 +457,8 @@ __device__ __forceinline__ void rect_walk(int P, const uint32_t *__restrict__ or
         for (int t = tid; t < T; t += 256) base[t] = tile_start[t] + crow[t];
     for (int t = tid; t < 4 * G; t += 256) span[t] = 0ull;
     const int j = blockIdx.x * 256 + tid;
-    const uint32_t g = j < P ? order[j] : 0u;
+    // order == nullptr: index order (the per-tile sort orders each list by depth afterwards)
+    const uint32_t g = j < P ? (order ? order[j] : (uint32_t)j) : 0u;
     int4 rc = make_int4(0, 0, 0, 0);
     if (j < P && !gauss_rect(g, xy, radii, gx, gy, rc)) rc = make_int4(0, 0, 0, 0);
     __syncthreads();
@@ -486,6 +487,8 @@ __global__ __launch_bounds__(256) void k_rect_place(int P, const uint32_t *__res
                                                     const uint32_t *__restrict__ cnt, const uint32_t *__restrict__ tile_start,
                                                     uint32_t cap, uint32_t *__restrict__ vals, int stage) {
     extern __shared__ uint32_t lds[];
+    // (writing each pair's depth key beside it here, for k_tile_sort to read coalesced, made this kernel
+    // 15 us slower per step at the bench size, more than the gather it saved)
     rect_walk(P, order, xy, radii, gx, gy, cnt, tile_start, stage, lds, [&](uint32_t g, int, uint32_t pos) {
         if (pos < cap) vals[pos] = g;
     });
@@ -521,6 +524,230 @@ __global__ __launch_bounds__(256) void k_rect_gather(int P, const uint32_t *__re
     dst[0] = s0;
     dst[1] = s1;
     dst[2] = s2;
+}
+
+// Per-tile depth sort (rect binning, the default; DGS_TILE_SORT=0 restores the global depth sort): the
+// count / place kernels run over the Gaussians in index order, so every tile's list comes out in index
+// order, and each list is then sorted stably by its 32-bit depth key, i.e. by (depth, index): exactly
+// the order the global stable depth sort produced. The lists, and everything computed from them, are
+// bit-identical. k_tile_sort: one workgroup per tile, a stable LSD radix sort of up to TS_MAX entries
+// in LDS — 8-bit digits, in-wave ranking by one ballot per digit bit (as radix.hip's passes), per-wave
+// digit offsets from one block scan, scatter through LDS — skipping the passes whose digit is the same
+// for every key of the tile (the depth exponent byte, typically). Per entry and pass that is ~15 VALU;
+// a bitonic network in registers measured 37 us per step at the bench size (~55 exchange stages of
+// 64-bit keys at E = 16 per lane), one in LDS 42 us, counting ranks from LDS 66 us (O(L^2)). A list
+// longer than TS_MAX is sorted as TS_MAX-long runs into scratch as (depth << 32 | index) keys, then each
+// entry's position = its index in its run + its lower bound in every other run (binary search, the run
+// staged in LDS).
+constexpr int TS_MAX = 1024;  // (2048: no faster at the bench size, whose longest list is 591)
+constexpr int TS_THR = 256;
+struct TileSortLds {
+    union {
+        struct {
+            uint32_t key[TS_MAX], val[TS_MAX];
+        } kv;
+        unsigned long long run[TS_MAX];  // a long list's merge: one sorted run staged
+    } u;
+    uint32_t cnt[4][256];  // per-wave digit counts -> per-wave output offsets
+    uint32_t misc[8];
+};
+
+// sorts the m <= TS_MAX entries ids[0, m) (index order) stably by dkey[id]; returns the number of passes
+// run (0: the order is unchanged) with the sorted (key, id) pairs in L.u.kv
+template <int NI>
+__device__ __forceinline__ int ts_block_radix(TileSortLds &L, const uint32_t *ids, int m, const uint32_t *__restrict__ dkey,
+                                              int tid) {
+    const int lane = tid & 63, w = tid >> 6, base = w * 64 * NI;
+    const uint64_t lanes_lt = (1ull << lane) - 1ull;
+    uint32_t key[NI], val[NI];
+    uint32_t kor = 0u, kand = ~0u;
+#pragma unroll
+    for (int r = 0; r < NI; r++) {
+        const int i = base + 64 * r + lane;
+        val[r] = i < m ? ids[i] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < NI; r++) {
+        const int i = base + 64 * r + lane;
+        key[r] = i < m ? dkey[val[r]] : 0u;
+        if (i < m) {
+            kor |= key[r];
+            kand &= key[r];
+        }
+    }
+    // the bits that differ between keys: a pass over a byte none of them has runs for nothing. Wave OR /
+    // AND in DPP (row shifts, then the row broadcasts: lane 63 holds the wave's), combined across the
+    // four waves in LDS (LDS atomics from every lane on one word cost 10 us per step at the bench size)
+    {
+        int o = (int)kor, n = (int)kand;
+        o |= __builtin_amdgcn_update_dpp(0, o, 0x111, 0xf, 0xf, false);
+        n &= __builtin_amdgcn_update_dpp(-1, n, 0x111, 0xf, 0xf, false);
+        o |= __builtin_amdgcn_update_dpp(0, o, 0x112, 0xf, 0xf, false);
+        n &= __builtin_amdgcn_update_dpp(-1, n, 0x112, 0xf, 0xf, false);
+        o |= __builtin_amdgcn_update_dpp(0, o, 0x114, 0xf, 0xf, false);
+        n &= __builtin_amdgcn_update_dpp(-1, n, 0x114, 0xf, 0xf, false);
+        o |= __builtin_amdgcn_update_dpp(0, o, 0x118, 0xf, 0xf, false);
+        n &= __builtin_amdgcn_update_dpp(-1, n, 0x118, 0xf, 0xf, false);
+        o |= __builtin_amdgcn_update_dpp(0, o, 0x142, 0xa, 0xf, false);
+        n &= __builtin_amdgcn_update_dpp(-1, n, 0x142, 0xa, 0xf, false);
+        o |= __builtin_amdgcn_update_dpp(0, o, 0x143, 0xc, 0xf, false);
+        n &= __builtin_amdgcn_update_dpp(-1, n, 0x143, 0xc, 0xf, false);
+        if (lane == 63) {
+            L.misc[2 * w] = (uint32_t)o;
+            L.misc[2 * w + 1] = (uint32_t)n;
+        }
+    }
+    __syncthreads();
+    uint32_t kor4 = 0u, kand4 = ~0u;
+#pragma unroll
+    for (int ww = 0; ww < 4; ww++) {
+        kor4 |= L.misc[2 * ww];
+        kand4 &= L.misc[2 * ww + 1];
+    }
+    __syncthreads();  // misc is reused by the passes' scans
+#ifdef TS_DIAG_PASSES  // diagnostic builds (tools/build_diag.sh): at most this many passes (wrong order)
+    const uint32_t diff = TS_DIAG_PASSES == 0 ? 0u : (kor4 ^ kand4) & (0xffffffffu >> (32 - 8 * (TS_DIAG_PASSES + (TS_DIAG_PASSES == 0))));  // wrong order
+#else
+    const uint32_t diff = kor4 ^ kand4;
+#endif
+    int passes = 0;
+    for (int shift = 0; shift < 32; shift += 8) {
+        if (((diff >> shift) & 255u) == 0u) continue;  // workgroup-uniform
+        passes++;
+#pragma unroll
+        for (int ww = 0; ww < 4; ww++) L.cnt[ww][tid] = 0;
+        __syncthreads();
+        uint32_t rank[NI];
+#pragma unroll
+        for (int r = 0; r < NI; r++) {
+            const bool ok = base + 64 * r + lane < m;
+            const uint32_t d = (key[r] >> shift) & 255u;
+            uint64_t mk = __ballot(ok);
+#pragma unroll
+            for (int bb = 0; bb < 8; bb++) {
+                const bool bit = (d >> bb) & 1u;
+                const uint64_t bal = __ballot(bit);
+                mk &= bit ? bal : ~bal;
+            }
+            const int leader = mk ? __ffsll((unsigned long long)mk) - 1 : 0;
+            uint32_t b0 = 0;
+            if (ok && lane == leader) {
+                b0 = L.cnt[w][d];
+                L.cnt[w][d] = b0 + (uint32_t)__popcll(mk);
+            }
+            b0 = (uint32_t)__shfl((int)b0, leader);
+            rank[r] = b0 + (uint32_t)__popcll(mk & lanes_lt);
+        }
+        __syncthreads();
+        {
+            const int d = tid;  // one thread per digit: per-wave offsets, then the digit starts
+            uint32_t c[4], tot = 0;
+#pragma unroll
+            for (int ww = 0; ww < 4; ww++) {
+                c[ww] = L.cnt[ww][d];
+                tot += c[ww];
+            }
+            // inclusive wave scan in DPP: row shifts 1/2/4/8, then the row broadcasts 15 / 31
+            int x = (int)tot;
+            x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);
+            x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);
+            x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);
+            x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);
+            x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);
+            x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);
+            if (lane == 63) L.misc[w] = (uint32_t)x;
+            __syncthreads();
+            uint32_t start = (uint32_t)x - tot;
+            for (int ww = 0; ww < w; ww++) start += L.misc[ww];
+#pragma unroll
+            for (int ww = 0; ww < 4; ww++) {
+                L.cnt[ww][d] = start;
+                start += c[ww];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < NI; r++) {
+            if (base + 64 * r + lane < m) {
+                const uint32_t dst = L.cnt[w][(key[r] >> shift) & 255u] + rank[r];
+                L.u.kv.key[dst] = key[r];
+                L.u.kv.val[dst] = val[r];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < NI; r++) {
+            const int i = base + 64 * r + lane;
+            if (i < m) {
+                key[r] = L.u.kv.key[i];
+                val[r] = L.u.kv.val[i];
+            }
+        }
+    }
+    return passes;
+}
+__device__ __forceinline__ int ts_block_any(TileSortLds &L, const uint32_t *ids, int m, const uint32_t *__restrict__ dkey,
+                                            int tid) {
+    if (m <= 256) return ts_block_radix<1>(L, ids, m, dkey, tid);
+    if (m <= 512) return ts_block_radix<2>(L, ids, m, dkey, tid);
+    return ts_block_radix<4>(L, ids, m, dkey, tid);
+}
+
+__global__ __launch_bounds__(TS_THR) void k_tile_sort(const uint2 *__restrict__ ranges, uint32_t cap,
+                                                      const uint32_t *__restrict__ dkey, uint32_t *__restrict__ vals,
+                                                      unsigned long long *__restrict__ scratch,
+                                                      uint32_t *__restrict__ spos) {
+    __shared__ TileSortLds L;
+    const int tid = threadIdx.x;
+    const uint2 rg = ranges[blockIdx.x];
+    const uint32_t a = min(rg.x, cap), b = min(rg.y, cap);
+    const int len = (int)(b - a);
+    if (len <= 1) return;
+    uint32_t *v = vals + a;
+    if (len <= TS_MAX) {
+        // every entry is read (into registers) before the first barrier; written back after the sort
+        if (ts_block_any(L, v, len, dkey, tid) == 0) return;
+        for (int i = tid; i < len; i += TS_THR) v[i] = L.u.kv.val[i];
+        return;
+    }
+    // a long list: TS_MAX-long runs sorted into scratch as (depth << 32 | index), then merged by rank
+    unsigned long long *sc = scratch + a;
+    uint32_t *ps = spos + a;
+    for (int c0 = 0; c0 < len; c0 += TS_MAX) {
+        const int m = min(TS_MAX, len - c0);
+        __syncthreads();  // L is reused
+        if (ts_block_any(L, v + c0, m, dkey, tid) == 0) {  // all keys equal: the run is in index order
+            for (int i = tid; i < m; i += TS_THR) {
+                const uint32_t g = v[c0 + i];
+                sc[c0 + i] = ((unsigned long long)dkey[g] << 32) | g;
+            }
+        } else {
+            for (int i = tid; i < m; i += TS_THR) sc[c0 + i] = ((unsigned long long)L.u.kv.key[i] << 32) | L.u.kv.val[i];
+        }
+        for (int i = tid; i < m; i += TS_THR) ps[c0 + i] = (uint32_t)i;  // its rank in its own run
+    }
+    __threadfence();
+    __syncthreads();
+    // per run q staged in LDS: every entry of the other runs adds its lower bound in q
+    for (int q0 = 0; q0 < len; q0 += TS_MAX) {
+        const int mq = min(TS_MAX, len - q0);
+        __syncthreads();  // the previous run's searches are done
+        for (int i = tid; i < mq; i += TS_THR) L.u.run[i] = __hip_atomic_load(sc + q0 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        for (int i = tid; i < len; i += TS_THR) {
+            if (i >= q0 && i < q0 + mq) continue;
+            const unsigned long long k = __hip_atomic_load(sc + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int lo = 0, hi = mq;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (L.u.run[mid] < k) lo = mid + 1;
+                else hi = mid;
+            }
+            ps[i] += (uint32_t)lo;  // this thread's own entry
+        }
+    }
+    // every list entry was read in the run phase: the list is overwritten in place
+    for (int i = tid; i < len; i += TS_THR) v[ps[i]] = (uint32_t)__hip_atomic_load(sc + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // L (the pair count) is read on the device and clipped to the launched capacity: an overflowing
@@ -1674,6 +1901,7 @@ struct dgs_raster_ctx {
     uint8_t *clamped = nullptr;
     uint32_t *vals = nullptr;
     bool rect_mode = false;  // rect binning (k_rect_*) instead of duplicate + tile sort
+    bool tsort = false;      // rect binning in index order + per-tile depth sort (k_tile_sort), no global depth sort
     uint32_t *rect_cnt = nullptr, *rect_start = nullptr, *rect_total = nullptr;
     unsigned long long *rect_tot = nullptr;  // tile totals tagged with a launch generation (k_rect_colscan)
     uint2 *ranges = nullptr;
@@ -1732,6 +1960,20 @@ bool blend_deterministic() {
         int want = e && e[0] == '1' ? 1 : 0;
         g_det.compare_exchange_strong(v, want);
         v = g_det.load();
+    }
+    return v == 1;
+}
+
+// DGS_TILE_SORT=0: rect binning over the global depth sort's order (k_rect_* on depth-ordered Gaussians)
+// instead of index order + the per-tile depth sort (k_tile_sort, the default); dgs_debug_set_tile_sort
+std::atomic<int> g_tile_sort{-1};
+bool tile_sort_enabled() {
+    int v = g_tile_sort.load();
+    if (v < 0) {
+        const char *e = getenv("DGS_TILE_SORT");
+        int want = e && e[0] == '0' ? 0 : 1;
+        g_tile_sort.compare_exchange_strong(v, want);
+        v = g_tile_sort.load();
     }
     return v == 1;
 }
@@ -1985,17 +2227,26 @@ static int bin_and_blend(dgs_raster_ctx *c, int cap, int P, int device, hipStrea
                          float *out_depth) {
     const int T = c->gx * c->gy;
     if (c->rect_mode) {
-        if (int rc = c->bin.ensure(4ull * std::max(cap, 1) + 256)) return rc;
+        // tile sort: the lists, then 8 + 4 bytes of scratch per pair for lists longer than k_tile_sort's LDS
+        const size_t vbytes = align_up(4ull * std::max(cap, 1) + 256);
+        if (int rc = c->bin.ensure(vbytes + (c->tsort ? 12ull * std::max(cap, 1) + 256 : 0))) return rc;
         c->vals = (uint32_t *)c->bin.p;
         const int nb = div_up(P, 256);
         if (cap > 0) {
             ScopedTimer tm("place", stream);
             const bool stage = rect_place_stage(c->gx, c->gy);
-            hipLaunchKernelGGL(k_rect_place, dim3(nb), dim3(256), rect_place_lds(c->gx, c->gy, stage), stream, P, c->order,
-                               c->xy, c->radii, c->gx, c->gy, c->rect_cnt, c->rect_start, (uint32_t)cap, c->vals,
-                               (int)stage);
+            hipLaunchKernelGGL(k_rect_place, dim3(nb), dim3(256), rect_place_lds(c->gx, c->gy, stage), stream, P,
+                               c->tsort ? nullptr : c->order, c->xy, c->radii, c->gx, c->gy, c->rect_cnt, c->rect_start,
+                               (uint32_t)cap, c->vals, (int)stage);
         }
         DGS_LAUNCH_CHECK("k_rect_place", dbg, stream);
+        if (cap > 0 && c->tsort) {
+            ScopedTimer tm("tile_sort", stream);
+            unsigned long long *scr = (unsigned long long *)((char *)c->bin.p + vbytes);
+            hipLaunchKernelGGL(k_tile_sort, dim3(T), dim3(TS_THR), 0, stream, c->ranges, (uint32_t)cap, c->dkey, c->vals, scr,
+                               (uint32_t *)(scr + std::max(cap, 1)));
+            DGS_LAUNCH_CHECK("k_tile_sort", dbg, stream);
+        }
     } else if (cap > 0) {  // k_duplicate clears c->ranges
         // 16-bit tile keys up to 65535 tiles (4080 x 4080 pixels), 32-bit beyond
         const int rc = T < 65535 ? bin_tiles<uint16_t>(c, cap, P, device, stream, dbg)
@@ -2158,6 +2409,9 @@ static int raster_forward(const dgs_raster_settings *s, int P, int M, const floa
         if (c->rtot.cap != tot_cap) DGS_HIP_CHECK(hipMemsetAsync(c->rtot.p, 0, c->rtot.cap, stream));
         c->rect_tot = (unsigned long long *)c->rtot.p;
     }
+    // the deterministic backward's gather re-walks the rectangles in the depth-sorted order the lists
+    // were placed in, so it keeps the global depth sort
+    c->tsort = c->rect_mode && tile_sort_enabled() && !blend_deterministic();
     c->seg_ok = c->rect_mode && blend_segmented();
     if (c->seg_ok) {
         const size_t cap0 = c->segq.cap;
@@ -2182,7 +2436,7 @@ static int raster_forward(const dgs_raster_settings *s, int P, int M, const floa
                                out_visible);
         }
         DGS_LAUNCH_CHECK("k_preprocess", dbg, stream);
-        {
+        if (!c->tsort) {
             // Gaussians by depth (stable on the index), then the pair offsets in that order
             ScopedTimer tm("depth_sort", stream);
             if (hipcub_sort()) {
@@ -2213,7 +2467,8 @@ static int raster_forward(const dgs_raster_settings *s, int P, int M, const floa
             *(volatile uint32_t *)c->h_total = COUNT_PENDING;  // k_rect_colscan overwrites it
             {
                 ScopedTimer tm("count", stream);
-                hipLaunchKernelGGL(k_rect_count, dim3(nb), dim3(256), 4ull * T, stream, P, c->order, c->xy, c->radii, c->gx,
+                hipLaunchKernelGGL(k_rect_count, dim3(nb), dim3(256), 4ull * T, stream, P, c->tsort ? nullptr : c->order,
+                                   c->xy, c->radii, c->gx,
                                    c->gy, c->rect_cnt, c->rect_total, c->seg_ok ? (uint32_t *)c->segq.p + 2 : nullptr);
             }
             DGS_LAUNCH_CHECK("k_rect_count", dbg, stream);
@@ -2303,7 +2558,7 @@ static int raster_backward(dgs_raster_ctx *c, const float *dL_dcolor, const floa
     const int T = c->gx * c->gy;
     float *acc = (float *)c->acc.p;  // [P][12], zeroed by the forward's k_preprocess
     // deterministic mode: k_rect_gather writes every row of acc (no zeroing needed)
-    const bool det = blend_deterministic() && c->rect_mode && !blend_one_pixel();
+    const bool det = blend_deterministic() && c->rect_mode && !c->tsort && !blend_one_pixel();
     // a second backward through the same forward (retain_graph, or a context kept alive): the blend
     // backward adds into the accumulators, so they are cleared first instead of doubling the gradients
     if (c->bwd_done && !det) DGS_HIP_CHECK(hipMemsetAsync(acc, 0, 4ull * ACC_STRIDE * P, stream));
@@ -2448,6 +2703,8 @@ extern "C" int dgs_debug_pair_cap(int device) { return pair_cap_get(device); }
 
 extern "C" void dgs_debug_set_blend_seg(int on) { g_blend_seg.store(on ? 1 : 0); }
 extern "C" void dgs_raster_set_deterministic(int on) { g_det.store(on ? 1 : 0); }
+extern "C" void dgs_debug_set_tile_sort(int on) { g_tile_sort.store(on ? 1 : 0); }
+extern "C" int dgs_debug_get_tile_sort(void) { return tile_sort_enabled() ? 1 : 0; }
 extern "C" int dgs_raster_get_deterministic(void) { return blend_deterministic() ? 1 : 0; }
 extern "C" int dgs_debug_get_blend_seg(void) { return blend_segmented() ? 1 : 0; }
 

@@ -146,6 +146,13 @@ int dgs_debug_get_blend_seg(void);
  * default (DGS_DETERMINISTIC=1 turns it on). Applies to backwards issued after the call. */
 void dgs_raster_set_deterministic(int on);
 int dgs_raster_get_deterministic(void);
+/* Rect binning order: 1 (default; DGS_TILE_SORT=0 turns it off) = the Gaussians are binned in index order
+ * and each tile's list is then sorted by (depth, index) in its own workgroup (k_tile_sort); 0 = a global
+ * stable depth sort first (4 radix passes), lists placed in that order. The lists are identical either
+ * way. The deterministic backward uses the global order (it re-walks the placement). Applies to forwards
+ * issued after the call. */
+void dgs_debug_set_tile_sort(int on);
+int dgs_debug_get_tile_sort(void);
 /* host nanoseconds spent waiting for num_rendered (and the number of waits) since process start */
 long long dgs_debug_count_wait_ns(long long *waits);
 /* dL/dscales convention. 0 (default) = the upstream CUDA op's: the gradient w.r.t. the modified scale

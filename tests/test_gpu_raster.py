@@ -494,3 +494,40 @@ def test_deterministic_blend_backward(case):
     for k in grads:
         ref = ra[3][k]
         np.testing.assert_allclose(grads[k], ref, rtol=1e-4, atol=1e-6 * max(1.0, np.abs(ref).max()), err_msg=k)
+
+
+@pytest.mark.parametrize("case", [
+    # N, H, W, cam, scale_boost: config 1; ragged tiles with big Gaussians; lists far beyond k_tile_sort's
+    # 2048-entry LDS sort (sorted runs merged by rank: up to ~10 runs per tile); the bench workload
+    (5000, 256, 256, 0, 0.0), (2000, 61, 83, 3, 1.0), (20000, 64, 80, 1, 3.0), (100_000, 800, 800, 0, 0.0)])
+def test_tile_sort_matches_global_depth_sort(case):
+    """Rect binning in index order + k_tile_sort (the default) vs the global stable depth sort
+    (dgs_debug_set_tile_sort(0)): the tile lists are the same, so the image, depth and radii are bitwise
+    equal and the gradients equal up to the float atomics' arrival order (1e-4 relative + 1e-6 of each
+    tensor's max); the tile-sorted result also passes every oracle check."""
+    from deformgs import _lib
+    lib = _lib.load()
+    N, H, W, ci, boost = case
+    inputs, rs, _ = scene(N, H, W, cam_index=ci, scale_boost=boost, seed=21)
+    rng = np.random.default_rng(11)
+    dcolor = rng.standard_normal((3, H, W)).astype(np.float32)
+    res = {}
+    before = lib.dgs_debug_get_tile_sort()
+    try:
+        for ts in (0, 1):
+            lib.dgs_debug_set_tile_sort(ts)
+            res[ts] = _run_gpu(inputs, rs, dcolor, None) + (_run_gpu.num_rendered,)
+    finally:
+        lib.dgs_debug_set_tile_sort(before)
+    for a, b in zip(res[1][:3], res[0][:3]):
+        np.testing.assert_array_equal(a, b)
+    assert res[1][4] == res[0][4]
+    for k in res[1][3]:
+        ref = res[0][3][k]
+        np.testing.assert_allclose(res[1][3][k], ref, rtol=1e-4, atol=1e-6 * max(1.0, np.abs(ref).max()), err_msg=k)
+    if N <= 20000:
+        o, g = oracle_run(inputs, rs, dcolor, None)
+        color, radii, depth, grads, nr = res[1]
+        _check(o, g, color, radii, depth, grads,
+               [("means3D", "means3D"), ("opacities", "opacities"), ("means2D", "means2D")],
+               nr=nr, tag=f"raster_tile_sort[{N}x{H}x{W}]")
