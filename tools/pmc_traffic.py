@@ -16,12 +16,13 @@ from collections import defaultdict
 
 CLASSES = {  # bench.py kernel class -> substring(s) of the device symbol (split-bf16 | exact-fp32 MLP)
     # mlp_fwd: the training forward (saved activations) only, the launches bench.py times
-    "mlp_fwd": ("mlps::k_fwd<true", "k_mlp_fwd<true"), "mlp_bwd": ("mlps::k_bwd", "k_mlp_bwd"),
+    "mlp_fwd": ("mlps::k_fwd8(", "mlps::k_fwd<true", "k_mlp_fwd<true"), "mlp_bwd": ("mlps::k_bwd", "k_mlp_bwd"),
     "mlp_dw": ("mlp::k_dw(", "mlps::k_dw(", "mlps::k_dws(", "mlps::k_dwg(", "mlp4k_dw"), "mlp_dw_reduce": "k_dw_reduce",
     "preprocess_fwd": ("k_preprocess(", "k_preprocess<"), "duplicate": "k_duplicate", "ranges": "k_ranges",
     "blend_fwd": "k_blend_fwd", "blend_bwd": "k_blend_bwd", "preprocess_bwd": "k_preprocess_bwd",
     "ssim_fwd": "k_ssim_fwd", "ssim_bwd": "k_ssim_bwd", "adam": "k_adam", "inputs_fwd": "k_inputs_fwd",
-    "inputs_bwd": "k_inputs_bwd",
+    "inputs_bwd": "k_inputs_bwd", "count": "k_rect_count", "scan": "k_rect_colscan", "place": "k_rect_place",
+    "tile_sort": "k_tile_sort", "depth_sort": ("radix::k_hist", "radix::k_scatter"), "blend_gather": "k_rect_gather",
 }
 
 

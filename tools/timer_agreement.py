@@ -9,7 +9,8 @@ import json
 import os
 import sys
 
-SYMBOL = {"mlp_fwd": "mlps::k_fwd<true", "mlp_bwd": "mlps::k_bwd<", "mlp_dw": "mlps::k_dws("}
+SYMBOL = {"mlp_fwd": ("mlps::k_fwd8(", "mlps::k_fwd<true"), "mlp_bwd": ("mlps::k_bwd<", "mlps::k_bwd8("),
+          "mlp_dw": ("mlps::k_dws(",)}
 
 
 def main():
@@ -19,7 +20,8 @@ def main():
     r = json.loads(line)["roofline"]
     f = glob.glob(os.path.join(root, "trace", "*kernel_trace.csv"))[0]
     rows = sorted(csv.DictReader(open(f)), key=lambda x: int(x["Start_Timestamp"]))
-    d = [(int(x["End_Timestamp"]) - int(x["Start_Timestamp"])) / 1e6 for x in rows if SYMBOL[r["kernel"]] in x["Kernel_Name"]]
+    d = [(int(x["End_Timestamp"]) - int(x["Start_Timestamp"])) / 1e6 for x in rows
+         if any(k in x["Kernel_Name"] for k in SYMBOL[r["kernel"]])]
     timed = d[-steps:]
     sampled = timed[0::4] if r["launches"] < steps else timed
     rp = sum(sampled) / len(sampled)

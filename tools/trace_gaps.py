@@ -8,7 +8,8 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 # step boundaries: each step launches exactly one MLP forward (split-bf16 k_fwd or exact k_mlp_fwd)
 starts = [int(r["Start_Timestamp"]) for r in rows
-          if "k_mlp_fwd<true>" in r["Kernel_Name"] or "mlps::k_fwd<true" in r["Kernel_Name"]]  # <SAVE[, FOLD]>
+          if "k_mlp_fwd<true>" in r["Kernel_Name"] or "mlps::k_fwd<true" in r["Kernel_Name"]  # <SAVE[, FOLD]>
+          or "mlps::k_fwd8(" in r["Kernel_Name"]]
 if len(starts) < 3:
     sys.exit("not enough steps")
 # last 5 complete timed steps: the final k_fwd is bench.py's pair-count render after the timed loop,
