@@ -1190,6 +1190,125 @@ __device__ __forceinline__ int2 compact_slot_n(bool keep, int tid, uint32_t *s_w
 
 __device__ __forceinline__ f2 sel2(bool a, bool b, f2 x, f2 y) { return f2{a ? x.x : y.x, b ? x.y : y.y}; }
 
+// Forward blend, two pixels per lane (DGS_BLEND_FWD2=1; the segmented backward's checkpoints stay on
+// k_blend_fwd): k_blend_bwd2's layout — a 16x16 tile as two waves, lane l of wave w holding the pixel
+// pair (l & 7, 8 w + l / 8) and (8 + l & 7, same row), 128-Gaussian batches — so every staged
+// Gaussian's broadcast LDS reads serve two pixels and the per-pixel arithmetic runs on packed fp32
+// pairs. Per pixel the operations, their order and the fused forms are k_blend_fwd's: the image,
+// the transmittance and n_contrib are bitwise the same (GPU test).
+__global__ __launch_bounds__(B2) void k_blend_fwd2(const uint2 *__restrict__ ranges, const uint32_t *__restrict__ vals,
+                                                   uint32_t cap, int W, int H, int gx, const float2 *__restrict__ xy,
+                                                   const float4 *__restrict__ conic_o, const float4 *__restrict__ rgbd,
+                                                   const float *bg, float *__restrict__ final_T,
+                                                   uint32_t *__restrict__ n_contrib, float *__restrict__ out_color,
+                                                   float *__restrict__ out_depth) {
+    __shared__ float2 s_xy[B2];
+    __shared__ float4 s_co[B2];
+    __shared__ float4 s_cd[B2];
+    __shared__ int s_pos[B2];
+    __shared__ uint32_t s_wcnt[B2 / 64];
+    const int tile = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int tx0i = (tile % gx) * TILE_X, ty0i = (tile / gx) * TILE_Y;
+    const float tx0 = (float)tx0i, ty0 = (float)ty0i;
+    const int px0 = tx0i + (lane & 7), px1 = px0 + 8, py = ty0i + 8 * wv + (lane >> 3);
+    const bool in0 = px0 < W && py < H, in1 = px1 < W && py < H;
+    const f2 pfx = f2{(float)px0, (float)px1};
+    const float pfy = (float)py;
+    uint2 range = ranges[tile];
+    range.x = min(range.x, cap);  // a speculative launch under capacity (redone at the exact size)
+    range.y = min(range.y, cap);
+    const int todo_total = (int)(range.y - range.x);
+    const int rounds = div_up(todo_total, B2);
+    bool done0 = !in0, done1 = !in1;
+    const f2 zero = f2{0.f, 0.f};
+    f2 T = f2{1.f, 1.f}, C0 = zero, C1 = zero, C2 = zero, Dd = zero;
+    uint32_t last0 = 0, last1 = 0;
+    for (int r = 0; r < rounds; r++) {
+        if (__syncthreads_count(done0 && done1) == B2) break;
+        const int prog = r * B2 + tid;
+        bool keep = false;
+        uint32_t id = 0;
+        float2 gl;
+        float4 cl;
+        if ((int)range.x + prog < (int)range.y) {
+            id = vals[range.x + prog];
+            gl = xy[id];
+            cl = conic_o[id];
+            keep = tile_reach(gl, cl, tx0, ty0);
+        }
+        const int2 sl = compact_slot_n<B2 / 64>(keep, tid, s_wcnt);
+        if (keep) {
+            s_xy[sl.x] = gl;
+            s_co[sl.x] = conic_q(cl);
+            s_cd[sl.x] = rgbd[id];
+            s_pos[sl.x] = prog;
+        }
+        const int n = sl.y, n4 = (sl.y + 3) & ~3;  // padded with inert entries, as k_blend_fwd
+        if (tid >= n && tid < n4) {
+            s_xy[tid] = make_float2(0.f, 0.f);
+            s_co[tid] = make_float4(0.f, 0.f, 0.f, 0.f);
+            s_cd[tid] = make_float4(0.f, 0.f, 0.f, 0.f);
+            s_pos[tid] = 0;
+        }
+        __syncthreads();
+        int lastj0 = 0, lastj1 = 0;
+        for (int j0 = 0; j0 < n4; j0 += 4) {
+            if (__ballot(!(done0 && done1)) == 0ull) break;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int j = j0 + u;
+                const float2 g = s_xy[j];
+                const float4 q = s_co[j];
+                const float4 cd = s_cd[j];
+                const f2 dx = g.x - pfx;
+                const float dy = g.y - pfy;
+                const f2 power = f2{q_power(q, dx.x, dy), q_power(q, dx.y, dy)};
+                const f2 alpha = f2{fminf(0.99f, q.w * __builtin_amdgcn_exp2f(power.x)),
+                                    fminf(0.99f, q.w * __builtin_amdgcn_exp2f(power.y))};
+                const f2 testT = T * (1.f - alpha);
+                bool use0 = !done0 && !(power.x > 0.f) && !(alpha.x < 1.f / 255.f);
+                bool use1 = !done1 && !(power.y > 0.f) && !(alpha.y < 1.f / 255.f);
+                const bool stop0 = use0 && testT.x < 0.0001f, stop1 = use1 && testT.y < 0.0001f;
+                done0 = done0 || stop0;
+                done1 = done1 || stop1;
+                use0 = use0 && !stop0;
+                use1 = use1 && !stop1;
+                const f2 w = sel2(use0, use1, alpha * T, zero);
+                C0 += cd.x * w;
+                C1 += cd.y * w;
+                C2 += cd.z * w;
+                Dd += cd.w * w;
+                T = sel2(use0, use1, testT, T);
+                lastj0 = use0 ? j + 1 : lastj0;
+                lastj1 = use1 ? j + 1 : lastj1;
+            }
+        }
+        if (lastj0) last0 = (uint32_t)s_pos[lastj0 - 1] + 1u;  // list position + 1 (n_contrib of the full list)
+        if (lastj1) last1 = (uint32_t)s_pos[lastj1 - 1] + 1u;
+    }
+    const int HW = H * W;
+    if (in0) {
+        const int pid = py * W + px0;
+        final_T[pid] = T.x;
+        n_contrib[pid] = last0;
+        out_color[pid] = C0.x + T.x * bg[0];
+        out_color[HW + pid] = C1.x + T.x * bg[1];
+        out_color[2 * HW + pid] = C2.x + T.x * bg[2];
+        out_depth[pid] = Dd.x;
+    }
+    if (in1) {
+        const int pid = py * W + px1;
+        final_T[pid] = T.y;
+        n_contrib[pid] = last1;
+        out_color[pid] = C0.y + T.y * bg[0];
+        out_color[HW + pid] = C1.y + T.y * bg[1];
+        out_color[2 * HW + pid] = C2.y + T.y * bg[2];
+        out_depth[pid] = Dd.y;
+    }
+}
+
 #define BWD2_OCC
 // DEPTH: the depth output has a gradient (dL_ddepth != nullptr); without one (every training step: the
 // loss reads only the image) the depth terms, the depth colour-behind state and its loads drop out.
@@ -1964,6 +2083,19 @@ bool blend_deterministic() {
     return v == 1;
 }
 
+// DGS_BLEND_FWD2=1 / dgs_debug_set_blend_fwd2: the two-pixels-per-lane forward blend (k_blend_fwd2)
+std::atomic<int> g_fwd2{-1};
+bool blend_fwd2() {
+    int v = g_fwd2.load();
+    if (v < 0) {
+        const char *e = getenv("DGS_BLEND_FWD2");
+        int want = e && e[0] == '1' ? 1 : 0;
+        g_fwd2.compare_exchange_strong(v, want);
+        v = g_fwd2.load();
+    }
+    return v == 1;
+}
+
 // DGS_TILE_SORT=0: rect binning over the global depth sort's order (k_rect_* on depth-ordered Gaussians)
 // instead of index order + the per-tile depth sort (k_tile_sort, the default); dgs_debug_set_tile_sort
 std::atomic<int> g_tile_sort{-1};
@@ -2131,8 +2263,11 @@ dgs_raster_ctx *ctx_acquire(int device, hipStream_t stream) {
 
 // The pair count of this frame on the host. Sort binning: the pinned word behind count_ev. Rect
 // binning: k_rect_colscan stores the count into the coherent pinned word itself, so the host polls
-// the word (no event record in the stream: one costs ~6 us of GPU idle); the stream is queried
-// every 1024 polls so a failed launch cannot spin forever.
+// the word (no event record in the stream: one costs ~6 us of GPU idle). Only a wait longer than
+// 20 ms queries the stream (then every 1024 polls), so a failed launch cannot spin forever: a query
+// of a busy stream appends a completion marker at its tail, which cost ~6 us of GPU idle before the
+// next launch (the optimizer's, when the native step waits for its own count at its end) on every step
+// when the stream was queried every 1024 polls (profiles/r5ts_trace_summary.txt).
 constexpr uint32_t COUNT_PENDING = 0xffffffffu;
 std::atomic<long long> g_count_wait_ns{0}, g_count_waits{0};  // host time spent waiting for num_rendered
 
@@ -2152,9 +2287,13 @@ static int wait_count_impl(dgs_raster_ctx *c, hipStream_t stream, int &nr) {
         return DGS_OK;
     }
     volatile uint32_t *w = c->h_total;
+    const auto t0 = std::chrono::steady_clock::now();
+    bool slow = false;
     for (uint32_t i = 1;; i++) {
         uint32_t v = *w;
-        if (v == COUNT_PENDING && (i & 1023) == 0) {
+        if (v == COUNT_PENDING && (i & 1023) == 0 && !slow)
+            slow = std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20);
+        if (v == COUNT_PENDING && (i & 1023) == 0 && slow) {
             const hipError_t e = hipStreamQuery(stream);
             if (e == hipSuccess) {
                 v = *w;
@@ -2266,7 +2405,11 @@ static int bin_and_blend(dgs_raster_ctx *c, int cap, int P, int device, hipStrea
         c->cfin = cfin;
         todo = (uint32_t *)c->segq.p + 4;
     }
-    {
+    if (!ckpt && blend_fwd2()) {
+        ScopedTimer tm("blend_fwd", stream);
+        hipLaunchKernelGGL(k_blend_fwd2, dim3(T), dim3(B2), 0, stream, c->ranges, c->vals, (uint32_t)cap, c->W, c->H, c->gx,
+                           c->xy, c->conic_o, c->rgbd, c->s.bg, c->final_T, c->n_contrib, out_color, out_depth);
+    } else {
         ScopedTimer tm("blend_fwd", stream);
         hipLaunchKernelGGL(ckpt ? k_blend_fwd<true> : k_blend_fwd<false>, dim3(T), dim3(TILE_PIX), 0, stream, c->ranges, c->vals, (uint32_t)cap, c->W, c->H, c->gx, c->xy,
                            c->conic_o, c->rgbd, c->s.bg, c->final_T, c->n_contrib, out_color, out_depth, ckpt, todo,
@@ -2704,6 +2847,8 @@ extern "C" int dgs_debug_pair_cap(int device) { return pair_cap_get(device); }
 extern "C" void dgs_debug_set_blend_seg(int on) { g_blend_seg.store(on ? 1 : 0); }
 extern "C" void dgs_raster_set_deterministic(int on) { g_det.store(on ? 1 : 0); }
 extern "C" void dgs_debug_set_tile_sort(int on) { g_tile_sort.store(on ? 1 : 0); }
+extern "C" void dgs_debug_set_blend_fwd2(int on) { g_fwd2.store(on ? 1 : 0); }
+extern "C" int dgs_debug_get_blend_fwd2(void) { return blend_fwd2() ? 1 : 0; }
 extern "C" int dgs_debug_get_tile_sort(void) { return tile_sort_enabled() ? 1 : 0; }
 extern "C" int dgs_raster_get_deterministic(void) { return blend_deterministic() ? 1 : 0; }
 extern "C" int dgs_debug_get_blend_seg(void) { return blend_segmented() ? 1 : 0; }

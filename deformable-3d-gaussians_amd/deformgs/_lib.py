@@ -66,6 +66,8 @@ _SIGS = {
     "dgs_raster_get_deterministic": ([], I),
     "dgs_debug_set_tile_sort": ([I], None),
     "dgs_debug_get_tile_sort": ([], I),
+    "dgs_debug_set_blend_fwd2": ([I], None),
+    "dgs_debug_get_blend_fwd2": ([], I),
     "dgs_debug_get_blend_seg": ([], I),
     "dgs_mlp_set_reserved_cus": ([I], None),
     "dgs_mlp_reserved_cus": ([], I),

@@ -153,6 +153,11 @@ int dgs_raster_get_deterministic(void);
  * issued after the call. */
 void dgs_debug_set_tile_sort(int on);
 int dgs_debug_get_tile_sort(void);
+/* Forward blend with two pixels per lane (k_blend_fwd2; DGS_BLEND_FWD2=1): 1 = on. Images, transmittance and
+ * per-pixel contributor counts are bitwise those of the default k_blend_fwd. Applies to forwards issued
+ * after the call (not with the segmented backward's checkpoints). */
+void dgs_debug_set_blend_fwd2(int on);
+int dgs_debug_get_blend_fwd2(void);
 /* host nanoseconds spent waiting for num_rendered (and the number of waits) since process start */
 long long dgs_debug_count_wait_ns(long long *waits);
 /* dL/dscales convention. 0 (default) = the upstream CUDA op's: the gradient w.r.t. the modified scale

@@ -531,3 +531,32 @@ def test_tile_sort_matches_global_depth_sort(case):
         _check(o, g, color, radii, depth, grads,
                [("means3D", "means3D"), ("opacities", "opacities"), ("means2D", "means2D")],
                nr=nr, tag=f"raster_tile_sort[{N}x{H}x{W}]")
+
+
+@pytest.mark.parametrize("case", [
+    (5000, 256, 256, 0, 0.0), (2000, 61, 83, 3, 1.0), (100_000, 800, 800, 0, 0.0)])
+def test_two_pixel_forward_blend_is_bitwise_equal(case):
+    """k_blend_fwd2 (two pixels per lane, dgs_debug_set_blend_fwd2(1)) vs k_blend_fwd: image, depth and
+    radii bitwise equal, and — with the deterministic backward, so the gradients are fixed-order sums —
+    every gradient bitwise equal (the backward replays from the forward's transmittance and contributor
+    counts, so this pins those too)."""
+    from deformgs import _lib
+    from deformgs.renderer import set_deterministic
+    lib = _lib.load()
+    N, H, W, ci, boost = case
+    inputs, rs, _ = scene(N, H, W, cam_index=ci, scale_boost=boost, seed=23)
+    rng = np.random.default_rng(13)
+    dcolor = rng.standard_normal((3, H, W)).astype(np.float32)
+    res = {}
+    before, det0 = lib.dgs_debug_get_blend_fwd2(), set_deterministic(True)
+    try:
+        for f2 in (0, 1):
+            lib.dgs_debug_set_blend_fwd2(f2)
+            res[f2] = _run_gpu(inputs, rs, dcolor, None)
+    finally:
+        lib.dgs_debug_set_blend_fwd2(before)
+        set_deterministic(det0)
+    for a, b in zip(res[1][:3], res[0][:3]):
+        np.testing.assert_array_equal(a, b)
+    for k in res[0][3]:
+        np.testing.assert_array_equal(res[1][3][k], res[0][3][k], err_msg=k)
