@@ -622,20 +622,23 @@ __device__ __forceinline__ int ts_block_radix(TileSortLds &L, const uint32_t *id
         for (int r = 0; r < NI; r++) {
             const bool ok = base + 64 * r + lane < m;
             const uint32_t d = (key[r] >> shift) & 255u;
-            uint64_t mk = __ballot(ok);
+            // lanes holding the same digit: the ones where no digit bit differs from this lane's
+            // (mismatch bits OR-ed per 32-lane half: one 3-input bit op per half and bit)
+            const uint64_t okm = __ballot(ok);
+            uint32_t xlo = ~(uint32_t)okm, xhi = ~(uint32_t)(okm >> 32);
 #pragma unroll
             for (int bb = 0; bb < 8; bb++) {
-                const bool bit = (d >> bb) & 1u;
-                const uint64_t bal = __ballot(bit);
-                mk &= bit ? bal : ~bal;
+                const uint64_t bal = __ballot((d >> bb) & 1u);
+                const uint32_t t = (uint32_t)((int32_t)(d << (31 - bb)) >> 31);  // the bit, sign-extended
+                xlo |= (uint32_t)bal ^ t;
+                xhi |= (uint32_t)(bal >> 32) ^ t;
             }
+            const uint64_t mk = ~(((uint64_t)xhi << 32) | xlo);
             const int leader = mk ? __ffsll((unsigned long long)mk) - 1 : 0;
-            uint32_t b0 = 0;
-            if (ok && lane == leader) {
-                b0 = L.cnt[w][d];
-                L.cnt[w][d] = b0 + (uint32_t)__popcll(mk);
-            }
-            b0 = (uint32_t)__shfl((int)b0, leader);
+            // every lane of a digit group reads the group's count before its leader advances it (the
+            // wave's LDS operations complete in order): no broadcast from the leader needed
+            const uint32_t b0 = ok ? L.cnt[w][d] : 0u;
+            if (ok && lane == leader) L.cnt[w][d] = b0 + (uint32_t)__popcll(mk);
             rank[r] = b0 + (uint32_t)__popcll(mk & lanes_lt);
         }
         __syncthreads();
