@@ -560,3 +560,58 @@ def test_two_pixel_forward_blend_is_bitwise_equal(case):
         np.testing.assert_array_equal(a, b)
     for k in res[0][3]:
         np.testing.assert_array_equal(res[1][3][k], res[0][3][k], err_msg=k)
+
+
+def test_deterministic_mode_under_overflow_and_both_binnings(binning):
+    """The deterministic backward through the training step's deferred pair count: without overflow the
+    deferred step's gradients equal the synchronous step's BITWISE (rect binning; the sort binning keeps
+    the float atomics and is held to the atomics' tolerance); a forced overflow (speculative capacity
+    777) runs its clipped backward in bounds and is detected; the synchronous redo equals the reference
+    (bitwise with rect binning)."""
+    from deformgs import _lib
+    from deformgs.arguments import OptimizationParams, PipelineParams
+    from deformgs.deform_model import DeformModelBaseline
+    from deformgs.gaussian_model import GaussianModel
+    from deformgs.renderer import set_deterministic
+    from deformgs.synthetic import synth_camera, synth_gaussians
+    from deformgs.train_step import deferred_overflowed, drop_grads, forward_backward
+    lib = _lib.load()
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    g = synth_gaussians(6000, seed=1, device=dev)
+    gs = GaussianModel(3)
+    gs.from_tensors(g["xyz"], g["features_dc"], g["features_rest"], g["scaling"], g["rotation"], g["opacity"])
+    gs.training_setup(OptimizationParams())
+    deform = DeformModelBaseline(is_blender=True, is_6dof=False, device=dev)
+    deform.train_setting(OptimizationParams())
+    cam = synth_camera(160, 128, index=3, fid=0.6, device=dev)
+    gt = torch.rand((3, 128, 160), device=dev)
+    params = [gs._xyz, gs._features_dc, gs._features_rest, gs._scaling, gs._rotation, gs._opacity] + \
+        list(deform.deform.parameters())
+
+    def run(deferred):
+        drop_grads(gs, deform)
+        loss, pkg = forward_backward(gs, deform, cam, gt, PipelineParams(), torch.zeros(3, device=dev),
+                                     deferred_count=deferred)
+        torch.cuda.synchronize()
+        return loss.item(), pkg["render"].detach().clone(), [p.grad.clone() for p in params]
+
+    def same(a, b):
+        assert a[0] == b[0] and torch.equal(a[1], b[1])
+        for x, y in zip(a[2], b[2]):
+            if binning == "rect":
+                assert torch.equal(x, y)
+            else:
+                torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-6 * max(1.0, y.abs().max().item()))
+
+    before = set_deterministic(True)
+    try:
+        ref = run(False)
+        same(run(True), ref)
+        assert not deferred_overflowed()
+        lib.dgs_debug_set_pair_cap(dev.index, 777)
+        run(True)
+        assert deferred_overflowed()
+        same(run(False), ref)
+    finally:
+        set_deterministic(before)
