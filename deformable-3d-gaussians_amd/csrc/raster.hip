@@ -495,32 +495,47 @@ __global__ __launch_bounds__(256) void k_rect_place(int P, const uint32_t *__res
 }
 
 // Deterministic blend backward (dgs_raster_set_deterministic): k_blend_bwd2<DEPTH, true> leaves every
-// pair of the replayed lists two 12-float slots (one per wave of its tile: the wave's reduced sums in the
-// accumulator row's field order, zeros for a pair the wave skipped or the tile culled) instead of
-// adding them into acc with float atomics. This gather walks the same rectangles as k_rect_place, one
-// thread per depth-ordered Gaussian, and sums its pairs' slots in tile row-major order, wave 0 before
-// wave 1: a fixed order, so acc (and every gradient after it) is bitwise reproducible. A pair past the
-// launched capacity or past its tile's replayed prefix (todo) was not replayed and adds nothing,
-// exactly as with the atomics. Every row of acc is written (zeros for a Gaussian without a rectangle).
+// pair of the replayed lists one 12-float slot (the pair's reduced sums in the accumulator row's field
+// order, zeros for a pair the tile culled or both waves skipped) instead of adding them into acc with
+// float atomics. This gather walks the same rectangles as k_rect_place (in its order: Gaussian index
+// with the per-tile sort, whose position map takes each walked pair to its sorted list position; depth
+// order without it), one thread per Gaussian, and sums its pairs' slots in tile row-major order: a fixed
+// order, so acc (and every gradient after it) is bitwise reproducible. A pair past the launched
+// capacity is skipped; one past its tile's replayed prefix holds zeros: neither adds anything, exactly
+// as with the atomics. Every row of acc is written (zeros for a Gaussian without a rectangle).
 __global__ __launch_bounds__(256) void k_rect_gather(int P, const uint32_t *__restrict__ order, const float2 *__restrict__ xy,
                                                      const int *__restrict__ radii, int gx, int gy,
                                                      const uint32_t *__restrict__ cnt, const uint32_t *__restrict__ tile_start,
-                                                     const uint2 *__restrict__ ranges, const uint32_t *__restrict__ tile_todo,
                                                      uint32_t cap, const float4 *__restrict__ slot, float *__restrict__ acc,
                                                      int stage) {
     extern __shared__ uint32_t lds[];
-    float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0, s2 = s0;
-    rect_walk(P, order, xy, radii, gx, gy, cnt, tile_start, stage, lds, [&](uint32_t, int t, uint32_t pos) {
-        if (pos >= cap || pos - min(ranges[t].x, cap) >= tile_todo[t]) return;
-        const float4 *q = slot + 6ull * pos;
-        const float4 a0 = q[0], a1 = q[1], a2 = q[2], b0 = q[3], b1 = q[4], b2 = q[5];
-        s0 = s0 + (a0 + b0);
-        s1 = s1 + (a1 + b1);
-        s2 = s2 + (a2 + b2);
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 s0 = z4, s1 = z4, s2 = z4;
+    // one pair behind: a pair's slot loads are added at the next pair, so their latency overlaps the
+    // walk to the next pair (same order of additions)
+    float4 pa = z4, pb = z4, pc = z4;
+    rect_walk(P, order, xy, radii, gx, gy, cnt, tile_start, stage, lds, [&](uint32_t, int, uint32_t pos) {
+        float4 na = z4, nb = z4, nc = z4;
+        if (pos < cap) {
+            const float4 *q = slot + 3ull * pos;
+            na = q[0];
+            nb = q[1];
+            nc = q[2];
+        }
+        s0 = s0 + pa;
+        s1 = s1 + pb;
+        s2 = s2 + pc;
+        pa = na;
+        pb = nb;
+        pc = nc;
     });
+    s0 = s0 + pa;
+    s1 = s1 + pb;
+    s2 = s2 + pc;
     const int j = blockIdx.x * 256 + threadIdx.x;
     if (j >= P) return;
-    float4 *dst = reinterpret_cast<float4 *>(acc + (size_t)order[j] * ACC_STRIDE);
+    // (order == nullptr: the index-order walk of the per-tile sort's placement)
+    float4 *dst = reinterpret_cast<float4 *>(acc + (size_t)(order ? order[j] : (uint32_t)j) * ACC_STRIDE);
     dst[0] = s0;
     dst[1] = s1;
     dst[2] = s2;
@@ -549,17 +564,24 @@ struct TileSortLds {
         unsigned long long run[TS_MAX];  // a long list's merge: one sorted run staged
     } u;
     uint32_t cnt[4][256];  // per-wave digit counts -> per-wave output offsets
+    uint16_t opos[TS_MAX];  // POS: each sorted entry's position in the index-ordered list
     uint32_t misc[8];
 };
 
 // sorts the m <= TS_MAX entries ids[0, m) (index order) stably by dkey[id]; returns the number of passes
 // run (0: the order is unchanged) with the sorted (key, id) pairs in L.u.kv
-template <int NI>
+// POS (the deterministic backward): L.opos carries each entry's position in the input list along
+template <int NI, bool POS>
 __device__ __forceinline__ int ts_block_radix(TileSortLds &L, const uint32_t *ids, int m, const uint32_t *__restrict__ dkey,
                                               int tid) {
     const int lane = tid & 63, w = tid >> 6, base = w * 64 * NI;
     const uint64_t lanes_lt = (1ull << lane) - 1ull;
     uint32_t key[NI], val[NI];
+    [[maybe_unused]] uint32_t opos[NI];
+    if constexpr (POS) {
+#pragma unroll
+        for (int r = 0; r < NI; r++) opos[r] = (uint32_t)(base + 64 * r + lane);
+    }
     uint32_t kor = 0u, kand = ~0u;
 #pragma unroll
     for (int r = 0; r < NI; r++) {
@@ -675,6 +697,7 @@ __device__ __forceinline__ int ts_block_radix(TileSortLds &L, const uint32_t *id
                 const uint32_t dst = L.cnt[w][(key[r] >> shift) & 255u] + rank[r];
                 L.u.kv.key[dst] = key[r];
                 L.u.kv.val[dst] = val[r];
+                if constexpr (POS) L.opos[dst] = (uint16_t)opos[r];
             }
         }
         __syncthreads();
@@ -684,38 +707,56 @@ __device__ __forceinline__ int ts_block_radix(TileSortLds &L, const uint32_t *id
             if (i < m) {
                 key[r] = L.u.kv.key[i];
                 val[r] = L.u.kv.val[i];
+                if constexpr (POS) opos[r] = L.opos[i];
             }
         }
     }
     return passes;
 }
+template <bool POS = false>
 __device__ __forceinline__ int ts_block_any(TileSortLds &L, const uint32_t *ids, int m, const uint32_t *__restrict__ dkey,
                                             int tid) {
-    if (m <= 256) return ts_block_radix<1>(L, ids, m, dkey, tid);
-    if (m <= 512) return ts_block_radix<2>(L, ids, m, dkey, tid);
-    return ts_block_radix<4>(L, ids, m, dkey, tid);
+    if (m <= 256) return ts_block_radix<1, POS>(L, ids, m, dkey, tid);
+    if (m <= 512) return ts_block_radix<2, POS>(L, ids, m, dkey, tid);
+    return ts_block_radix<4, POS>(L, ids, m, dkey, tid);
 }
 
+// pre (the deterministic backward, or nullptr): pre[a + p] = the position q, in the index-ordered list
+// k_rect_place wrote, of the entry the sort put at position p (the backward leaves the pair's sums at
+// a + q, where k_rect_gather's index-order walk finds them); vorig: scratch for the long-list path's
+// copy of that list
+template <bool PRE>
 __global__ __launch_bounds__(TS_THR) void k_tile_sort(const uint2 *__restrict__ ranges, uint32_t cap,
                                                       const uint32_t *__restrict__ dkey, uint32_t *__restrict__ vals,
                                                       unsigned long long *__restrict__ scratch,
-                                                      uint32_t *__restrict__ spos) {
+                                                      uint32_t *__restrict__ spos, uint32_t *__restrict__ pre,
+                                                      uint32_t *__restrict__ vorig) {
     __shared__ TileSortLds L;
     const int tid = threadIdx.x;
     const uint2 rg = ranges[blockIdx.x];
     const uint32_t a = min(rg.x, cap), b = min(rg.y, cap);
     const int len = (int)(b - a);
+    if (PRE && len == 1 && tid == 0) pre[a] = 0u;
     if (len <= 1) return;
     uint32_t *v = vals + a;
     if (len <= TS_MAX) {
         // every entry is read (into registers) before the first barrier; written back after the sort
-        if (ts_block_any(L, v, len, dkey, tid) == 0) return;
-        for (int i = tid; i < len; i += TS_THR) v[i] = L.u.kv.val[i];
+        if (ts_block_any<PRE>(L, v, len, dkey, tid) == 0) {
+            if constexpr (PRE)
+                for (int i = tid; i < len; i += TS_THR) pre[a + i] = (uint32_t)i;
+            return;
+        }
+        for (int i = tid; i < len; i += TS_THR) {
+            v[i] = L.u.kv.val[i];
+            if constexpr (PRE) pre[a + i] = L.opos[i];
+        }
         return;
     }
     // a long list: TS_MAX-long runs sorted into scratch as (depth << 32 | index), then merged by rank
     unsigned long long *sc = scratch + a;
     uint32_t *ps = spos + a;
+    if constexpr (PRE)  // the index-ordered list, kept for the positions (the list is overwritten below)
+        for (int i = tid; i < len; i += TS_THR) vorig[a + i] = v[i];
     for (int c0 = 0; c0 < len; c0 += TS_MAX) {
         const int m = min(TS_MAX, len - c0);
         __syncthreads();  // L is reused
@@ -750,7 +791,19 @@ __global__ __launch_bounds__(TS_THR) void k_tile_sort(const uint2 *__restrict__ 
         }
     }
     // every list entry was read in the run phase: the list is overwritten in place
-    for (int i = tid; i < len; i += TS_THR) v[ps[i]] = (uint32_t)__hip_atomic_load(sc + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int i = tid; i < len; i += TS_THR) {
+        const uint32_t g = (uint32_t)__hip_atomic_load(sc + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v[ps[i]] = g;
+        if constexpr (PRE) {  // g's position in the index-ordered (ascending id) list
+            int lo = 0, hi = len;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (__hip_atomic_load(vorig + a + mid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < g) lo = mid + 1;
+                else hi = mid;
+            }
+            pre[a + ps[i]] = (uint32_t)lo;
+        }
+    }
 }
 
 // L (the pair count) is read on the device and clipped to the launched capacity: an overflowing
@@ -1315,9 +1368,13 @@ __global__ __launch_bounds__(B2) void k_blend_fwd2(const uint2 *__restrict__ ran
 #define BWD2_OCC
 // DEPTH: the depth output has a gradient (dL_ddepth != nullptr); without one (every training step: the
 // loss reads only the image) the depth terms, the depth colour-behind state and its loads drop out.
-// DET: the deterministic mode (k_rect_gather): each wave writes its reduced sums for list position p
-// to slot[2 p + wave] (12 floats, zeros when it skips the Gaussian; the staging thread zeros both slots
-// of a culled one) and the tile's replayed length to tile_todo, instead of adding into acc
+// DET: the deterministic mode (k_rect_gather): the two waves' reduced sums for a staged Gaussian meet in
+// an LDS row (each field gets at most one add per wave onto zero: a + b either way round), written out
+// after the batch to the pair's slot (12 floats; the staging thread writes zeros for a culled entry), and
+// the tile's replayed length to tile_todo, instead of adding into acc; the pairs past the replayed
+// prefix get zeros. A pair's slot is its list position when the lists were placed in depth order, else
+// (the per-tile sort) the position k_rect_place gave it in index order (tile start + pre[position]):
+// where k_rect_gather's walk, in k_rect_place's order, finds it
 template <bool DEPTH, bool DET>
 __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restrict__ ranges, const uint32_t *__restrict__ vals,
                                                    uint32_t cap, int W, int H, int gx, const float *bg,
@@ -1326,13 +1383,14 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
                                                    const uint32_t *__restrict__ n_contrib,
                                                    const float *__restrict__ dL_dpix, const float *__restrict__ dL_ddepth,
                                                    float *__restrict__ acc, float *__restrict__ slot,
-                                                   uint32_t *__restrict__ tile_todo) {
+                                                   uint32_t *__restrict__ tile_todo, const uint32_t *__restrict__ pre) {
     __shared__ float4 s_q[B2];   // staged conic in exponent form + opacity
     __shared__ float4 s_xyc[B2]; // mean2D x, y, list position (bits), Gaussian id (bits)
     __shared__ float4 s_co[B2];
     __shared__ float4 s_cd[B2];
     __shared__ uint32_t s_wcnt[B2 / 64];
     __shared__ uint32_t s_maxlast;
+    __shared__ float4 s_slot[DET ? 3 * B2 : 1];  // DET: per staged Gaussian, its 12 gradient sums
     const int tile = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1370,6 +1428,17 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
     __syncthreads();
     const int todo_total = (int)s_maxlast;  // Gaussians past every pixel's last contributor are skipped
     if (DET && tid == 0) tile_todo[tile] = (uint32_t)todo_total;
+    // DET: a pair's slot (pre: the per-tile sort's map back to the walk's index-order position)
+    [[maybe_unused]] auto slot_of = [&](uint32_t lp) { return reinterpret_cast<float4 *>(slot + 12ull * (pre ? range.x + pre[lp] : lp)); };
+    if constexpr (DET) {  // the pairs past the replayed prefix add nothing: zeros (the gather reads every pair)
+        const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (uint32_t lp = range.x + (uint32_t)todo_total + tid; lp < range.y; lp += B2) {
+            float4 *z = slot_of(lp);
+            z[0] = z4;
+            z[1] = z4;
+            z[2] = z4;
+        }
+    }
     const float b0 = bg[0], b1 = bg[1], b2 = bg[2];
     const f2 kbg = -Tfinal * (b0 * dp0 + b1 * dp1 + b2 * dp2);  // dL/dalpha's background term / (1 - alpha)
     const float hx = 0.5f * W, hy = 0.5f * H;
@@ -1397,11 +1466,18 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
             cl = conic_o[id];
             keep = tile_reach(gl, cl, (float)tx0, (float)ty0);
             if (DET && !keep) {
-                float4 *z = reinterpret_cast<float4 *>(slot + 24ull * (end - prog - 1));
+                float4 *z = slot_of((uint32_t)(end - prog - 1));
                 const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-                for (int i = 0; i < 6; i++) z[i] = z4;
+                z[0] = z4;
+                z[1] = z4;
+                z[2] = z4;
             }
+        }
+        if constexpr (DET) {  // this round's rows (the previous round's were written out before the barrier)
+            const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            s_slot[3 * tid] = z4;
+            s_slot[3 * tid + 1] = z4;
+            s_slot[3 * tid + 2] = z4;
         }
         const int2 sl = compact_slot_n<B2 / 64>(keep, tid, s_wcnt);
         if (keep) {
@@ -1435,10 +1511,7 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
             // compare is its lane mask; of a combined predicate the compiler materialises it first)
             const float ga0 = (contributor < last0 && power.x <= 0.f) ? alpha.x : 0.f;
             const float ga1 = (contributor < last1 && power.y <= 0.f) ? alpha.y : 0.f;
-            if (__ballot(fmaxf(ga0, ga1) >= 1.f / 255.f) == 0ull) {  // wave-uniform
-                if (DET && lane < 12) slot[12ull * (2 * ((uint32_t)range.x + contributor) + wv) + lane] = 0.f;
-                return;
-            }
+            if (__ballot(fmaxf(ga0, ga1) >= 1.f / 255.f) == 0ull) return;  // wave-uniform
             const bool act0 = ga0 >= 1.f / 255.f, act1 = ga1 >= 1.f / 255.f;
             const float4 cd = s_cd[j];
             const float4 co = s_co[j];
@@ -1481,10 +1554,10 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
                 const int row = lane >> 4;
                 const int fo = ((row & 1) << 1) + (row >> 1);
                 if constexpr (DET) {
-                    float *dst = slot + 12ull * (2 * ((uint32_t)range.x + contributor) + wv) + fo;
-                    dst[0] = w0 * sc0;
-                    dst[4] = w1 * sc1;
-                    dst[8] = w2 * sc2;
+                    float *dst = reinterpret_cast<float *>(s_slot + 3 * j) + fo;
+                    atomicAdd(dst, w0 * sc0);
+                    atomicAdd(dst + 4, w1 * sc1);
+                    atomicAdd(dst + 8, w2 * sc2);
                 } else {
                     float *dst = acc + (size_t)__float_as_uint(xc.w) * ACC_STRIDE + fo;
                     atomicAdd(dst, w0 * sc0);
@@ -1505,6 +1578,15 @@ __global__ __launch_bounds__(B2) BWD2_OCC void k_blend_bwd2(const uint2 *__restr
             gauss(j + 1, xb, qb);
         }
         if (j < n) gauss(j, xa, qa);
+        if constexpr (DET) {
+            __syncthreads();  // both waves' adds are in
+            if (tid < n) {
+                float4 *dst = slot_of((uint32_t)range.x + __float_as_uint(s_xyc[tid].z));
+                dst[0] = s_slot[3 * tid];
+                dst[1] = s_slot[3 * tid + 1];
+                dst[2] = s_slot[3 * tid + 2];
+            }
+        }
     }
 }
 
@@ -2024,6 +2106,8 @@ struct dgs_raster_ctx {
     uint32_t *vals = nullptr;
     bool rect_mode = false;  // rect binning (k_rect_*) instead of duplicate + tile sort
     bool tsort = false;      // rect binning in index order + per-tile depth sort (k_tile_sort), no global depth sort
+    bool det_fwd = false;    // deterministic mode at the forward: the det buffer holds the tile sort's position map
+    int det_cap = 0;         // the pair capacity the det buffer was laid out for
     uint32_t *rect_cnt = nullptr, *rect_start = nullptr, *rect_total = nullptr;
     unsigned long long *rect_tot = nullptr;  // tile totals tagged with a launch generation (k_rect_colscan)
     uint2 *ranges = nullptr;
@@ -2365,13 +2449,28 @@ static int bin_tiles(dgs_raster_ctx *c, int cap, int P, int device, hipStream_t 
     return DGS_OK;
 }
 
+// The deterministic mode's buffer for a pair capacity: [tile end (T, padded) | per-pair slots (12 floats)
+// | the tile sort's position map (1 word per pair)], laid out for the capacity the forward binned with
+static int det_layout(dgs_raster_ctx *c, int cap, uint32_t **tile_end, float **slot, uint32_t **pre) {
+    const size_t T = (size_t)c->gx * c->gy, tpad = (T + 63) & ~(size_t)63, n = (size_t)std::max(cap, 1);
+    if (int rc = c->det.ensure(4ull * tpad + 52ull * n)) return rc;
+    c->det_cap = cap;
+    uint32_t *te = (uint32_t *)c->det.p;
+    float *sl = (float *)(te + tpad);
+    if (tile_end) *tile_end = te;
+    if (slot) *slot = sl;
+    if (pre) *pre = (uint32_t *)(sl + 12 * n);
+    return DGS_OK;
+}
+
 static int bin_and_blend(dgs_raster_ctx *c, int cap, int P, int device, hipStream_t stream, bool dbg, float *out_color,
                          float *out_depth) {
     const int T = c->gx * c->gy;
     if (c->rect_mode) {
-        // tile sort: the lists, then 8 + 4 bytes of scratch per pair for lists longer than k_tile_sort's LDS
+        // tile sort: the lists, then 8 + 4 (+ 4: the deterministic mode's copy) bytes of scratch per pair for
+    // lists longer than k_tile_sort's LDS
         const size_t vbytes = align_up(4ull * std::max(cap, 1) + 256);
-        if (int rc = c->bin.ensure(vbytes + (c->tsort ? 12ull * std::max(cap, 1) + 256 : 0))) return rc;
+        if (int rc = c->bin.ensure(vbytes + (c->tsort ? 16ull * std::max(cap, 1) + 256 : 0))) return rc;
         c->vals = (uint32_t *)c->bin.p;
         const int nb = div_up(P, 256);
         if (cap > 0) {
@@ -2385,8 +2484,16 @@ static int bin_and_blend(dgs_raster_ctx *c, int cap, int P, int device, hipStrea
         if (cap > 0 && c->tsort) {
             ScopedTimer tm("tile_sort", stream);
             unsigned long long *scr = (unsigned long long *)((char *)c->bin.p + vbytes);
-            hipLaunchKernelGGL(k_tile_sort, dim3(T), dim3(TS_THR), 0, stream, c->ranges, (uint32_t)cap, c->dkey, c->vals, scr,
-                               (uint32_t *)(scr + std::max(cap, 1)));
+            uint32_t *spos = (uint32_t *)(scr + std::max(cap, 1)), *vorig = spos + std::max(cap, 1);
+            if (c->det_fwd) {
+                uint32_t *pre = nullptr;
+                if (int rc = det_layout(c, cap, nullptr, nullptr, &pre)) return rc;
+                hipLaunchKernelGGL(k_tile_sort<true>, dim3(T), dim3(TS_THR), 0, stream, c->ranges, (uint32_t)cap, c->dkey,
+                                   c->vals, scr, spos, pre, vorig);
+            } else {
+                hipLaunchKernelGGL(k_tile_sort<false>, dim3(T), dim3(TS_THR), 0, stream, c->ranges, (uint32_t)cap, c->dkey,
+                                   c->vals, scr, spos, nullptr, nullptr);
+            }
             DGS_LAUNCH_CHECK("k_tile_sort", dbg, stream);
         }
     } else if (cap > 0) {  // k_duplicate clears c->ranges
@@ -2555,9 +2662,8 @@ static int raster_forward(const dgs_raster_settings *s, int P, int M, const floa
         if (c->rtot.cap != tot_cap) DGS_HIP_CHECK(hipMemsetAsync(c->rtot.p, 0, c->rtot.cap, stream));
         c->rect_tot = (unsigned long long *)c->rtot.p;
     }
-    // the deterministic backward's gather re-walks the rectangles in the depth-sorted order the lists
-    // were placed in, so it keeps the global depth sort
-    c->tsort = c->rect_mode && tile_sort_enabled() && !blend_deterministic();
+    c->tsort = c->rect_mode && tile_sort_enabled();
+    c->det_fwd = c->rect_mode && blend_deterministic();
     c->seg_ok = c->rect_mode && blend_segmented();
     if (c->seg_ok) {
         const size_t cap0 = c->segq.cap;
@@ -2704,28 +2810,30 @@ static int raster_backward(dgs_raster_ctx *c, const float *dL_dcolor, const floa
     const int T = c->gx * c->gy;
     float *acc = (float *)c->acc.p;  // [P][12], zeroed by the forward's k_preprocess
     // deterministic mode: k_rect_gather writes every row of acc (no zeroing needed)
-    const bool det = blend_deterministic() && c->rect_mode && !c->tsort && !blend_one_pixel();
+    // deterministic: asked for at this forward too (the tile sort then left the position map)
+    const bool det = blend_deterministic() && c->rect_mode && c->det_fwd && !blend_one_pixel();
     // a second backward through the same forward (retain_graph, or a context kept alive): the blend
     // backward adds into the accumulators, so they are cleared first instead of doubling the gradients
     if (c->bwd_done && !det) DGS_HIP_CHECK(hipMemsetAsync(acc, 0, 4ull * ACC_STRIDE * P, stream));
     c->bwd_done = true;
     if (cap > 0 && det) {
-        const size_t tpad = ((size_t)T + 63) & ~(size_t)63;
-        if (int rc = c->det.ensure(4ull * tpad + 96ull * cap)) return rc;
-        uint32_t *todo = (uint32_t *)c->det.p;
-        float *slot = (float *)(todo + tpad);
+        uint32_t *todo = nullptr, *pre = nullptr;
+        float *slot = nullptr;
+        // with the tile sort, the forward laid the buffer out (its position map is in it)
+        if (int rc = det_layout(c, c->tsort ? c->det_cap : (int)cap, &todo, &slot, &pre)) return rc;
+        if (!c->tsort) pre = nullptr;  // lists placed in depth order: the slot index is the list position
         {
             ScopedTimer tm("blend_bwd", stream);
             hipLaunchKernelGGL((dL_ddepth ? k_blend_bwd2<true, true> : k_blend_bwd2<false, true>), dim3(T), dim3(B2), 0,
                                stream, c->ranges, c->vals, cap, c->W, c->H, c->gx, c->s.bg, c->xy, c->conic_o, c->rgbd,
-                               c->final_T, c->n_contrib, dL_dcolor, dL_ddepth, acc, slot, todo);
+                               c->final_T, c->n_contrib, dL_dcolor, dL_ddepth, acc, slot, todo, pre);
         }
         DGS_LAUNCH_CHECK("k_blend_bwd2<det>", dbg, stream);
         ScopedTimer tm("blend_gather", stream);
         const bool stage = rect_place_stage(c->gx, c->gy);
         hipLaunchKernelGGL(k_rect_gather, dim3(div_up(P, 256)), dim3(256), rect_place_lds(c->gx, c->gy, stage), stream, P,
-                           c->order, c->xy, c->radii, c->gx, c->gy, c->rect_cnt, c->rect_start, c->ranges, todo, cap,
-                           (const float4 *)slot, acc, (int)stage);
+                           c->tsort ? nullptr : c->order, c->xy, c->radii, c->gx, c->gy, c->rect_cnt, c->rect_start,
+                           cap, (const float4 *)slot, acc, (int)stage);
     } else if (cap > 0) {
         ScopedTimer tm("blend_bwd", stream);
         if (blend_one_pixel())
@@ -2742,11 +2850,11 @@ static int raster_backward(dgs_raster_ctx *c, const float *dL_dcolor, const floa
             if (dL_ddepth)
                 hipLaunchKernelGGL((k_blend_bwd2<true, false>), dim3(T), dim3(B2), 0, stream, c->ranges, c->vals, cap, c->W,
                                    c->H, c->gx, c->s.bg, c->xy, c->conic_o, c->rgbd, c->final_T, c->n_contrib, dL_dcolor,
-                                   dL_ddepth, acc, nullptr, nullptr);
+                                   dL_ddepth, acc, nullptr, nullptr, nullptr);
             else
                 hipLaunchKernelGGL((k_blend_bwd2<false, false>), dim3(T), dim3(B2), 0, stream, c->ranges, c->vals, cap, c->W,
                                    c->H, c->gx, c->s.bg, c->xy, c->conic_o, c->rgbd, c->final_T, c->n_contrib, dL_dcolor,
-                                   nullptr, acc, nullptr, nullptr);
+                                   nullptr, acc, nullptr, nullptr, nullptr);
     }
     DGS_LAUNCH_CHECK("k_blend_bwd", dbg, stream);
     const float fx = c->W / (2.f * c->s.tanfovx), fy = c->H / (2.f * c->s.tanfovy);
