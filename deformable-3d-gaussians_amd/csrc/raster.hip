@@ -151,6 +151,22 @@ __global__ __launch_bounds__(256) void k_preprocess(
     uint32_t *__restrict__ dkey, uint32_t *__restrict__ gid, float4 *__restrict__ acc,
     uint8_t *__restrict__ visible) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = i < P;
+    // every per-Gaussian input is in flight with the SH rows (one HBM round trip per block instead of
+    // a chain of them: camera -> mean -> cull -> scale / rotation; the grid is ~1.5 blocks per CU)
+    float3 p = make_float3(0.f, 0.f, 0.f), s = p;
+    float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+    float op = 0.f;
+    if (live) {
+        p = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
+        if (!cov_pre) {
+            s = make_float3(scales[3 * i], scales[3 * i + 1], scales[3 * i + 2]);
+            q = *reinterpret_cast<const float4 *>(rots + 4 * i);
+        }
+        op = opac[i];
+    }
+    Cam cam;
+    load_cam(cam, view, proj, campos);
     [[maybe_unused]] const float *s_row = nullptr;
     if constexpr (STAGE) {
         __shared__ float s_sh[256 * SH_PAD];
@@ -159,18 +175,15 @@ __global__ __launch_bounds__(256) void k_preprocess(
         __syncthreads();
         s_row = s_sh + threadIdx.x * SH_PAD;
     }
-    if (i >= P) return;
+    if (!live) return;
     // zero this Gaussian's backward accumulator row (the blend backward adds into it): no memset
     // launch in the backward
     acc[3 * i] = acc[3 * i + 1] = acc[3 * i + 2] = make_float4(0.f, 0.f, 0.f, 0.f);
-    Cam cam;
-    load_cam(cam, view, proj, campos);
     radii[i] = 0;
     if (visible) visible[i] = 0;  // render()'s visibility_filter (radii > 0), when asked for
     tiles[i] = 0;
     dkey[i] = 0xffffffffu;  // culled: sorts last, emits no pairs
     gid[i] = (uint32_t)i;
-    float3 p = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
     float3 pv = xform43(cam.v, p);
     if (pv.z <= 0.2f) return;
     float c3[6];
@@ -178,8 +191,6 @@ __global__ __launch_bounds__(256) void k_preprocess(
 #pragma unroll
         for (int k = 0; k < 6; k++) c3[k] = cov_pre[6 * i + k];
     } else {
-        float3 s = make_float3(scales[3 * i], scales[3 * i + 1], scales[3 * i + 2]);
-        float4 q = *reinterpret_cast<const float4 *>(rots + 4 * i);
         cov3d(s, mod, q, c3);
     }
     Ewa e;
@@ -239,7 +250,7 @@ __global__ __launch_bounds__(256) void k_preprocess(
     radii[i] = rad;
     if (visible) visible[i] = rad > 0;
     xy[i] = make_float2(px, py);
-    conic_o[i] = make_float4(con.x, con.y, con.z, opac[i]);
+    conic_o[i] = make_float4(con.x, con.y, con.z, op);
     rgbd[i] = make_float4(rgb.x, rgb.y, rgb.z, pv.z);
     tiles[i] = (uint32_t)area;
     clamped[i] = cl;
@@ -1772,6 +1783,34 @@ __device__ inline void dR_dq(float4 q, const float dR[9], float4 &dq) {
     dq.w = 2.f * (-r * dR[1] + x * dR[2] + r * dR[3] + y * dR[5] + x * dR[6] + y * dR[7]) - 4.f * z * (dR[0] + dR[4]);
 }
 
+// one Gaussian's backward inputs, loaded before the block's SH staging so that they and the SH rows
+// share one HBM round trip (the loads otherwise chained: accumulators -> radius -> scale / rotation)
+struct PbIn {
+    float4 a0, a1, a2;  // blend-backward accumulators (mx, my, cx, cy), (cz, op, r, g), (b, depth, dx, dy)
+    float3 p, s;
+    float4 q;
+    int rad;
+    uint8_t cl;
+};
+
+__device__ __forceinline__ void pb_load(PbIn &in, int i, const float *acc, const int *radii, const float *means3D,
+                                        const float *scales, const float *rots, const float *cov_pre,
+                                        const uint8_t *clamped) {
+    const float *a = acc + (size_t)i * ACC_STRIDE;
+    in.a0 = *reinterpret_cast<const float4 *>(a);
+    in.a1 = *reinterpret_cast<const float4 *>(a + 4);
+    in.a2 = *reinterpret_cast<const float4 *>(a + 8);
+    in.rad = radii[i];
+    in.p = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
+    in.s = make_float3(0.f, 0.f, 0.f);
+    in.q = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (!cov_pre) {
+        in.s = make_float3(scales[3 * i], scales[3 * i + 1], scales[3 * i + 2]);
+        in.q = *reinterpret_cast<const float4 *>(rots + 4 * i);
+    }
+    in.cl = clamped ? clamped[i] : (uint8_t)0;
+}
+
 // STAGE (degree-3 SH rows, M = 16, 16-byte aligned tensors): the block's SH rows (contiguous in
 // HBM) are read into LDS with coalesced 16-byte loads, and its SH gradient rows are written back the
 // same way (one thread per Gaussian would otherwise store 48 scattered words per row: 3x the HBM
@@ -1785,7 +1824,7 @@ __device__ __forceinline__ void preprocess_bwd_one(
     const float *__restrict__ acc, float *__restrict__ dL_dmeans3D, float *__restrict__ dL_dmeans2D,
     float *__restrict__ dL_ddens, float *__restrict__ dL_dcolors, float *__restrict__ dL_dopac,
     float *__restrict__ dL_dcov3D, float *__restrict__ dL_dshs, float *__restrict__ dL_dscales,
-    float *__restrict__ dL_drots, float *s_row, float dsmul);
+    float *__restrict__ dL_drots, float *s_row, float dsmul, const PbIn &in, const Cam &cam);
 
 template <bool STAGE>
 __global__ __launch_bounds__(256) void k_preprocess_bwd(
@@ -1800,6 +1839,10 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     [[maybe_unused]] const int b0 = blockIdx.x * blockDim.x, nrow = min(256, P - b0);
     [[maybe_unused]] float *s_row = nullptr;
+    PbIn in;
+    if (i < P) pb_load(in, i, acc, radii, means3D, scales, rots, cov_pre, clamped);
+    Cam cam;
+    load_cam(cam, view, proj, campos);
     if constexpr (STAGE) {
         __shared__ float s_sh[256 * SH_PAD];
         s_row = s_sh + threadIdx.x * SH_PAD;
@@ -1807,13 +1850,15 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(
         __syncthreads();
         if (i < P) preprocess_bwd_one<STAGE>(i, D, M, means3D, scales, mod, rots, cov_pre, shs, view, proj, campos, W, H,
                                              tanx, tany, fx, fy, radii, clamped, acc, dL_dmeans3D, dL_dmeans2D, dL_ddens,
-                                             dL_dcolors, dL_dopac, dL_dcov3D, dL_dshs, dL_dscales, dL_drots, s_row, dsmul);
+                                             dL_dcolors, dL_dopac, dL_dcov3D, dL_dshs, dL_dscales, dL_drots, s_row, dsmul,
+                                             in, cam);
         __syncthreads();
         sh_stage_out(s_sh, dL_dshs, dL_dshs_rest, b0, nrow);
     } else {
         if (i < P) preprocess_bwd_one<STAGE>(i, D, M, means3D, scales, mod, rots, cov_pre, shs, view, proj, campos, W, H,
                                              tanx, tany, fx, fy, radii, clamped, acc, dL_dmeans3D, dL_dmeans2D, dL_ddens,
-                                             dL_dcolors, dL_dopac, dL_dcov3D, dL_dshs, dL_dscales, dL_drots, nullptr, dsmul);
+                                             dL_dcolors, dL_dopac, dL_dcov3D, dL_dshs, dL_dscales, dL_drots, nullptr, dsmul,
+                                             in, cam);
     }
 }
 
@@ -1827,11 +1872,8 @@ __device__ __forceinline__ void preprocess_bwd_one(
     const float *__restrict__ acc, float *__restrict__ dL_dmeans3D, float *__restrict__ dL_dmeans2D,
     float *__restrict__ dL_ddens, float *__restrict__ dL_dcolors, float *__restrict__ dL_dopac,
     float *__restrict__ dL_dcov3D, float *__restrict__ dL_dshs, float *__restrict__ dL_dscales,
-    float *__restrict__ dL_drots, float *s_row, float dsmul) {
-    const float *a = acc + (size_t)i * ACC_STRIDE;
-    float4 a0 = *reinterpret_cast<const float4 *>(a);
-    float4 a1 = *reinterpret_cast<const float4 *>(a + 4);
-    float4 a2 = *reinterpret_cast<const float4 *>(a + 8);
+    float *__restrict__ dL_drots, float *s_row, float dsmul, const PbIn &in, const Cam &cam) {
+    const float4 a0 = in.a0, a1 = in.a1, a2 = in.a2;
     // a0 = (mx, my, cx, cy), a1 = (cz, op, r, g), a2 = (b, depth, dx, dy)
     dL_dmeans2D[3 * i] = a0.x;
     dL_dmeans2D[3 * i + 1] = a0.y;
@@ -1845,22 +1887,18 @@ __device__ __forceinline__ void preprocess_bwd_one(
         dL_dcolors[3 * i + 1] = a1.w;
         dL_dcolors[3 * i + 2] = a2.x;
     }
-    const bool vis = radii[i] > 0;
-    float3 p = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
-    Cam cam;
-    load_cam(cam, view, proj, campos);
+    const bool vis = in.rad > 0;
+    const float3 p = in.p;
     float dm0 = 0.f, dm1 = 0.f, dm2 = 0.f;
     float dcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float c3[6];
-    float3 s3 = make_float3(0.f, 0.f, 0.f);
-    float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float3 s3 = in.s;
+    const float4 q = in.q;
     if (vis) {
         if (cov_pre) {
 #pragma unroll
             for (int k = 0; k < 6; k++) c3[k] = cov_pre[6 * i + k];
         } else {
-            s3 = make_float3(scales[3 * i], scales[3 * i + 1], scales[3 * i + 2]);
-            q = *reinterpret_cast<const float4 *>(rots + 4 * i);
             cov3d(s3, mod, q, c3);
         }
         float3 tv = xform43(cam.v, p);
@@ -1934,7 +1972,7 @@ __device__ __forceinline__ void preprocess_bwd_one(
             float vx = p.x - cam.c[0], vy = p.y - cam.c[1], vz = p.z - cam.c[2];
             float n = sqrtf(vx * vx + vy * vy + vz * vz);
             float x = vx / n, y = vy / n, z = vz / n;
-            uint8_t cl = clamped[i];
+            const uint8_t cl = in.cl;
             float g3[3] = {(cl & 1) ? 0.f : a1.z, (cl & 2) ? 0.f : a1.w, (cl & 4) ? 0.f : a2.x};
             float ddx = 0.f, ddy = 0.f, ddz = 0.f;
             float xx = x * x, yy = y * y, zz = z * z, xy_ = x * y, yz = y * z, xz = x * z;
