@@ -277,10 +277,12 @@ def main():
     lib.dgs_timing_reset()
     lib.dgs_timing_select({"roofline": b"mlp_fwd,mlp_bwd,mlp_dw", "major": b"mlp_fwd,mlp_bwd,mlp_dw,blend_fwd,blend_bwd",
                            "all": b"", "none": b""}[args.kernel_timing])
-    # the roofline candidates are timed on every 4th step (each timed launch adds two stream markers, ~6 us
-    # of GPU idle each, inside the timed region); the other classes, when asked for, on every step. The
-    # roofline reports the timed class with the longest average launch (the dominant kernel)
-    lib.dgs_timing_sample(4 if args.kernel_timing == "roofline" and args.steps >= 8 else 1)  # (period below)
+    # the roofline candidates are timed on every 8th step (each timed launch adds two stream markers, ~6 us
+    # of GPU idle each, inside the timed region: 28 us per timed step, profiles/r5y2 trace), every 4th on
+    # shorter runs; the other classes, when asked for, on every step. The roofline reports the timed class
+    # with the longest average launch (the dominant kernel)
+    period = (8 if args.steps >= 16 else 4 if args.steps >= 8 else 1) if args.kernel_timing == "roofline" else 1
+    lib.dgs_timing_sample(period)
     lib.dgs_timing_enable(0 if args.kernel_timing == "none" else 1)
     if world > 1:
         dist.barrier()
@@ -315,7 +317,6 @@ def main():
 
     # per class: accumulated ms over the timed launches, how many were timed, how many ran (the
     # roofline candidates are timed on every `period`-th launch)
-    period = 4 if args.kernel_timing == "roofline" and args.steps >= 8 else 1
     kernels = {}
     for name in KERNEL_CLASSES:
         n_l = _lib.I(0)
