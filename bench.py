@@ -7,8 +7,11 @@ all-reduce when N>1] -> Adam on the Gaussians and the MLP. Workload: synth-100k 
 100k Gaussians, 800x800, blender deformation network (timenet on), SH degree 3, synthetic
 (random-init weights, random target image). Inputs are resident in HBM before timing starts.
 
-Run: python bench.py [--gpus N --steps K --warmup W]; N>1 under torch.distributed.run (one rank per
-GPU, RCCL). Rank 0 prints ONE JSON line (value = whole-job iters/s = world * K / max-rank time).
+Run: python bench.py [--gpus N --steps K --warmup W]. N>1: one rank per GPU over RCCL. Under
+torch.distributed.run (WORLD_SIZE set) each process is one rank; invoked directly with --gpus N > 1 the
+parent makes no GPU call and starts `python -m torch.distributed.run --nproc-per-node N bench.py ...` as
+a child process, waits for it and exits with its return code (launcher_cmd). Rank 0 prints ONE JSON line
+(value = whole-job iters/s = world * K / max-rank time).
 """
 import argparse
 import ctypes
@@ -26,9 +29,10 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense FP32 matrix peak (spec)
-# split-bf16 GEMMs (csrc/mlp_split.hip): an fp32 product costs six bf16 MFMA products, so their fp32
-# roofline is the dense bf16 MFMA peak (~2.5 PF, MI355X_MICROARCH.md) / 6
-SPLIT_MFMA_PEAK_TFLOPS = 2500.0 / 6
+# split-f16 GEMMs (csrc/mlp_split.hip, round 6): an fp32 product costs three f16 MFMA products (hh + hl +
+# lh of a scaled two-piece split), so their fp32 roofline is the dense f16 MFMA peak (~2.5 PF, the bf16
+# rate: MI355X_MICROARCH.md) / 3 (rounds 1-5: the bf16x6 split, / 6)
+SPLIT_MFMA_PEAK_TFLOPS = 2500.0 / 3
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")  # tools/pmc_traffic.py output
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak (spec)
 
@@ -43,7 +47,32 @@ MLP_DX_MAC = 461312             # W^T products whose input gradient is needed (h
 MLP_DW_MAC = 493568             # every trunk + head weight once, t_emb columns from gb (x) te
 
 
-def parse():
+def launcher_cmd(argv, nproc, port):
+    """The child command that runs this bench as `nproc` ranks on one node (no GPU call in the parent):
+    torch.distributed.run on 127.0.0.1 with the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def maybe_launch(args, argv):
+    """--gpus N > 1 without WORLD_SIZE: run the ranks as a child torch.distributed.run (subprocess, not
+    exec: the parent has touched no GPU and simply waits) and return its exit code; else None."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    import subprocess
+    cmd = launcher_cmd(argv, args.gpus, _free_port())
+    print("[bench] launching " + " ".join(cmd), file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -64,7 +93,7 @@ def parse():
     ap.add_argument("--raw-init", action="store_true",
                     help="keep nn.Linear's default init on the deformation heads (the iteration-3000 transient: "
                          "deltas O(0.3) make every Gaussian hundreds of pixels wide)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 SYNC_COUNT = os.environ.get("DGS_BENCH_SYNC_COUNT", "0") == "1"  # A/B: the synchronous pair count
@@ -77,7 +106,7 @@ def mfma_peak(name):
         return FP32_MFMA_PEAK_TFLOPS, "fp32 MFMA (v_mfma_f32_32x32x2_f32)"
     if exact:
         return FP32_MFMA_PEAK_TFLOPS, "fp32 MFMA (v_mfma_f32_32x32x2_f32)"
-    return SPLIT_MFMA_PEAK_TFLOPS, "bf16 MFMA peak / 6 (exact hi/mid/lo split, six products per fp32 product)"
+    return SPLIT_MFMA_PEAK_TFLOPS, "f16 MFMA peak / 3 (scaled hi/lo f16 split, three products per fp32 product)"
 
 
 def kernel_algorithmic(name, N, P, HW, cap=None, T=None):
@@ -197,6 +226,9 @@ def cpu_baseline(N, res, steps, warmup=3):
 
 def main():
     args = parse()
+    rc = maybe_launch(args, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
     from deformgs import _lib
     from deformgs.dist import OverflowAgreement, OverlappedGradAllReduce, init_from_env
     from deformgs.deform_model import DeformModelBaseline
@@ -294,15 +326,29 @@ def main():
     for k in range(args.steps):
         step(k)
     torch.cuda.synchronize()
+    t_local = time.perf_counter() - t0  # this rank's own steps, before waiting for the others
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     wait_ms = (lib.dgs_debug_count_wait_ns(waits) - wait0) / 1e6
     lib.dgs_timing_enable(0)
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    # per rank: its own timed span, the wait for the slowest rank at the closing barrier (imbalance
+    # plus collective waits the stream dependencies pushed to the end), the host's pair-count wait and
+    # forward / backward issue time, and the world size it saw
+    mine = torch.tensor([rank, world, t_local * 1e3 / args.steps, (elapsed - t_local) * 1e3 / args.steps,
+                         wait_ms / args.steps, state["host_fb"] * 1e3 / args.steps, state["redos"]],
+                        dtype=torch.float64, device=dev)
+    per_rank = [mine]
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        per_rank = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(per_rank, mine)
     elapsed = float(el.item())
+    ranks_info = [{"rank": int(v[0]), "world_seen": int(v[1]), "own_ms_per_step": float(v[2]),
+                   "barrier_wait_ms_per_step": float(v[3]), "count_wait_ms_per_step": float(v[4]),
+                   "host_fwd_bwd_ms_per_step": float(v[5]), "redone_steps": int(v[6])}
+                  for v in (t.cpu() for t in per_rank)]
 
     # pair count of one render (for the raster rooflines), measured once outside the timed region
     with torch.no_grad():
@@ -367,8 +413,8 @@ def main():
             "mlp_flop": mlp_flop, "raster_bytes": raster_bytes, "step_ms": step_s * 1e3,
             "frac_split_basis": (mlp_flop / (SPLIT_MFMA_PEAK_TFLOPS * 1e12) + raster_bytes / (HBM_PEAK_GBS * 1e9)) / step_s,
             "frac_fp32_basis": (mlp_flop / (FP32_MFMA_PEAK_TFLOPS * 1e12) + raster_bytes / (HBM_PEAK_GBS * 1e9)) / step_s,
-            "note": "kernel frac is vs the split-bf16 ceiling (2.5 PF bf16 / 6); vs the 157.3 TF fp32 MFMA peak the "
-                    "split kernels can exceed 1 (six bf16 products per fp32 product at 16x the fp32 rate)"}
+            "note": "kernel frac is vs the split-f16 ceiling (2.5 PF f16 / 3); vs the 157.3 TF fp32 MFMA peak the "
+                    "split kernels can exceed 1 (three f16 products per fp32 product at 16x the fp32 rate)"}
     result = {
         "metric": f"train iters/s (deform+raster fwd+bwd), {N // 1000}k Gaussians @ {R}x{R}",
         "value": value, "unit": "iters/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -392,6 +438,8 @@ def main():
         "host_ms_per_step": {"fwd_bwd": state["host_fb"] / args.steps * 1e3, "count_wait": wait_ms / args.steps,
                              "optimizer": state["host_opt"] / args.steps * 1e3},
         "cpu_baseline": None,
+        "dist": {"world_size": world, "backend": dist.get_backend() if world > 1 else None,
+                 "ranks": ranks_info},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:

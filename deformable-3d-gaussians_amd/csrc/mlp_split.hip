@@ -1,37 +1,54 @@
-// Fused deformation MLP (positional encoding + timenet + 8x256 trunk with skip + heads) on bf16 MFMA
-// with an exact three-way operand split: the default path of dgs_deform_* (the fp32-MFMA kernels of
+// Fused deformation MLP (positional encoding + timenet + 8x256 trunk with skip + heads) on f16 MFMA
+// with a scaled two-piece operand split: the default path of dgs_deform_* (the fp32-MFMA kernels of
 // mlp.hip run instead under DGS_MLP_EXACT_FP32).
 //
 // Replaces DeformNetworkBaseline.forward and its autograd backward (utils/time_utils.py:56-127;
 // DeformNetwork :129-201 via DGS_MLP_NO_ROTSCALE; 6-DoF heads :114-121 emitted raw, exp_se3 stays in
 // the host glue).
 //
-// Numerics ("bf16x6"). Every fp32 operand x is split EXACTLY into three bf16 values
-//   hi = bf16(x), mid = bf16(x - hi), lo = x - hi - mid        (round to nearest)
-// (x - hi is exact in fp32 and has at most 16 significant bits, so lo has at most 8: x = hi+mid+lo,
-// |mid| <= 2^-8 |x|, |lo| <= 2^-16 |x|). A product a*b is accumulated as the six bf16 x bf16 products
-// hh + hm + mh + hl + lh + mm, each exact in the fp32 accumulator of the MFMA; the dropped ml + lm +
-// ll are below 2^-23 |ab| (fp32's own rounding of a product is up to 2^-24 |ab|). An MFMA aligns its
-// products and C to the largest term within a limited window (tools/mfma_round_probe.hip), so the
-// five corrections of each k-step go into a fresh accumulator that is added to the running sum in
-// fp32 (tools/mfma_accum_probe.hip: as accurate as the fp32 fma chain). The GEMMs keep fp32 accuracy
-// (tests/test_gpu_mlp.py holds them to the exact-fp32 path's error) at 16/6 = 2.67x the fp32-MFMA
-// rate (MI355X: bf16 MFMA = 16x f32 MFMA per clock). Biases, ReLU, PE and reductions stay fp32.
+// Numerics ("f16x3", round 6; rounds 1-5 ran a three-piece bf16 split with six products per fp32
+// product). Every fp32 operand x is multiplied by a power of two S (exact) that puts its group's
+// magnitude bound into [2^14, 2^15), then split into two f16 values
+//   hi = f16(S x), lo = f16(S x - hi)                           (round to nearest)
+// (S x - hi is exact in fp32; |S x - hi| <= 2^-11 |hi|, so lo carries the next 11 bits: S x = hi + lo
+// to 2^-22 relative; below the f16 normal range the pieces keep 2^-25 absolute, i.e. 2^-39 of the
+// group's bound). A product a*b is accumulated as the three f16 x f16 products hh + hl + lh, each
+// exact in the fp32 accumulator of the MFMA (hl, lh <= 2^-11 |hh|; the dropped ll <= 2^-22 |ab|),
+// hh in the running accumulator and hl + lh in their own (an MFMA aligns its terms and C to the
+// largest within a limited window, tools/mfma_round_probe.hip), added once per GEMM. The scales are
+// undone in fp32 (powers of two: exact) in the epilogue. F16 MFMA forms run at the bf16 rate
+// (MI355X_MICROARCH: 'the F16 forms take the same cycles'), so the GEMMs issue half the MFMAs of the
+// bf16x6 split (16/3 = 5.3x the fp32-MFMA rate), read two operand planes instead of three, and split
+// in 5 VALU per two values instead of 11. Accuracy: tests/test_gpu_mlp.py holds every output and
+// parameter gradient to 2x the exact-fp32 path's error against float64, including the bench step's
+// own near-cancelling upstream gradient at 100k points (test_split_accuracy_bench_regime).
+//   Scales. A (weights): one per (image, 16-row n-tile) over the whole K, from the tile's max |w|
+// (k_pack, written into every k-slot of the tile). B (activations / dZ in LDS): one per layer, the
+// same on every wave without any synchronisation: the writers of layer L's output all evaluate the
+// bound  max_rows sum_k |W_L[row, k]| * max|input of L| + max|b_L|  (>= every output; the row abs
+// sums are per-image statistics k_pack computes, the input maximum is the maximum of the ACTUAL
+// maxima the previous layer's writers published in LDS before their hand-off signal, so the bound is
+// loose by ~sqrt(K) at most, never compounding over layers). Inputs staged from memory (x_emb, t
+// encodings, dOut) and the narrow per-point timenet outputs take their block's actual maximum behind
+// the workgroup barrier their staging already has. A GEMM whose K spans two scale groups (x_emb |
+// h of linear.5, x_emb | t_emb of linear.0) rescales its accumulators once at the boundary.
 //
 // Layout ("transposed" formulation, Y^T = W X^T: features on MFMA rows, points on MFMA columns),
-// v_mfma_f32_16x16x32_bf16:
+// v_mfma_f32_16x16x32_f16:
 //  * One workgroup = 64 points x 16 waves (4 per SIMD); wave r owns output rows 16r..16r+15 of every
-//    256-wide layer for all four 16-point column tiles, so each 3 KiB weight fragment (16 rows x 32
-//    features x 3 splits) fetched from L2 feeds 4 x 6 MFMAs.
-//  * Activations live in LDS split into hi/mid/lo bf16 images of 16-byte units (8 features x 1
-//    point), [8-feature group][split][64 points]: the B operand of a k-step (32 features) is one
-//    ds_read_b128 per split and column tile, and an accumulator's 4 rows are one 8-byte store per
-//    split into the next layer's image. XE | TE | H groups are contiguous, so cat(x_emb, t_emb) and
-//    cat(x_emb, t_emb, h) are plain group ranges (147 KB of LDS: one block per CU).
+//    256-wide layer for all four 16-point column tiles, so each 2 KiB weight fragment (16 rows x 32
+//    features x 2 splits) fetched from L2 feeds 4 x 3 MFMAs. The training forward / dX chain run as
+//    8 waves of two n-tiles (k_fwd8 / k_bwd8).
+//  * Activations live in LDS split into hi/lo f16 images of 16-byte units (8 features x 1 point),
+//    [8-feature group][split][64 points]: the B operand of a k-step (32 features) is one ds_read_b128
+//    per split and column tile, and an accumulator's 4 rows are one 8-byte store per split into the
+//    next layer's image. XE | TE | H groups are contiguous, so cat(x_emb, t_emb) and cat(x_emb, t_emb,
+//    h) are plain group ranges.
 //  * Narrow layers (timenet.2, heads, the t_emb rows of the backward) run as full-K 16x16 tiles on a
 //    subset of the waves: no partial sums.
-//  * Weights are packed every call (they change every optimizer step) by one gather + split launch
-//    into A-fragment images [n-tile][k-step][split][64 lanes][8 bf16].
+//  * Weights are packed every call (they change every optimizer step) by one gather + scale + split
+//    launch into A-fragment images [n-tile][k-step][split][64 lanes][8 f16] (k-slot stride 3 KiB: hi,
+//    lo, and the tile's inverse scale).
 //  * Saved activations / dZ stay fp32 feature-major [rows][Ns] (mlp_shared.h row map; the dW GEMM
 //    reads them), written in each layer's epilogue; relu' masks are one u16 per lane and 16-row
 //    tile ([64-point block][row / 16][64 lanes]). Every reduction has a fixed order: bitwise
@@ -58,16 +75,18 @@ using namespace mlpc;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
 
 constexpr int BM = 64;            // points per workgroup
 constexpr int NQ = 4;             // 16-point column tiles per workgroup
 constexpr int NWAVE = 16;         // one 16-row n-tile of a 256-wide layer per wave
 constexpr int NTHR = NWAVE * 64;
-constexpr int NSPLIT = 3;         // hi, mid, lo
+constexpr int NSPLIT = 2;         // hi, lo
 constexpr int UG = NSPLIT * BM;   // 16-B units per 8-feature group (all splits, all points)
-constexpr int KSLOT = 3 * 64;     // units per (n-tile, k-step) of an A image: 3 splits x 64 lanes
+constexpr int KSLOT = 3 * 64;     // units per (n-tile, k-step) of an A image: hi, lo, inverse scale
 constexpr int KG = 4;             // 8-feature groups per k-step (32 features)
 // forward LDS groups: XE (64 features) | TE (32) | H (256) | TIN (16 + 16 zero: one k-step)
 constexpr int G_XE = 0, G_TE = 8, G_H = 12, G_TIN = 44, G_FWD = 48;
@@ -81,82 +100,141 @@ constexpr int ST_TE = 64, ST_TIN = 96;
 constexpr int MR_TH = M_TH / 16;
 
 static_assert(G_TE == G_XE + 8 && G_H == G_TE + 4, "XE|TE|H must be contiguous");
-static_assert(G_FWD * UG * 16 + (8 * 256 + 16) * 4 + NTHR * 4 + 128 <= 160 * 1024 && G_BWD * UG * 16 <= 160 * 1024,
-              "LDS (k_fwd: + trunk biases, pending relu' bits, hand-off counters)");
+static_assert(G_FWD * UG * 16 + (8 * 256 + 16) * 4 + NTHR * 4 + 512 <= 160 * 1024 && G_BWD * UG * 16 <= 160 * 1024,
+              "LDS (k_fwd: + trunk biases, pending relu' bits, hand-off counters, scales)");
 static_assert(112 * BM * 4 <= 32 * UG * 16, "fp32 staging must fit the H region");
 
 // ------------------------------------------------------------------------------------------------
-// exact three-way split
+// scaled two-piece f16 split
 // ------------------------------------------------------------------------------------------------
+// 2^e as a float (e in [-126, 127])
+__device__ __forceinline__ float pow2f(int e) { return __uint_as_float((uint32_t)(e + 127) << 23); }
+// the power-of-two scale S that brings a bound m >= max |x| into [2^14, 2^15), and 1 / S; exponents
+// clamped to +-60 (a zero or tiny bound keeps S = 2^74, an infinite one 2^-46)
+struct Scale {
+    float s, inv;
+};
+__device__ __forceinline__ Scale scale_for(float m) {
+    int e = (int)((__float_as_uint(m) >> 23) & 255u) - 127;
+    e = min(max(e, -60), 60);
+    return Scale{pow2f(14 - e), pow2f(e - 14)};
+}
+
+// hi = f16(a), lo = f16(a - hi) of two (already scaled) values, pairwise: v_cvt_pk_f16_f32, two
+// f16 -> f32, a packed subtraction, v_cvt_pk_f16_f32 (5 VALU per two values)
+__device__ __forceinline__ void hsplit2(float a, float b, uint32_t &h, uint32_t &l) {
+    const h16x2 hv = __builtin_convertvector((f32x2){a, b}, h16x2);
+    const f32x2 hf = __builtin_convertvector(hv, f32x2);
+    const h16x2 lv = __builtin_convertvector((f32x2){a - hf[0], b - hf[1]}, h16x2);
+    h = __builtin_bit_cast(uint32_t, hv);
+    l = __builtin_bit_cast(uint32_t, lv);
+}
+
 struct Split4 {
-    bf16x4 h, m, l;
+    h16x4 h, l;
 };
 
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
-// RNE of two floats into one packed bf16 pair (one v_cvt_pk_bf16_f32)
-__device__ __forceinline__ uint32_t cvt2(float a, float b) {
-    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
+// four values times the scale S -> their hi / lo halves of a unit
+__device__ inline Split4 split4(float a, float b, float c, float d, float S) {
+    uint32_t h0, l0, h1, l1;
+    hsplit2(a * S, b * S, h0, l0);
+    hsplit2(c * S, d * S, h1, l1);
+    return Split4{__builtin_bit_cast(h16x4, make_uint2(h0, h1)), __builtin_bit_cast(h16x4, make_uint2(l0, l1))};
 }
 
-// the exact split of two values, pairwise: 3 v_cvt_pk_bf16_f32 + 4 unpacks (the bf16 -> f32 of
-// a packed pair is a shift / mask) + 4 subtractions
-__device__ __forceinline__ void split2(float a, float b, uint32_t &h, uint32_t &m, uint32_t &l) {
-    h = cvt2(a, b);
-    const float ra = a - __uint_as_float(h << 16), rb = b - __uint_as_float(h & 0xffff0000u);
-    m = cvt2(ra, rb);
-    l = cvt2(ra - __uint_as_float(m << 16), rb - __uint_as_float(m & 0xffff0000u));
-}
-
-__device__ inline Split4 split4(float a, float b, float c, float d) {
-    uint32_t h0, m0, l0, h1, m1, l1;
-    split2(a, b, h0, m0, l0);
-    split2(c, d, h1, m1, l1);
-    Split4 s;
-    s.h = __builtin_bit_cast(bf16x4, make_uint2(h0, h1));
-    s.m = __builtin_bit_cast(bf16x4, make_uint2(m0, m1));
-    s.l = __builtin_bit_cast(bf16x4, make_uint2(l0, l1));
-    return s;
-}
-
-// 8 consecutive features of one point -> the three 16-B units of group g (LDS image [g][split][BM])
-__device__ inline void put_unit8(bf16x8 *lds, int g, int m, const float (&v)[8]) {
-    const Split4 a = split4(v[0], v[1], v[2], v[3]);
-    const Split4 b = split4(v[4], v[5], v[6], v[7]);
-    bf16x8 *u = lds + g * UG + m;
+// 8 consecutive features of one point -> the two 16-B units of group g (LDS image [g][split][BM])
+__device__ inline void put_unit8(h16x8 *lds, int g, int m, const float (&v)[8], float S) {
+    const Split4 a = split4(v[0], v[1], v[2], v[3], S);
+    const Split4 b = split4(v[4], v[5], v[6], v[7], S);
+    h16x8 *u = lds + g * UG + m;
     u[0] = __builtin_shufflevector(a.h, b.h, 0, 1, 2, 3, 4, 5, 6, 7);
-    u[BM] = __builtin_shufflevector(a.m, b.m, 0, 1, 2, 3, 4, 5, 6, 7);
-    u[2 * BM] = __builtin_shufflevector(a.l, b.l, 0, 1, 2, 3, 4, 5, 6, 7);
+    u[BM] = __builtin_shufflevector(a.l, b.l, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// max over the wave of non-negative floats (as u32: the same order), in every lane: DPP row shifts,
+// the row broadcasts into lane 63, then readlane
+__device__ __forceinline__ float wave_max(float v) {
+    uint32_t x = __float_as_uint(v);
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));
+    return __uint_as_float(__builtin_amdgcn_readlane(x, 63));
+}
+
+// max |v| over this lane's tiles
+template <int NQ_>
+__device__ inline float tiles_absmax(const f32x4 (&v)[NQ_]) {
+    float m = 0.f;
+#pragma unroll
+    for (int q = 0; q < NQ_; q++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) m = fmaxf(m, fabsf(v[q][i]));
+    return m;
+}
+
+// LDS max of non-negative floats (ds_max_u32 on the bits)
+__device__ __forceinline__ void lds_fmax(uint32_t *p, float v) {
+    __hip_atomic_fetch_max(p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Per-block scale state in LDS. Every B-operand scale is per 16-point column tile q (the MFMA's column
+// block), so a point's arithmetic does not depend on which other points share its workgroup (the tail
+// decomposition, block_split, stays bitwise equal to 64-point blocks):
+//  ksc[k][q]: inverse scale of k-step k of the LDS image, column tile q (every writer of a k-step stores
+//             the same value)
+//  amax[par][w][q]: actual max |output| of writer wave w in the layer (chain step) of parity par
+//  ain[i][q]: maxima of the staged inputs: [0] x_emb (forward) / dOut (backward), [1] t_emb
+//  bsync[i][q]: block-wide maxima gathered behind a workgroup barrier (staging, narrow timenet tiles)
+//  bmax[L]: max |bias| of trunk layer L (8: heads), from the launch-constant bias table
+//  wstat[L]: max row abs sum of the layer's A image (k_pack's tile statistics; [8]: heads^T)
+struct ScaleLDS {
+    float ksc[12][4];
+    float amax[2][16][4];
+    float ain[2][4];
+    uint32_t bsync[8][4];
+    uint32_t bmax[10];
+    uint32_t wstat[10];
+};
+// block-sync slots
+constexpr int BS_XE = 0, BS_TE = 1, BS_TIN = 2, BS_TH = 3, BS_TET = 4, BS_G = 5, BS_GTE = 6;
+
+__device__ inline float amax_of(const ScaleLDS *sc, int par, int nw, int q) {
+    float m = 0.f;
+    for (int w = 0; w < nw; w++) m = fmaxf(m, sc->amax[par][w][q]);
+    return m;
 }
 
 // ------------------------------------------------------------------------------------------------
 // GEMM pieces. 16x16x32 lane maps (cdna_hip_programming.md §3): lane l (kq = l >> 4, col = l & 15)
 // holds A[row col][k = 8 kq + j] and B[k = 8 kq + j][col col]; C/D element i is row 4 kq + i, col col.
 // ------------------------------------------------------------------------------------------------
-#define MF16(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
+#define MF16(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_f16((a), (b), (c), 0, 0, 0)
 
-struct AFrag {  // one operand fragment in its three split parts
-    bf16x8 h, m, l;
+struct AFrag {  // one operand fragment in its two split parts
+    h16x8 h, l;
 };
 
-__device__ inline AFrag load_a(const bf16x8 *p) { return AFrag{p[0], p[64], p[128]}; }
+__device__ inline AFrag load_a(const h16x8 *p) { return AFrag{p[0], p[64]}; }
 
 // B fragment of column tile q from the LDS image (p: this lane's unit of split 0, column tile 0)
-__device__ inline AFrag load_b(const bf16x8 *p, int q) { return AFrag{p[16 * q], p[BM + 16 * q], p[2 * BM + 16 * q]}; }
+__device__ inline AFrag load_b(const h16x8 *p, int q) { return AFrag{p[16 * q], p[BM + 16 * q]}; }
 
 __device__ inline f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
-// The six split products of one k-step: hh into the running accumulator, the five corrections
-// (|.| <= 2^-8 |hh|) into their own accumulator, added in fp32 once per GEMM (see the numerics note:
-// at 2^-8 of the sum's magnitude the corrections lose nothing in their own C)
-__device__ inline void mma6(const AFrag &a, const AFrag &b, f32x4 &acc, f32x4 &lo) {
-    lo = MF16(a.m, b.m, lo);
-    lo = MF16(a.h, b.l, lo);
+// The three split products of one k-step: hh into the running accumulator, the two corrections
+// (|.| <= 2^-11 |hh|) into their own accumulator, added in fp32 once per GEMM
+__device__ inline void mma3(const AFrag &a, const AFrag &b, f32x4 &acc, f32x4 &lo) {
     lo = MF16(a.l, b.h, lo);
-    lo = MF16(a.h, b.m, lo);
-    lo = MF16(a.m, b.h, lo);
+    lo = MF16(a.h, b.l, lo);
     acc = MF16(a.h, b.h, acc);
+}
+
+// inverse scale of an A image's n-tile: the float after its first k-slot's two planes
+__device__ __forceinline__ float a_inv(const h16x8 *tile_slot0) {
+    return reinterpret_cast<const float *>(tile_slot0 + 128)[0];
 }
 
 #ifdef DGS_MLP_PROFILE  // diagnostic build only (tools/mlp_phase.py): per-phase s_memtime stamps
@@ -274,21 +352,27 @@ struct HGate {
 
 // acc[q] += A . X for the column tiles q0 .. q0 + NQ_ - 1 over NK k-steps of this wave's A image
 // (Aw: unit pointer of its n-tile at k-step 0) and of the LDS image from group g0 (k-step c =
-// groups g0 + 4c + kq). Fully unrolled; per k-step: each column tile's six MFMAs followed by its B
+// groups g0 + 4c + kq). Fully unrolled; per k-step: each column tile's three MFMAs followed by its B
 // fragment for the next k-step into the same registers, then the A fragment RING k-steps ahead
 // (register ring: the A stream comes from L2). sched_barrier keeps that order per k-step; the other
-// three waves of the SIMD cover the B reload latency. pre() runs after the A prologue. SKIP: k-steps
+// waves of the SIMD cover the B reload latency. pre() runs after the A prologue. SKIP: k-steps
 // >= SKIP read the LDS image one k-step further on (linear.5 with t_emb folded: x_emb | h, past t_emb).
-template <int NK, int NQ_, class Pre = NoPre, class Gate = NoGate, int SKIP = (1 << 20)>
-__device__ inline void gemm(const bf16x8 *__restrict__ Aw, const bf16x8 *lds, int g0, int q0, int lane,
-                            f32x4 (&acc)[NQ_], Pre pre = Pre(), Gate gate = Gate()) {
+// Scales: ksc[g / 4][q] is the inverse scale of the image k-step at group g, column tile q (read once
+// its writers have signalled). BND: bit k set = k-step k starts a new scale group (x_emb | t_emb | h);
+// there the accumulators are brought to the new group's scale (one multiply by a power of two). ib[q]:
+// the inverse scale of the last group: the result is acc[q] * (A's inverse scale) * ib[q].
+template <int NK, int NQ_, class Pre = NoPre, class Gate = NoGate, int SKIP = (1 << 20), unsigned BND = 0u>
+__device__ inline void gemm(const h16x8 *__restrict__ Aw, const h16x8 *lds, int g0, int q0, int lane,
+                            f32x4 (&acc)[NQ_], float (&ib)[NQ_], const float (*ksc)[4], Pre pre = Pre(),
+                            Gate gate = Gate()) {
     static_assert(NK >= 1, "empty GEMM");
     const int kq = lane >> 4, col = lane & 15;
-    const bf16x8 *Ap = Aw + lane;
+    const h16x8 *Ap = Aw + lane;
     const int bunit = (g0 + kq) * UG + 16 * q0 + col;  // this lane's B unit at k-step 0
     constexpr int AK = KSLOT;
     constexpr int BK = KG * UG;
     auto bofs = [](int k) { return (k + (k >= SKIP ? 1 : 0)) * BK; };  // compile-time per unrolled k
+    auto kidx = [&](int k) { return (g0 >> 2) + k + (k >= SKIP ? 1 : 0); };
     // the B fragments of k-step k from a base formed once per k-step (the unit index is opaque to the
     // compiler): the image spans > 64 KB, so a single base would need one address add per ds_read
     // (a DS immediate offset is 16 bits); from the k-step base every fragment is an immediate offset
@@ -304,7 +388,10 @@ __device__ inline void gemm(const bf16x8 *__restrict__ Aw, const bf16x8 *lds, in
         if (k < NK) ring[k] = load_a(Ap + k * AK);
     pre();
     gate.need(0, gate.peek(0));
-    const bf16x8 *Bk = kbase(0);
+    float cur[NQ_], nxt[NQ_];
+#pragma unroll
+    for (int q = 0; q < NQ_; q++) nxt[q] = cur[q] = ksc[kidx(0)][q0 + q];
+    const h16x8 *Bk = kbase(0);
     AFrag b = load_b(Bk, 0);
     f32x4 lo[NQ_];
 #pragma unroll
@@ -313,31 +400,38 @@ __device__ inline void gemm(const bf16x8 *__restrict__ Aw, const bf16x8 *lds, in
     for (int k = 0; k < NK; k++) {
         __builtin_amdgcn_sched_barrier(0);
         if (k > 0) gate.done(k - 1);  // k-step k-1's B fragments were consumed by its MFMAs
+        if (k > 0 && k < 32 && ((BND >> k) & 1u)) {  // a new scale group starts here
+#pragma unroll
+            for (int q = 0; q < NQ_; q++) {
+                acc[q] = (acc[q] + lo[q]) * (cur[q] / nxt[q]);
+                lo[q] = zero4();
+                cur[q] = nxt[q];
+            }
+        }
         const uint32_t seen = k + 1 < NK ? gate.peek(k + 1) : 0u;
 #pragma unroll
         for (int q = 0; q < NQ_; q++) {
             // the next tile's B fragment (or the next k-step's first) is in flight during this tile's MFMAs
             AFrag nb;
-#ifdef DGS_DIAG_BHALF  // diagnostic only (wrong results): every other tile reuses the previous B fragment
-            if (q + 1 < NQ_) nb = ((q + 1) & 1) ? b : load_b(Bk, q + 1);
-#else
             if (q + 1 < NQ_) nb = load_b(Bk, q + 1);
-#endif
             else if (k + 1 < NK) {
                 gate.need(k + 1, seen);
+                if (k + 1 < 32 && ((BND >> (k + 1)) & 1u))
+#pragma unroll
+                    for (int q2 = 0; q2 < NQ_; q2++) nxt[q2] = ksc[kidx(k + 1)][q0 + q2];
                 Bk = kbase(k + 1);
                 nb = load_b(Bk, 0);
             }
-            // the reads stay ahead of ALL six MFMAs of this tile: without this barrier the scheduler,
-            // short of registers, sank them below the tile's first four MFMAs (reusing the current
+            // the reads stay ahead of ALL the MFMAs of this tile: without this barrier the scheduler,
+            // short of registers, sank them below the tile's first MFMAs (reusing the current
             // fragment's registers), so the next tile's first MFMAs waited on them (k_fwd -1.4 %,
             // profiles/r5f_mlp_bread_pin_ab.txt)
             __builtin_amdgcn_sched_barrier(0);
-            mma6(ring[k % RING], b, acc[q], lo[q]);
+            mma3(ring[k % RING], b, acc[q], lo[q]);
             if (q + 1 < NQ_ || k + 1 < NK) b = nb;
-            // pin the order per column tile: the next fragment's reads stay ahead of this tile's six
-            // MFMAs (left to itself the scheduler, at the 128-VGPR cap, pulls each read down to its
-            // first use and waits on it: lgkmcnt(0) in front of most MFMAs)
+            // pin the order per column tile: the next fragment's reads stay ahead of this tile's
+            // MFMAs (left to itself the scheduler pulls each read down to its first use and waits on
+            // it: lgkmcnt(0) in front of most MFMAs)
             __builtin_amdgcn_sched_barrier(0);
         }
         if (k + RING < NK) ring[k % RING] = load_a(Ap + (k + RING) * AK);
@@ -345,23 +439,28 @@ __device__ inline void gemm(const bf16x8 *__restrict__ Aw, const bf16x8 *lds, in
     }
     gate.done(NK - 1);
 #pragma unroll
-    for (int q = 0; q < NQ_; q++) acc[q] += lo[q];
+    for (int q = 0; q < NQ_; q++) {
+        acc[q] += lo[q];
+        ib[q] = cur[q];
+    }
 }
 
-// gemm() for TWO n-tiles per wave (the 8-wave k_fwd8): n-tile t's A image at Aw + t * astride units;
-// every B fragment read from LDS feeds both n-tiles' six MFMAs, so the activation image is read by 8
-// waves per layer instead of 16. Each (n-tile, column tile) accumulator sees the same MFMA sequence
-// as in gemm(): outputs bitwise equal to the 16-wave kernel.
-template <int NK, int NQ_, class Pre = NoPre, class Gate = NoGate, int SKIP = (1 << 20)>
-__device__ inline void gemm2(const bf16x8 *__restrict__ Aw, int astride, const bf16x8 *lds, int g0, int q0, int lane,
-                             f32x4 (&acc)[2][NQ_], Pre pre = Pre(), Gate gate = Gate()) {
+// gemm() for TWO n-tiles per wave (the 8-wave k_fwd8 / k_bwd8): n-tile t's A image at Aw + t * astride
+// units; every B fragment read from LDS feeds both n-tiles' MFMAs, so the activation image is read by 8
+// waves per layer instead of 16. Each (n-tile, column tile) accumulator sees the same MFMA sequence as
+// in gemm().
+template <int NK, int NQ_, class Pre = NoPre, class Gate = NoGate, int SKIP = (1 << 20), unsigned BND = 0u>
+__device__ inline void gemm2(const h16x8 *__restrict__ Aw, int astride, const h16x8 *lds, int g0, int q0, int lane,
+                             f32x4 (&acc)[2][NQ_], float (&ib)[NQ_], const float (*ksc)[4], Pre pre = Pre(),
+                             Gate gate = Gate()) {
     static_assert(NK >= 1, "empty GEMM");
     const int kq = lane >> 4, col = lane & 15;
-    const bf16x8 *Ap0 = Aw + lane, *Ap1 = Aw + astride + lane;
+    const h16x8 *Ap0 = Aw + lane, *Ap1 = Aw + astride + lane;
     const int bunit = (g0 + kq) * UG + 16 * q0 + col;
     constexpr int AK = KSLOT;
     constexpr int BK = KG * UG;
     auto bofs = [](int k) { return (k + (k >= SKIP ? 1 : 0)) * BK; };
+    auto kidx = [&](int k) { return (g0 >> 2) + k + (k >= SKIP ? 1 : 0); };
     auto kbase = [&](int k) {
         int u = bunit + bofs(k);
         asm volatile("" : "+v"(u));
@@ -377,7 +476,10 @@ __device__ inline void gemm2(const bf16x8 *__restrict__ Aw, int astride, const b
         }
     pre();
     gate.need(0, gate.peek(0));
-    const bf16x8 *Bk = kbase(0);
+    float cur[NQ_], nxt[NQ_];
+#pragma unroll
+    for (int q = 0; q < NQ_; q++) nxt[q] = cur[q] = ksc[kidx(0)][q0 + q];
+    const h16x8 *Bk = kbase(0);
     AFrag b = load_b(Bk, 0);
     f32x4 lo[2][NQ_];
 #pragma unroll
@@ -388,6 +490,18 @@ __device__ inline void gemm2(const bf16x8 *__restrict__ Aw, int astride, const b
     for (int k = 0; k < NK; k++) {
         __builtin_amdgcn_sched_barrier(0);
         if (k > 0) gate.done(k - 1);
+        if (k > 0 && k < 32 && ((BND >> k) & 1u)) {
+#pragma unroll
+            for (int q = 0; q < NQ_; q++) {
+                const float r = cur[q] / nxt[q];
+#pragma unroll
+                for (int t = 0; t < 2; t++) {
+                    acc[t][q] = (acc[t][q] + lo[t][q]) * r;
+                    lo[t][q] = zero4();
+                }
+                cur[q] = nxt[q];
+            }
+        }
         const uint32_t seen = k + 1 < NK ? gate.peek(k + 1) : 0u;
 #pragma unroll
         for (int q = 0; q < NQ_; q++) {
@@ -395,12 +509,15 @@ __device__ inline void gemm2(const bf16x8 *__restrict__ Aw, int astride, const b
             if (q + 1 < NQ_) nb = load_b(Bk, q + 1);
             else if (k + 1 < NK) {
                 gate.need(k + 1, seen);
+                if (k + 1 < 32 && ((BND >> (k + 1)) & 1u))
+#pragma unroll
+                    for (int q2 = 0; q2 < NQ_; q2++) nxt[q2] = ksc[kidx(k + 1)][q0 + q2];
                 Bk = kbase(k + 1);
                 nb = load_b(Bk, 0);
             }
             __builtin_amdgcn_sched_barrier(0);
-            mma6(ring[k % RING][0], b, acc[0][q], lo[0][q]);
-            mma6(ring[k % RING][1], b, acc[1][q], lo[1][q]);
+            mma3(ring[k % RING][0], b, acc[0][q], lo[0][q]);
+            mma3(ring[k % RING][1], b, acc[1][q], lo[1][q]);
             if (q + 1 < NQ_ || k + 1 < NK) b = nb;
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -415,17 +532,19 @@ __device__ inline void gemm2(const bf16x8 *__restrict__ Aw, int astride, const b
     for (int t = 0; t < 2; t++)
 #pragma unroll
         for (int q = 0; q < NQ_; q++) acc[t][q] += lo[t][q];
+#pragma unroll
+    for (int q = 0; q < NQ_; q++) ib[q] = cur[q];
 }
 
 // accumulator tile q (rows 16r + 4kq + i of this wave, point 16q + col) -> its 8-byte half of the
 // split units of group 2r + (kq >> 1) (LDS image from group gbase)
-__device__ inline void acc_to_lds(const f32x4 &v, bf16x8 *lds, int gbase, int r, int q, int lane) {
+// (times the layer's scale S)
+__device__ inline void acc_to_lds(const f32x4 &v, h16x8 *lds, int gbase, int r, int q, int lane, float S) {
     const int kq = lane >> 4, col = lane & 15;
-    const Split4 s = split4(v[0], v[1], v[2], v[3]);
-    bf16x4 *u = reinterpret_cast<bf16x4 *>(lds + (gbase + 2 * r + (kq >> 1)) * UG + 16 * q + col) + (kq & 1);
+    const Split4 s = split4(v[0], v[1], v[2], v[3], S);
+    h16x4 *u = reinterpret_cast<h16x4 *>(lds + (gbase + 2 * r + (kq >> 1)) * UG + 16 * q + col) + (kq & 1);
     u[0] = s.h;
-    u[2 * BM] = s.m;  // bf16x4 units: one 16-B unit = 2 of them
-    u[4 * BM] = s.l;
+    u[2 * BM] = s.l;  // h16x4 units: one 16-B unit = 2 of them
 }
 
 // A wave's 16-row x 64-point tile of a feature-major [rows][Ns] array through a buffer descriptor
@@ -500,15 +619,22 @@ __device__ inline float4 load_bias4(const float *bias, int r, int lane) {
     return *reinterpret_cast<const float4 *>(bias + 16 * r + 4 * (lane >> 4));
 }
 
+// v[q] * (ia * ib[q]) + b (ia: A's inverse scale, ib: the GEMM's B scales per column tile), then ReLU
 template <int NQ_>
-__device__ inline void bias_relu(f32x4 (&v)[NQ_], float4 b, bool relu) {
+__device__ inline void bias_relu(f32x4 (&v)[NQ_], float ia, const float (&ib)[NQ_], float4 b, bool relu) {
 #pragma unroll
     for (int q = 0; q < NQ_; q++) {
-        v[q] += f32x4{b.x, b.y, b.z, b.w};  // two v_pk_add_f32
+        v[q] = v[q] * (ia * ib[q]) + f32x4{b.x, b.y, b.z, b.w};
         if (relu)
 #pragma unroll
             for (int i = 0; i < 4; i++) v[q][i] = fmaxf(v[q][i], 0.f);
     }
+}
+
+template <int NQ_>
+__device__ inline void scale_tiles(f32x4 (&v)[NQ_], float ia, const float (&ib)[NQ_]) {
+#pragma unroll
+    for (int q = 0; q < NQ_; q++) v[q] *= ia * ib[q];
 }
 
 template <int NQ_>
@@ -540,7 +666,7 @@ struct FwdArgs {
     int N;
     size_t Ns;
     const float *xyz, *t;
-    const bf16x8 *img;  // A images
+    const h16x8 *img;  // A images
     const float *fp;    // fp32 region: biases, timenet weights
     float *out;
     float *saved;
@@ -555,6 +681,12 @@ struct FwdArgs {
     uint32_t *queue;  // block queue (persistent launch, BlockQueue) or nullptr: one launch block per block
     int nblk;         // blocks (64-point + 16-point)
 };
+
+// k_pack's statistic of an image n-tile: max over its 16 rows of sum_k |A[row][k]| (the float after the
+// tile's inverse scale)
+__device__ __forceinline__ float tile_stat(const h16x8 *tile_slot0) {
+    return reinterpret_cast<const float *>(tile_slot0 + 128)[1];
+}
 
 // The reference feeds every Gaussian the same frame time (train_baseline.py:107-110), so the
 // timenet (time_utils.py:74-76, 13 -> 256 -> 30) has one value per launch: evaluated here once in
@@ -626,9 +758,30 @@ __global__ __launch_bounds__(256) void k_timenet(FwdArgs a) {
 // One block of NQB 16-point column tiles (NQB = 4: the 64-point blocks; NQB = 1: the 16-point tail
 // blocks that spread the last, sparse round of blocks over the idle CUs). p0: first point; slot: the
 // block's relu'-mask slot.
+
+// per column tile q (16 points): max |v| over this wave's tiles of it (two n-tiles: both), in every lane
+template <int NQ_>
+__device__ inline void col_absmax(const f32x4 (&v)[NQ_], float (&m)[NQ_]) {
+#pragma unroll
+    for (int q = 0; q < NQ_; q++) {
+        float x = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; i++) x = fmaxf(x, fabsf(v[q][i]));
+        m[q] = fmaxf(m[q], x);
+    }
+}
+template <int NQ_>
+__device__ inline void col_wave_max(float (&m)[NQ_]) {
+#pragma unroll
+    for (int q = 0; q < NQ_; q++) m[q] = wave_max(m[q]);
+}
+
+// the stage value of point slot m (0 .. 63 of the image) goes to column tile m >> 4
+__device__ __forceinline__ int qof(int m) { return m >> 4; }
+
 template <bool SAVE, int NQB, bool FOLD>
-__device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_t *hwr, uint32_t *hrd, const float4 *sb,
-                                          uint32_t *s_mpend, int p0, int slot) {
+__device__ __forceinline__ void fwd_block(const FwdArgs &a, h16x8 *lds, uint32_t *hwr, uint32_t *hrd, const float4 *sb,
+                                          uint32_t *s_mpend, ScaleLDS *sc, int p0, int slot) {
     constexpr int BMB = 16 * NQB;  // points of this block (the LDS images keep the BM-point stride)
     float *lf = reinterpret_cast<float *>(lds);
     float *stage = lf + G_H * UG * 4;  // fp32 [112][BM] feature staging (H region, before the trunk)
@@ -675,16 +828,22 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
         hwr[tid] = 0;
         hrd[tid] = 0;
     }
+    if (tid < 32) (&sc->bsync[0][0])[tid] = 0;
     // ---- positional encodings (utils/time_utils.py:42-54) into fp32 staging: feature 3 band + d,
     // band 0 = x, band 1 + 2i = sin(2^i x), band 2 + 2i = cos(2^i x). The block's xyz rows are read
     // once (one coalesced load per thread, a single HBM round trip) into the identity band, then the
-    // 10 sin/cos bands are evaluated from LDS in two rounds of the workgroup ----
+    // 10 sin/cos bands are evaluated from LDS in two rounds of the workgroup. x_emb's scale bound per
+    // column tile: max(1, max |xyz|) (|sin|, |cos| <= 1) ----
+    float xmax = 0.f;
     if (tid < 3 * BMB) {
         const int m = tid / 3, d = tid - 3 * m;
-        stage[d * BM + m] = p0 + m < pend ? a.xyz[3 * (size_t)p0 + tid] : 0.f;
+        const float v = p0 + m < pend ? a.xyz[3 * (size_t)p0 + tid] : 0.f;
+        stage[d * BM + m] = v;
+        xmax = fabsf(v);
     }
     if (tid < BMB) stage[63 * BM + tid] = 0.f;  // padding feature
     __syncthreads();
+    if (tid < 3 * BMB) lds_fmax(&sc->bsync[BS_XE][qof(tid / 3)], xmax);
     for (int e = tid; e < BMB * 3 * 10; e += NTHR) {
         const int m = e % BMB, rr = e / BMB, d = rr % 3, i = rr / 3;
         const bool ok = p0 + m < pend;
@@ -697,7 +856,9 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
     } else if (uniform_t) {  // TE and TIN: k_timenet's values broadcast over the points
         for (int e = tid; e < 48 * BMB; e += NTHR) {
             const int f = e / BMB, m = e % BMB;
-            stage[(ST_TE + f) * BM + m] = f < 32 ? a.tc[TC_TE + f] : a.tc[TC_TIN + f - 32];
+            const float v = f < 32 ? a.tc[TC_TE + f] : a.tc[TC_TIN + f - 32];
+            stage[(ST_TE + f) * BM + m] = v;
+            lds_fmax(&sc->bsync[f < 32 ? BS_TE : BS_TIN][qof(m)], fabsf(v));
         }
     } else {  // per-point t encodings: TIN (blender, 16 rows) or the raw t PE as TE (32 rows)
         const int row0 = F.blender ? ST_TIN : ST_TE, nrow = F.blender ? 16 : 32;
@@ -716,9 +877,22 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
                 }
             }
             stage[(row0 + f) * BM + m] = v;
+            lds_fmax(&sc->bsync[F.blender ? BS_TIN : BS_TE][qof(m)], fabsf(v));
         }
     }
     __syncthreads();
+    // column-tile scales of the staged inputs (every thread evaluates the same values)
+    if (tid < 4) {
+        const int q = tid;
+        const float xe_b = fmaxf(1.f, __uint_as_float(sc->bsync[BS_XE][q]));
+        sc->ksc[0][q] = sc->ksc[1][q] = scale_for(xe_b).inv;
+        sc->ain[0][q] = xe_b;
+        if (!fold) {
+            sc->ksc[G_TE / 4][q] = scale_for(__uint_as_float(sc->bsync[BS_TE][q])).inv;
+            sc->ksc[G_TIN / 4][q] = scale_for(__uint_as_float(sc->bsync[BS_TIN][q])).inv;
+            sc->ain[1][q] = __uint_as_float(sc->bsync[BS_TE][q]);  // per-point blender: replaced by the TE tile's
+        }
+    }
     // saved network inputs (fp32, coalesced) and their split LDS images
     const bool te_ready = uniform_t || !F.blender;
     if (SAVE) {
@@ -742,14 +916,17 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
             float v[8];
 #pragma unroll
             for (int j = 0; j < 8; j++) v[j] = stage[(8 * g + j) * BM + m];
-            put_unit8(lds, g < 12 ? g : G_TIN + g - 12, m, v);
+            const int slot_b = g < G_TE ? BS_XE : g < 12 ? BS_TE : BS_TIN;
+            const float bnd = __uint_as_float(sc->bsync[slot_b][qof(m)]);
+            put_unit8(lds, g < 12 ? g : G_TIN + g - 12, m, v, scale_for(g < G_TE ? fmaxf(1.f, bnd) : bnd).s);
         }
         if (F.blender && !fold)  // TIN k-step padding (features 16..31): zero, not stale LDS
-            for (int u = tid; u < 2 * UG; u += NTHR) lds[(G_TIN + 2) * UG + u] = bf16x8{};
+            for (int u = tid; u < 2 * UG; u += NTHR) lds[(G_TIN + 2) * UG + u] = h16x8{};
     }
     lds_barrier();
     DGS_STAMP(1);
     f32x4 c[NQB];
+    float ib[NQB];
     if (SAVE && uniform_t && !F.uniform_t) {  // TH tile from k_timenet: relu' bits + saved rows (per-point backward)
         const float4 th = load_bias4(a.tc + TC_TH, r, lane);
 #pragma unroll
@@ -757,26 +934,52 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
         store_mask(relu_bits(c), MR_TH + r);
         tile16(a.saved, Ns, S_TH + 16 * r, p0, lane).store(c);
     }
-    // ---- per-point timenet (blender, t not frame-uniform): Linear(13,256)+ReLU -> H; Linear(256,30) -> TE
+    // ---- per-point timenet (blender, t not frame-uniform): Linear(13,256)+ReLU -> H; Linear(256,30) -> TE.
+    // Both outputs are narrow per-block tiles: their scales are the actual maxima per column tile,
+    // gathered behind a workgroup barrier
     if (F.blender && !uniform_t) {
         zero_tiles(c);
-        gemm<1, NQB>(a.img + (size_t)(a.fT1 + r) * KSLOT, lds, G_TIN, 0, lane, c);
-        bias_relu(c, load_bias4(a.fp + a.bT1, r, lane), true);
+        const h16x8 *A1 = a.img + (size_t)(a.fT1 + r) * KSLOT;
+        gemm<1, NQB>(A1, lds, G_TIN, 0, lane, c, ib, sc->ksc);
+        bias_relu(c, a_inv(A1), ib, load_bias4(a.fp + a.bT1, r, lane), true);
         if (SAVE) {
             store_mask(relu_bits(c), MR_TH + r);
             tile16(a.saved, Ns, S_TH + 16 * r, p0, lane).store(c);
         }
+        float thm[NQB] = {};
+        col_absmax(c, thm);
+        col_wave_max(thm);
+        if (lane == 0)
 #pragma unroll
-        for (int q = 0; q < NQB; q++) acc_to_lds(c[q], lds, G_H, r, q, lane);
+            for (int q = 0; q < NQB; q++) lds_fmax(&sc->bsync[BS_TH][q], thm[q]);
         lds_barrier();
+#pragma unroll
+        for (int q = 0; q < NQB; q++)
+            acc_to_lds(c[q], lds, G_H, r, q, lane, scale_for(__uint_as_float(sc->bsync[BS_TH][q])).s);
+        if (tid < 32) sc->ksc[G_H / 4 + (tid >> 2)][tid & 3] = scale_for(__uint_as_float(sc->bsync[BS_TH][tid & 3])).inv;
+        lds_barrier();
+        f32x4 c1[1] = {zero4()};
         if (r < 2 * NQB) {  // TE tile (n-tile r / NQB of 2, column tile r % NQB), full K on one wave
             const int nt = r / NQB, q = r % NQB;
-            f32x4 c1[1] = {zero4()};
-            gemm<8, 1>(a.img + (size_t)(a.fT2 + nt * 8) * KSLOT, lds, G_H, q, lane, c1);
+            const h16x8 *A2 = a.img + (size_t)(a.fT2 + nt * 8) * KSLOT;
+            float ib2[1];
+            gemm<8, 1>(A2, lds, G_H, q, lane, c1, ib2, sc->ksc);
             const float4 b = load_bias4(a.fp + a.bT2, nt, lane);
-            c1[0] += f32x4{b.x, b.y, b.z, b.w};
+            c1[0] = c1[0] * (a_inv(A2) * ib2[0]) + f32x4{b.x, b.y, b.z, b.w};
             if (SAVE) tile16(a.saved, Ns, S_TE + 16 * nt, p0, lane).store(c1, q);
-            acc_to_lds(c1[0], lds, G_TE, nt, q, lane);  // TE groups: not read by the T2 GEMM
+            float tm[1] = {0.f};
+            col_absmax(c1, tm);
+            col_wave_max(tm);
+            if (lane == 0) lds_fmax(&sc->bsync[BS_TET][q], tm[0]);
+        }
+        lds_barrier();
+        if (r < 2 * NQB)  // TE groups: not read by the T2 GEMM
+            acc_to_lds(c1[0], lds, G_TE, r / NQB, r % NQB, lane,
+                       scale_for(__uint_as_float(sc->bsync[BS_TET][r % NQB])).s);
+        if (tid < 4) {
+            const float tet = __uint_as_float(sc->bsync[BS_TET][tid]);
+            sc->ksc[G_TE / 4][tid] = scale_for(tet).inv;
+            sc->ain[1][tid] = tet;
         }
         lds_barrier();
     }
@@ -784,44 +987,60 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
     // No workgroup barriers: the four waves of a SIMD finish a GEMM thousands of cycles apart (the
     // oldest issues first), so each wave runs its epilogue as soon as every wave has read the H
     // k-step it overwrites (hrd), and the next layer reads an H k-step once its two writer waves
-    // have stored it (hwr): early waves' epilogues overlap late waves' MFMAs.
+    // have stored it (hwr): early waves' epilogues overlap late waves' MFMAs. Every writer derives the
+    // layer's output scales from the same bounds (header note), so none waits for another's maximum.
 #pragma unroll 1
     for (int L = 0; L < 8; L++) {
         const int g0 = (L == 0 || L == 5) ? G_XE : G_H;
         const int nk = layer_kpad_f(F, L) / 32;
         zero_tiles(c);
-        const bf16x8 *Aw = a.img + (size_t)(a.fL[L] + r * nk) * KSLOT;
-        float4 bv;
-        // the bias comes from the workgroup's LDS copy after the GEMM (sb): a register preload
-        // across the GEMM was spilled at 128 VGPRs and its scratch reload sat in every epilogue
-        using PreT = NoPre;
-        const PreT bp{};
+        const h16x8 *Aw = a.img + (size_t)(a.fL[L] + r * nk) * KSLOT;
         const HGate hg{hwr, hrd, L == 5 ? (fold ? 2 : 3) : 0, 2u * L, true, lane};
         if (L == 0) {
-            if constexpr (FOLD) gemm<2, NQB>(Aw, lds, g0, 0, lane, c, bp);  // XE only
-            else gemm<3, NQB>(Aw, lds, g0, 0, lane, c, bp);                 // XE | TE
+            if constexpr (FOLD) gemm<2, NQB>(Aw, lds, g0, 0, lane, c, ib, sc->ksc);  // XE only
+            else gemm<3, NQB, NoPre, NoGate, 1 << 20, 1u << 2>(Aw, lds, g0, 0, lane, c, ib, sc->ksc);  // XE | TE
         } else if (L == 5) {
-            if constexpr (FOLD) gemm<10, NQB, PreT, HGate, 2>(Aw, lds, g0, 0, lane, c, bp, hg);  // XE | H
-            else gemm<11, NQB>(Aw, lds, g0, 0, lane, c, bp, hg);                                    // XE | TE | H
+            if constexpr (FOLD) gemm<10, NQB, NoPre, HGate, 2, 1u << 2>(Aw, lds, g0, 0, lane, c, ib, sc->ksc, NoPre(), hg);  // XE | H
+            else gemm<11, NQB, NoPre, HGate, 1 << 20, (1u << 2) | (1u << 3)>(Aw, lds, g0, 0, lane, c, ib, sc->ksc, NoPre(), hg);  // XE | TE | H
         } else {
-            gemm<8, NQB>(Aw, lds, g0, 0, lane, c, bp, hg);
+            gemm<8, NQB>(Aw, lds, g0, 0, lane, c, ib, sc->ksc, NoPre(), hg);
         }
-        bv = sb[64 * L + 4 * r + kq];
+        const float4 bv = sb[64 * L + 4 * r + kq];
         DGS_STAMP(4 + 2 * L);
         DGS_WSTAMP(22, L);  // per wave: GEMM end (layer 3)
-        bias_relu(c, bv, true);
+        bias_relu(c, a_inv(Aw), ib, bv, true);
         if (SAVE) {
             trunk_mask(relu_bits(c), L);
 #ifndef DGS_DIAG_NOSAVE  // diagnostic only (wrong backward): the trunk's saved-activation stores skipped
             tile16(a.saved, Ns, s_h(L) + 16 * r, p0, lane).store(c);
 #endif
         }
+        // the layer's output scales: max_rows sum |W_L| x max |input| + max |b_L| per column tile (the
+        // same on every wave)
+        float so[NQB], my[NQB] = {};
+        const float ws = __uint_as_float(sc->wstat[L]), bm = __uint_as_float(sc->bmax[L]);
+#pragma unroll
+        for (int q = 0; q < NQB; q++) {
+            float ain = L == 0 || L == 5 ? sc->ain[0][q] : 0.f;
+            if (!fold && (L == 0 || L == 5)) ain = fmaxf(ain, sc->ain[1][q]);
+            if (L > 0) ain = fmaxf(ain, amax_of(sc, (L - 1) & 1, NWAVE, q));
+            so[q] = fmaf(ws, ain, bm);
+        }
+        col_absmax(c, my);
+        col_wave_max(my);
         if (L == 3 && r == 0) DGS_STAMP(54);
-        // this wave's rows are H k-step r / 2: every wave must have read it in this layer
+        // this wave's rows are H k-step r / 2: every wave must have read it (and its scales) in this layer
         if (L > 0) lds_wait_ge(hrd + (r >> 1), 16u * L, lds_peek(hrd + (r >> 1)));
         if (L == 3 && r == 0) DGS_STAMP(56);
 #pragma unroll
-        for (int q = 0; q < NQB; q++) acc_to_lds(c[q], lds, G_H, r, q, lane);
+        for (int q = 0; q < NQB; q++) {
+            const Scale s = scale_for(so[q]);
+            if (lane == 0) {
+                sc->amax[L & 1][r][q] = my[q];
+                sc->ksc[G_H / 4 + (r >> 1)][q] = s.inv;
+            }
+            acc_to_lds(c[q], lds, G_H, r, q, lane, s.s);
+        }
         lds_signal(hwr + (r >> 1), lane);
         if (L == 3 && r == 0) DGS_STAMP(55);
         DGS_STAMP(5 + 2 * L);
@@ -835,9 +1054,11 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
     const int hq = r - (NWAVE - NQB);
     if (hq >= 0) {
         f32x4 c1[1] = {zero4()};
-        gemm<8, 1>(a.img + (size_t)a.fHd * KSLOT, lds, G_H, hq, lane, c1, NoPre(), HGate{hwr, hrd, 0, 16u, false, lane});
+        float ib1[1];
+        const h16x8 *Ah = a.img + (size_t)a.fHd * KSLOT;
+        gemm<8, 1>(Ah, lds, G_H, hq, lane, c1, ib1, sc->ksc, NoPre(), HGate{hwr, hrd, 0, 16u, false, lane});
         const float4 b = sb[8 * 64 + kq];
-        c1[0] += f32x4{b.x, b.y, b.z, b.w};
+        c1[0] = c1[0] * (a_inv(Ah) * ib1[0]) + f32x4{b.x, b.y, b.z, b.w};
         const int p = p0 + 16 * hq + col;
 #pragma unroll
         for (int i = 0; i < 4; i++)
@@ -852,30 +1073,46 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, bf16x8 *lds, uint32_
 #endif
 }
 
-template <bool SAVE, bool FOLD>
-__global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
-    __shared__ bf16x8 lds[G_FWD * UG];
-    __shared__ uint32_t hwr[8], hrd[8];  // trunk hand-off counters (HGate)
-    __shared__ int s_next;
-    // trunk and head biases (launch constants: FOLD's linear.0 / linear.5 biases come from
-    // k_timenet), one float4 per (layer, 4 rows), the heads' 16 rows last; the first block's staging
-    // barriers publish them
-    __shared__ float4 s_bias[8 * 64 + 4];
-    __shared__ uint32_t s_mpend[NTHR];  // relu' bits of an even trunk layer, per thread (fwd_block)
-    for (int i = threadIdx.x; i < 8 * 64 + 4; i += NTHR) {
+// The launch-constant bias table of the forward kernels (one float4 per (layer, 4 rows), the heads' 16
+// rows last; FOLD's linear.0 / linear.5 biases come from k_timenet), each layer's max |b| and the trunk
+// images' row statistics (over their 16 n-tiles) for the output-scale bounds
+template <bool FOLD>
+__device__ inline void load_bias_table(const FwdArgs &a, float4 *s_bias, ScaleLDS *sc, int nthr) {
+    if (threadIdx.x < 10) sc->bmax[threadIdx.x] = sc->wstat[threadIdx.x] = 0;
+    __syncthreads();
+    if (threadIdx.x < 8 * 16) {
+        const int L = threadIdx.x >> 4, t = threadIdx.x & 15;
+        const int nk = layer_kpad_f(make_flags(a.flags), L) / 32;
+        lds_fmax(&sc->wstat[L], tile_stat(a.img + (size_t)(a.fL[L] + t * nk) * KSLOT));
+    }
+    for (int i = threadIdx.x; i < 8 * 64 + 4; i += nthr) {
         const int L = i >> 6;
         const float *bias = L == 8                ? a.fp + a.bHd
                             : FOLD && L == 0      ? a.tc + TC_C0
                             : FOLD && L == 5      ? a.tc + TC_C5
                                                   : a.fp + a.bL[L];
-        s_bias[i] = reinterpret_cast<const float4 *>(bias)[i & 63];
+        const float4 v = reinterpret_cast<const float4 *>(bias)[i & 63];
+        s_bias[i] = v;
+        lds_fmax(&sc->bmax[L], fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
     }
+}
+
+template <bool SAVE, bool FOLD>
+__global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
+    __shared__ h16x8 lds[G_FWD * UG];
+    __shared__ uint32_t hwr[8], hrd[8];  // trunk hand-off counters (HGate)
+    __shared__ int s_next;
+    __shared__ float4 s_bias[8 * 64 + 4];
+    __shared__ uint32_t s_mpend[NTHR];  // relu' bits of an even trunk layer, per thread (fwd_block)
+    __shared__ ScaleLDS sc;
+    // the first block's staging barriers publish the bias table
+    load_bias_table<FOLD>(a, s_bias, &sc, NTHR);
     CLK_BEGIN();
     for (int b = blockIdx.x;;) {
         int nx = 0;
         if (a.queue && threadIdx.x == 0) nx = queue_take(a.queue);
-        if (b < a.nfull) fwd_block<SAVE, NQ, FOLD>(a, lds, hwr, hrd, s_bias, s_mpend, b * BM, b);
-        else fwd_block<SAVE, 1, FOLD>(a, lds, hwr, hrd, s_bias, s_mpend, a.nfull * BM + (b - a.nfull) * 16, b);
+        if (b < a.nfull) fwd_block<SAVE, NQ, FOLD>(a, lds, hwr, hrd, s_bias, s_mpend, &sc, b * BM, b);
+        else fwd_block<SAVE, 1, FOLD>(a, lds, hwr, hrd, s_bias, s_mpend, &sc, a.nfull * BM + (b - a.nfull) * 16, b);
         if (!a.queue) break;
         if (threadIdx.x == 0) s_next = nx;
         __syncthreads();  // also: the next block's staging overwrites LDS this one's heads read
@@ -888,13 +1125,13 @@ __global__ __launch_bounds__(NTHR) void k_fwd(FwdArgs a) {
 
 
 // The training forward (saved activations, frame-uniform t folded) as 8 waves of two n-tiles
-// (k_fwd8, 512 threads, 2 waves per SIMD, 256 VGPRs): wave w owns rows 32w .. 32w + 31 of every trunk
-// layer = H k-step w, so each k-step has ONE writer (hand-off target L per layer) and 8 readers.
-// Same LDS image, saved-activation / relu'-mask layouts and arithmetic as fwd_block<true, NQB, true>.
+// (k_fwd8, 512 threads, 2 waves per SIMD): wave w owns rows 32w .. 32w + 31 of every trunk layer = H
+// k-step w, so each k-step has ONE writer (hand-off target L per layer) and 8 readers. Same LDS image,
+// saved-activation / relu'-mask layouts, scales and arithmetic as fwd_block<true, NQB, true>.
 constexpr int NW8 = 8, NTHR8 = NW8 * 64;
 template <int NQB>
-__device__ __forceinline__ void fwd_block8(const FwdArgs &a, bf16x8 *lds, uint32_t *hwr, uint32_t *hrd, const float4 *sb,
-                                           uint32_t *s_mpend, int p0, int slot) {
+__device__ __forceinline__ void fwd_block8(const FwdArgs &a, h16x8 *lds, uint32_t *hwr, uint32_t *hrd, const float4 *sb,
+                                           uint32_t *s_mpend, ScaleLDS *sc, int p0, int slot) {
     constexpr int BMB = 16 * NQB;
     float *lf = reinterpret_cast<float *>(lds);
     float *stage = lf + G_H * UG * 4;
@@ -920,13 +1157,18 @@ __device__ __forceinline__ void fwd_block8(const FwdArgs &a, bf16x8 *lds, uint32
         hwr[tid] = 0;
         hrd[tid] = 0;
     }
+    if (tid < 4) sc->bsync[BS_XE][tid] = 0;
     // positional encodings (utils/time_utils.py:42-54), as fwd_block
+    float xmax = 0.f;
     if (tid < 3 * BMB) {
         const int m = tid / 3, d = tid - 3 * m;
-        stage[d * BM + m] = p0 + m < pend ? a.xyz[3 * (size_t)p0 + tid] : 0.f;
+        const float v = p0 + m < pend ? a.xyz[3 * (size_t)p0 + tid] : 0.f;
+        stage[d * BM + m] = v;
+        xmax = fabsf(v);
     }
     if (tid < BMB) stage[63 * BM + tid] = 0.f;
     __syncthreads();
+    if (tid < 3 * BMB) lds_fmax(&sc->bsync[BS_XE][qof(tid / 3)], xmax);
     for (int e = tid; e < BMB * 3 * 10; e += NTHR8) {
         const int m = e % BMB, rr = e / BMB, d = rr % 3, i = rr / 3;
         const bool ok = p0 + m < pend;
@@ -936,6 +1178,11 @@ __device__ __forceinline__ void fwd_block8(const FwdArgs &a, bf16x8 *lds, uint32
         stage[(3 * (2 + 2 * i) + d) * BM + m] = ok ? cv : 0.f;
     }
     __syncthreads();
+    if (tid < 4) {
+        const float xe_b = fmaxf(1.f, __uint_as_float(sc->bsync[BS_XE][tid]));
+        sc->ksc[0][tid] = sc->ksc[1][tid] = scale_for(xe_b).inv;
+        sc->ain[0][tid] = xe_b;
+    }
     for (int e = tid; e < 64 * BMB; e += NTHR8) {  // saved x_emb rows (folded: dW reads x_emb only)
         const int f = e / BMB, m = e % BMB;
         a.saved[(size_t)(S_XE + f) * Ns + p0 + m] = stage[f * BM + m];
@@ -945,44 +1192,66 @@ __device__ __forceinline__ void fwd_block8(const FwdArgs &a, bf16x8 *lds, uint32
         float v[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) v[j] = stage[(8 * g + j) * BM + m];
-        put_unit8(lds, g, m, v);
+        put_unit8(lds, g, m, v, scale_for(fmaxf(1.f, __uint_as_float(sc->bsync[BS_XE][qof(m)]))).s);
     }
     lds_barrier();
     f32x4 c[2][NQB];
+    float ib[NQB];
 #pragma unroll 1
     for (int L = 0; L < 8; L++) {
         const int g0 = (L == 0 || L == 5) ? G_XE : G_H;
         const int nk = layer_kpad_f(F, L) / 32;
 #pragma unroll
         for (int t = 0; t < 2; t++) zero_tiles(c[t]);
-        const bf16x8 *Aw = a.img + (size_t)(a.fL[L] + 2 * w * nk) * KSLOT;
+        const h16x8 *Aw = a.img + (size_t)(a.fL[L] + 2 * w * nk) * KSLOT;
         const int astride = nk * KSLOT;
         const HGate hg{hwr, hrd, L == 5 ? 2 : 0, 1u * L, true, lane};
-        if (L == 0) gemm2<2, NQB>(Aw, astride, lds, g0, 0, lane, c);
-        else if (L == 5) gemm2<10, NQB, NoPre, HGate, 2>(Aw, astride, lds, g0, 0, lane, c, NoPre(), hg);
-        else gemm2<8, NQB>(Aw, astride, lds, g0, 0, lane, c, NoPre(), hg);
+        if (L == 0) gemm2<2, NQB>(Aw, astride, lds, g0, 0, lane, c, ib, sc->ksc);
+        else if (L == 5) gemm2<10, NQB, NoPre, HGate, 2, 1u << 2>(Aw, astride, lds, g0, 0, lane, c, ib, sc->ksc, NoPre(), hg);
+        else gemm2<8, NQB>(Aw, astride, lds, g0, 0, lane, c, ib, sc->ksc, NoPre(), hg);
+        float my[NQB] = {};
 #pragma unroll
         for (int t = 0; t < 2; t++) {
             const int nt = 2 * w + t;
-            bias_relu(c[t], sb[64 * L + 4 * nt + kq], true);
+            bias_relu(c[t], a_inv(Aw + t * astride), ib, sb[64 * L + 4 * nt + kq], true);
             trunk_mask(relu_bits(c[t]), L, nt);
             tile16(a.saved, Ns, s_h(L) + 16 * nt, p0, lane).store(c[t]);
+            col_absmax(c[t], my);
         }
-        // this wave's rows are H k-step w: all 8 waves must have read it in this layer
+        // the layer's output scales: max_rows sum |W_L| x max |input| + max |b_L| per column tile (the
+        // same on every wave)
+        float so[NQB];
+        const float ws = __uint_as_float(sc->wstat[L]), bm = __uint_as_float(sc->bmax[L]);
+#pragma unroll
+        for (int q = 0; q < NQB; q++) {
+            float ain = L == 0 || L == 5 ? sc->ain[0][q] : 0.f;
+            if (L > 0) ain = fmaxf(ain, amax_of(sc, (L - 1) & 1, NW8, q));
+            so[q] = fmaf(ws, ain, bm);
+        }
+        col_wave_max(my);
+        // this wave's rows are H k-step w: all 8 waves must have read it (and its scales) in this layer
         if (L > 0) lds_wait_ge(hrd + w, (uint32_t)NW8 * L, lds_peek(hrd + w));
 #pragma unroll
-        for (int t = 0; t < 2; t++)
+        for (int q = 0; q < NQB; q++) {
+            const Scale s = scale_for(so[q]);
+            if (lane == 0) {
+                sc->amax[L & 1][w][q] = my[q];
+                sc->ksc[G_H / 4 + w][q] = s.inv;
+            }
 #pragma unroll
-            for (int q = 0; q < NQB; q++) acc_to_lds(c[t][q], lds, G_H, 2 * w + t, q, lane);
+            for (int t = 0; t < 2; t++) acc_to_lds(c[t][q], lds, G_H, 2 * w + t, q, lane, s.s);
+        }
         lds_signal(hwr + w, lane);
     }
     // heads on the last NQB waves (one column tile each), once all 8 layers' writers have signalled
     const int hq = w - (NW8 - NQB);
     if (hq >= 0) {
         f32x4 c1[1] = {zero4()};
-        gemm<8, 1>(a.img + (size_t)a.fHd * KSLOT, lds, G_H, hq, lane, c1, NoPre(), HGate{hwr, hrd, 0, 8u, false, lane});
+        float ib1[1];
+        const h16x8 *Ah = a.img + (size_t)a.fHd * KSLOT;
+        gemm<8, 1>(Ah, lds, G_H, hq, lane, c1, ib1, sc->ksc, NoPre(), HGate{hwr, hrd, 0, 8u, false, lane});
         const float4 b = sb[8 * 64 + kq];
-        c1[0] += f32x4{b.x, b.y, b.z, b.w};
+        c1[0] = c1[0] * (a_inv(Ah) * ib1[0]) + f32x4{b.x, b.y, b.z, b.w};
         const int p = p0 + 16 * hq + (lane & 15);
 #pragma unroll
         for (int i = 0; i < 4; i++)
@@ -991,21 +1260,18 @@ __device__ __forceinline__ void fwd_block8(const FwdArgs &a, bf16x8 *lds, uint32
 }
 
 __global__ __launch_bounds__(NTHR8) void k_fwd8(FwdArgs a) {
-    __shared__ bf16x8 lds[G_FWD * UG];
+    __shared__ h16x8 lds[G_FWD * UG];
     __shared__ uint32_t hwr[8], hrd[8];
     __shared__ int s_next;
     __shared__ float4 s_bias[8 * 64 + 4];
     __shared__ uint32_t s_mpend[NTHR];  // [n-tile][64 lanes]
-    for (int i = threadIdx.x; i < 8 * 64 + 4; i += NTHR8) {
-        const int L = i >> 6;
-        const float *bias = L == 8 ? a.fp + a.bHd : L == 0 ? a.tc + TC_C0 : L == 5 ? a.tc + TC_C5 : a.fp + a.bL[L];
-        s_bias[i] = reinterpret_cast<const float4 *>(bias)[i & 63];
-    }
+    __shared__ ScaleLDS sc;
+    load_bias_table<true>(a, s_bias, &sc, NTHR8);
     for (int b = blockIdx.x;;) {
         int nx = 0;
         if (a.queue && threadIdx.x == 0) nx = queue_take(a.queue);
-        if (b < a.nfull) fwd_block8<NQ>(a, lds, hwr, hrd, s_bias, s_mpend, b * BM, b);
-        else fwd_block8<1>(a, lds, hwr, hrd, s_bias, s_mpend, a.nfull * BM + (b - a.nfull) * 16, b);
+        if (b < a.nfull) fwd_block8<NQ>(a, lds, hwr, hrd, s_bias, s_mpend, &sc, b * BM, b);
+        else fwd_block8<1>(a, lds, hwr, hrd, s_bias, s_mpend, &sc, a.nfull * BM + (b - a.nfull) * 16, b);
         if (!a.queue) break;
         if (threadIdx.x == 0) s_next = nx;
         __syncthreads();
@@ -1021,7 +1287,7 @@ __global__ __launch_bounds__(NTHR8) void k_fwd8(FwdArgs a) {
 struct BwdArgs {
     int N;
     size_t Ns;
-    const bf16x8 *img;
+    const h16x8 *img;
     const uint32_t *mask;
     const float *dout;
     float *dz;
@@ -1049,11 +1315,67 @@ struct MaskPre {
     __device__ void operator()() const { *mk = tile[lane]; }
 };
 
+// the dX chain's row statistics (launch constants): wstat[L] over tL[L]'s n-tiles (max column abs sum
+// of W_L), wstat[8] over the heads' transposed image; published by the first block's staging barriers
+__device__ inline void load_wstats_bwd(const BwdArgs &a, ScaleLDS *sc) {
+    if (threadIdx.x < 10) sc->wstat[threadIdx.x] = 0;
+    __syncthreads();
+    const int i = threadIdx.x;
+    if (i < 16) {
+        lds_fmax(&sc->wstat[8], tile_stat(a.img + (size_t)(a.tHd + i) * KSLOT));
+    } else if (i < 16 + 7 * 32) {
+        const int L = 1 + (i - 16) / 32, t = (i - 16) % 32;
+        if (t < layer_kpad(L) / 16) lds_fmax(&sc->wstat[L], tile_stat(a.img + (size_t)(a.tL[L] + t * 8) * KSLOT));
+    }
+}
+
+// dOut -> dz rows Z_G (heads' dW) and the split G image, scaled by its max |dOut| per column tile
+template <int NQB, int NT>
+__device__ inline void stage_dout(const BwdArgs &a, h16x8 *lds, ScaleLDS *sc, float *stage, int p0, int tid) {
+    constexpr int BMB = 16 * NQB;
+    const Flags F = make_flags(a.flags);
+    if (tid < 32) (&sc->bsync[0][0])[tid] = 0;
+    for (int e = tid; e < 32 * BMB; e += NT) {
+        const int c = e / BMB, m = e % BMB;
+        const int p = p0 + m;
+        const float v = (p < a.N && c < F.nout) ? a.dout[(size_t)p * F.nout + c] : 0.f;
+        a.dz[(size_t)(Z_G + c) * a.Ns + p] = v;
+        stage[c * BM + m] = v;
+    }
+    __syncthreads();
+    for (int e = tid; e < 32 * BMB; e += NT) {
+        const int c = e / BMB, m = e % BMB;
+        lds_fmax(&sc->bsync[BS_G][qof(m)], fabsf(stage[c * BM + m]));
+    }
+    __syncthreads();
+    if (tid < 4) {
+        const float gmax = __uint_as_float(sc->bsync[BS_G][tid]);
+        sc->ksc[G_BG / 4][tid] = scale_for(gmax).inv;
+        sc->ain[0][tid] = gmax;
+    }
+    if (tid < 4 * BMB) {
+        const int g = tid / BMB, m = tid % BMB;
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = stage[(8 * g + j) * BM + m];
+        put_unit8(lds, G_BG + g, m, v, scale_for(__uint_as_float(sc->bsync[BS_G][qof(m)])).s);
+    }
+    lds_barrier();
+}
+
+// The output scales of a dX-chain step per column tile: max_cols sum |W| x max |dZ in| (the relu' mask
+// only zeroes), the same on every wave
+template <int NQB>
+__device__ inline void chain_scales(const ScaleLDS *sc, float ws, int par, int nw, float (&so)[NQB]) {
+#pragma unroll
+    for (int q = 0; q < NQB; q++) so[q] = ws * (par < 0 ? sc->ain[0][q] : amax_of(sc, par, nw, q));
+}
+
 // TE_ROWS: per-point dL/dt_emb (blender, t not frame-uniform); the other instantiation carries no
 // t_emb registers or code (raw t PE has no parameters upstream; uniform t: k_tgrad)
 template <bool TE_ROWS, int NQB>
-__device__ __forceinline__ void bwd_block(const BwdArgs &a, bf16x8 *lds, uint32_t *hwr, uint32_t *hrd, int p0, int slot) {
-    constexpr int BMB = 16 * NQB;  // points of this block (fwd_block)
+__device__ __forceinline__ void bwd_block(const BwdArgs &a, h16x8 *lds, uint32_t *hwr, uint32_t *hrd, ScaleLDS *sc,
+                                          int p0, int slot) {
     float *lf = reinterpret_cast<float *>(lds);
     float *stage = lf + G_BH * UG * 4;  // fp32 [32][BM] (H region, before the first dZ)
     // re-derived per block (opaque to loop-invariant hoisting): in the persistent loop, lane
@@ -1074,24 +1396,9 @@ __device__ __forceinline__ void bwd_block(const BwdArgs &a, bf16x8 *lds, uint32_
         hwr[tid] = 0;
         hrd[tid] = 0;
     }
-    // dOut -> dz rows Z_G (heads' dW) and the split G image
-    for (int e = tid; e < 32 * BMB; e += NTHR) {
-        const int c = e / BMB, m = e % BMB;
-        const int p = p0 + m;
-        const float v = (p < a.N && c < F.nout) ? a.dout[(size_t)p * F.nout + c] : 0.f;
-        a.dz[(size_t)(Z_G + c) * Ns + p] = v;
-        stage[c * BM + m] = v;
-    }
-    __syncthreads();
-    if (tid < 4 * BMB) {
-        const int g = tid / BMB, m = tid % BMB;
-        float v[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) v[j] = stage[(8 * g + j) * BM + m];
-        put_unit8(lds, G_BG + g, m, v);
-    }
-    lds_barrier();
+    stage_dout<NQB, NTHR>(a, lds, sc, stage, p0, tid);
     f32x4 c[NQB];
+    float ib[NQB];
     // The dZ chain runs without workgroup barriers (see k_fwd's trunk): step 0 (heads^T) and steps
     // i = 1..7 (layer L = 8 - i) each write dZ into H; step i reads H once both writers of each
     // k-step have signalled (hwr >= 2i) and overwrites its own k-step once all 16 waves have read
@@ -1100,51 +1407,91 @@ __device__ __forceinline__ void bwd_block(const BwdArgs &a, bf16x8 *lds, uint32_
     {
         uint32_t mk;
         zero_tiles(c);
-        gemm<1, NQB>(a.img + (size_t)(a.tHd + r) * KSLOT, lds, G_BG, 0, lane, c, trunk_pre(&mk, 7));
+        const h16x8 *Ah = a.img + (size_t)(a.tHd + r) * KSLOT;
+        gemm<1, NQB>(Ah, lds, G_BG, 0, lane, c, ib, sc->ksc, trunk_pre(&mk, 7));
+        scale_tiles(c, a_inv(Ah), ib);
         mask_apply(c, mk);
         tile16(a.dz, Ns, Z_L0 + 7 * 256 + 16 * r, p0, lane).store(c);
+        float so[NQB], my[NQB] = {};
+        chain_scales(sc, __uint_as_float(sc->wstat[8]), -1, 0, so);
+        col_absmax(c, my);
+        col_wave_max(my);
 #pragma unroll
-        for (int q = 0; q < NQB; q++) acc_to_lds(c[q], lds, G_BH, r, q, lane);
+        for (int q = 0; q < NQB; q++) {
+            const Scale s = scale_for(so[q]);
+            if (lane == 0) {
+                sc->amax[0][r][q] = my[q];
+                sc->ksc[G_BH / 4 + (r >> 1)][q] = s.inv;
+            }
+            acc_to_lds(c[q], lds, G_BH, r, q, lane, s.s);
+        }
         lds_signal(hwr + (r >> 1), lane);
     }
-    f32x4 te5[1] = {zero4()};  // t_emb tile of layer 5's dX (waves 0-7, TE_ROWS)
+    f32x4 te5[1] = {zero4()};  // t_emb tile of layer 5's dX (waves 0-7, TE_ROWS), true units
 #pragma unroll 1
     for (int L = 7; L >= 1; L--) {
         const uint32_t step = 8 - L;
         // dX_L = W_L^T dZ_L; the H-part rows of the padded L5 input are n-tiles F_H / 16 + r
-        if (TE_ROWS && L == 5 && r < 2 * NQB)  // t_emb rows (padded 64..95 = n-tiles 4, 5) x column tile r % NQB
-            gemm<8, 1>(a.img + (size_t)(a.tL[5] + (F_TE / 16 + r / NQB) * 8) * KSLOT, lds, G_BH, r % NQB, lane, te5,
-                       NoPre(), HGate{hwr, hrd, 0, 2u * step, false, lane});
+        if (TE_ROWS && L == 5 && r < 2 * NQB) {  // t_emb rows (padded 64..95 = n-tiles 4, 5) x column tile r % NQB
+            const h16x8 *At = a.img + (size_t)(a.tL[5] + (F_TE / 16 + r / NQB) * 8) * KSLOT;
+            float ib1[1];
+            gemm<8, 1>(At, lds, G_BH, r % NQB, lane, te5, ib1, sc->ksc, NoPre(), HGate{hwr, hrd, 0, 2u * step, false, lane});
+            te5[0] *= a_inv(At) * ib1[0];
+        }
         const int tile0 = (L == 5) ? F_H / 16 : 0;
         uint32_t mk;
         zero_tiles(c);
-        gemm<8, NQB>(a.img + (size_t)(a.tL[L] + (tile0 + r) * 8) * KSLOT, lds, G_BH, 0, lane, c,
-                    trunk_pre(&mk, L - 1), HGate{hwr, hrd, 0, 2u * step, true, lane});
+        const h16x8 *Aw = a.img + (size_t)(a.tL[L] + (tile0 + r) * 8) * KSLOT;
+        gemm<8, NQB>(Aw, lds, G_BH, 0, lane, c, ib, sc->ksc, trunk_pre(&mk, L - 1), HGate{hwr, hrd, 0, 2u * step, true, lane});
+        scale_tiles(c, a_inv(Aw), ib);
         mask_apply(c, mk);
 #ifndef DGS_DIAG_NOSAVE  // diagnostic only (wrong dW): the dZ chain's stores skipped
         tile16(a.dz, Ns, Z_L0 + (L - 1) * 256 + 16 * r, p0, lane).store(c);
 #endif
+        float so[NQB], my[NQB] = {};
+        chain_scales(sc, __uint_as_float(sc->wstat[L]), (step - 1) & 1, NWAVE, so);
+        col_absmax(c, my);
+        col_wave_max(my);
         lds_wait_ge(hrd + (r >> 1), 16u * step, lds_peek(hrd + (r >> 1)));
 #pragma unroll
-        for (int q = 0; q < NQB; q++) acc_to_lds(c[q], lds, G_BH, r, q, lane);
+        for (int q = 0; q < NQB; q++) {
+            const Scale s = scale_for(so[q]);
+            if (lane == 0) {
+                sc->amax[step & 1][r][q] = my[q];
+                sc->ksc[G_BH / 4 + (r >> 1)][q] = s.inv;
+            }
+            acc_to_lds(c[q], lds, G_BH, r, q, lane, s.s);
+        }
         lds_signal(hwr + (r >> 1), lane);
     }
     if (!TE_ROWS) return;
     // layer 0's t_emb rows added to layer 5's: dTE tile (n-tile r / NQB, column tile r % NQB) -> dz rows
-    // Z_TE (timenet.2's dW) and the split G image (dOut's, no longer read)
+    // Z_TE (timenet.2's dW) and the split G image (dOut's, no longer read), scaled by its column tile's max
     if (r < 2 * NQB) {
         const int nt = r / NQB, q = r % NQB;
-        gemm<8, 1>(a.img + (size_t)(a.tL[0] + (F_TE / 16 + nt) * 8) * KSLOT, lds, G_BH, q, lane, te5, NoPre(),
-                   HGate{hwr, hrd, 0, 16u, false, lane});
+        f32x4 t0[1] = {zero4()};
+        float ib1[1];
+        const h16x8 *At = a.img + (size_t)(a.tL[0] + (F_TE / 16 + nt) * 8) * KSLOT;
+        gemm<8, 1>(At, lds, G_BH, q, lane, t0, ib1, sc->ksc, NoPre(), HGate{hwr, hrd, 0, 16u, false, lane});
+        te5[0] += t0[0] * (a_inv(At) * ib1[0]);
         tile16(a.dz, Ns, Z_TE + 16 * nt, p0, lane).store(te5, q);
-        acc_to_lds(te5[0], lds, G_BG, nt, q, lane);
+        float tm[1] = {0.f};
+        col_absmax(te5, tm);
+        col_wave_max(tm);
+        if (lane == 0) lds_fmax(&sc->bsync[BS_GTE][q], tm[0]);
     }
+    lds_barrier();
+    if (r < 2 * NQB)
+        acc_to_lds(te5[0], lds, G_BG, r / NQB, r % NQB, lane, scale_for(__uint_as_float(sc->bsync[BS_GTE][r % NQB])).s);
+    if (tid < 4) sc->ksc[G_BG / 4][tid] = scale_for(__uint_as_float(sc->bsync[BS_GTE][tid])).inv;
     lds_barrier();
     // timenet.2^T: dTH = W_T2^T dTE (K = 32) -> mask TH -> dZ_T1
     {
         uint32_t mk;
         zero_tiles(c);
-        gemm<1, NQB>(a.img + (size_t)(a.tT2 + r) * KSLOT, lds, G_BG, 0, lane, c, MaskPre{&mk, mask_tile(MR_TH + r), lane});
+        const h16x8 *A2 = a.img + (size_t)(a.tT2 + r) * KSLOT;
+        gemm<1, NQB>(A2, lds, G_BG, 0, lane, c, ib, sc->ksc, MaskPre{&mk, mask_tile(MR_TH + r), lane});
+        scale_tiles(c, a_inv(A2), ib);
         mask_apply(c, mk);
         tile16(a.dz, Ns, Z_T1 + 16 * r, p0, lane).store(c);
     }
@@ -1152,7 +1499,7 @@ __device__ __forceinline__ void bwd_block(const BwdArgs &a, bf16x8 *lds, uint32_
 
 // The dX chain for a frame-uniform t (TE_ROWS = false: every training step) as 8 waves of two n-tiles
 // (k_bwd8, as k_fwd8): wave w writes dZ rows 32w .. 32w + 31 = H k-step w (one writer per k-step and
-// step, 8 readers). Same arithmetic, layouts and outputs as bwd_block<false, NQB>.
+// step, 8 readers). Same arithmetic, scales, layouts and outputs as bwd_block<false, NQB>.
 struct MaskPre32x2 {
     uint32_t *mk;              // [2]
     const uint32_t *word;      // n-tile 2w's word row; 2w + 1's is 64 words on
@@ -1163,8 +1510,8 @@ struct MaskPre32x2 {
     }
 };
 template <int NQB>
-__device__ __forceinline__ void bwd_block8(const BwdArgs &a, bf16x8 *lds, uint32_t *hwr, uint32_t *hrd, int p0, int slot) {
-    constexpr int BMB = 16 * NQB;
+__device__ __forceinline__ void bwd_block8(const BwdArgs &a, h16x8 *lds, uint32_t *hwr, uint32_t *hrd, ScaleLDS *sc,
+                                           int p0, int slot) {
     float *lf = reinterpret_cast<float *>(lds);
     float *stage = lf + G_BH * UG * 4;
     int tid = threadIdx.x;
@@ -1181,38 +1528,43 @@ __device__ __forceinline__ void bwd_block8(const BwdArgs &a, bf16x8 *lds, uint32
         hwr[tid] = 0;
         hrd[tid] = 0;
     }
-    for (int e = tid; e < 32 * BMB; e += NTHR8) {  // dOut -> dz rows Z_G and the split G image
-        const int c = e / BMB, m = e % BMB;
-        const int p = p0 + m;
-        const float v = (p < a.N && c < F.nout) ? a.dout[(size_t)p * F.nout + c] : 0.f;
-        a.dz[(size_t)(Z_G + c) * Ns + p] = v;
-        stage[c * BM + m] = v;
-    }
-    __syncthreads();
-    if (tid < 4 * BMB) {
-        const int g = tid / BMB, m = tid % BMB;
-        float v[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) v[j] = stage[(8 * g + j) * BM + m];
-        put_unit8(lds, G_BG + g, m, v);
-    }
-    lds_barrier();
+    stage_dout<NQB, NTHR8>(a, lds, sc, stage, p0, tid);
     f32x4 c[2][NQB];
+    float ib[NQB];
+    // one chain step's epilogue: scale, relu' mask, dz stores, output scales, hand-off
+    auto epilogue = [&](const h16x8 *Aw, int astride, const uint32_t (&mk)[2], int zrow, float ws, int par_in,
+                        uint32_t step) {
+        float my[NQB] = {};
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+            scale_tiles(c[t], a_inv(Aw + t * astride), ib);
+            mask_apply(c[t], mk[t]);
+            tile16(a.dz, Ns, zrow + 16 * (2 * w + t), p0, lane).store(c[t]);
+            col_absmax(c[t], my);
+        }
+        float so[NQB];
+        chain_scales(sc, ws, par_in, NW8, so);
+        col_wave_max(my);
+        if (step > 0) lds_wait_ge(hrd + w, (uint32_t)NW8 * step, lds_peek(hrd + w));
+#pragma unroll
+        for (int q = 0; q < NQB; q++) {
+            const Scale s = scale_for(so[q]);
+            if (lane == 0) {
+                sc->amax[step & 1][w][q] = my[q];
+                sc->ksc[G_BH / 4 + w][q] = s.inv;
+            }
+#pragma unroll
+            for (int t = 0; t < 2; t++) acc_to_lds(c[t][q], lds, G_BH, 2 * w + t, q, lane, s.s);
+        }
+        lds_signal(hwr + w, lane);
+    };
     {  // heads^T: dH7 = W_h^T dOut (K = 32 from G) -> mask H7 -> dZ7
         uint32_t mk[2];
 #pragma unroll
         for (int t = 0; t < 2; t++) zero_tiles(c[t]);
-        gemm2<1, NQB>(a.img + (size_t)(a.tHd + 2 * w) * KSLOT, KSLOT, lds, G_BG, 0, lane, c, trunk_pre(mk, 7));
-#pragma unroll
-        for (int t = 0; t < 2; t++) {
-            mask_apply(c[t], mk[t]);
-            tile16(a.dz, Ns, Z_L0 + 7 * 256 + 16 * (2 * w + t), p0, lane).store(c[t]);
-        }
-#pragma unroll
-        for (int t = 0; t < 2; t++)
-#pragma unroll
-            for (int q = 0; q < NQB; q++) acc_to_lds(c[t][q], lds, G_BH, 2 * w + t, q, lane);
-        lds_signal(hwr + w, lane);
+        const h16x8 *Ah = a.img + (size_t)(a.tHd + 2 * w) * KSLOT;
+        gemm2<1, NQB>(Ah, KSLOT, lds, G_BG, 0, lane, c, ib, sc->ksc, trunk_pre(mk, 7));
+        epilogue(Ah, KSLOT, mk, Z_L0 + 7 * 256, __uint_as_float(sc->wstat[8]), -1, 0u);
     }
 #pragma unroll 1
     for (int L = 7; L >= 1; L--) {
@@ -1221,31 +1573,24 @@ __device__ __forceinline__ void bwd_block8(const BwdArgs &a, bf16x8 *lds, uint32
         uint32_t mk[2];
 #pragma unroll
         for (int t = 0; t < 2; t++) zero_tiles(c[t]);
-        gemm2<8, NQB>(a.img + (size_t)(a.tL[L] + (tile0 + 2 * w) * 8) * KSLOT, 8 * KSLOT, lds, G_BH, 0, lane, c,
-                      trunk_pre(mk, L - 1), HGate{hwr, hrd, 0, step, true, lane});
-#pragma unroll
-        for (int t = 0; t < 2; t++) {
-            mask_apply(c[t], mk[t]);
-            tile16(a.dz, Ns, Z_L0 + (L - 1) * 256 + 16 * (2 * w + t), p0, lane).store(c[t]);
-        }
-        lds_wait_ge(hrd + w, (uint32_t)NW8 * step, lds_peek(hrd + w));
-#pragma unroll
-        for (int t = 0; t < 2; t++)
-#pragma unroll
-            for (int q = 0; q < NQB; q++) acc_to_lds(c[t][q], lds, G_BH, 2 * w + t, q, lane);
-        lds_signal(hwr + w, lane);
+        const h16x8 *Aw = a.img + (size_t)(a.tL[L] + (tile0 + 2 * w) * 8) * KSLOT;
+        gemm2<8, NQB>(Aw, 8 * KSLOT, lds, G_BH, 0, lane, c, ib, sc->ksc, trunk_pre(mk, L - 1),
+                      HGate{hwr, hrd, 0, step, true, lane});
+        epilogue(Aw, 8 * KSLOT, mk, Z_L0 + (L - 1) * 256, __uint_as_float(sc->wstat[L]), (int)((step - 1) & 1), step);
     }
 }
 
 __global__ __launch_bounds__(NTHR8) void k_bwd8(BwdArgs a) {
-    __shared__ bf16x8 lds[G_BWD * UG];
+    __shared__ h16x8 lds[G_BWD * UG];
     __shared__ uint32_t hwr[8], hrd[8];
     __shared__ int s_next;
+    __shared__ ScaleLDS sc;
+    load_wstats_bwd(a, &sc);
     for (int b = blockIdx.x;;) {
         int nx = 0;
         if (a.queue && threadIdx.x == 0) nx = queue_take(a.queue);
-        if (b < a.nfull) bwd_block8<NQ>(a, lds, hwr, hrd, b * BM, b);
-        else bwd_block8<1>(a, lds, hwr, hrd, a.nfull * BM + (b - a.nfull) * 16, b);
+        if (b < a.nfull) bwd_block8<NQ>(a, lds, hwr, hrd, &sc, b * BM, b);
+        else bwd_block8<1>(a, lds, hwr, hrd, &sc, a.nfull * BM + (b - a.nfull) * 16, b);
         if (!a.queue) break;
         if (threadIdx.x == 0) s_next = nx;
         __syncthreads();
@@ -1257,15 +1602,17 @@ __global__ __launch_bounds__(NTHR8) void k_bwd8(BwdArgs a) {
 
 template <bool TE_ROWS>
 __global__ __launch_bounds__(NTHR) void k_bwd(BwdArgs a) {
-    __shared__ bf16x8 lds[G_BWD * UG];
+    __shared__ h16x8 lds[G_BWD * UG];
     __shared__ uint32_t hwr[8], hrd[8];  // dZ hand-off counters (HGate), as in k_fwd's trunk
     __shared__ int s_next;
+    __shared__ ScaleLDS sc;
+    load_wstats_bwd(a, &sc);
     CLK_BEGIN();
     for (int b = blockIdx.x;;) {  // persistent: as k_fwd
         int nx = 0;
         if (a.queue && threadIdx.x == 0) nx = queue_take(a.queue);
-        if (b < a.nfull) bwd_block<TE_ROWS, NQ>(a, lds, hwr, hrd, b * BM, b);
-        else bwd_block<TE_ROWS, 1>(a, lds, hwr, hrd, a.nfull * BM + (b - a.nfull) * 16, b);
+        if (b < a.nfull) bwd_block<TE_ROWS, NQ>(a, lds, hwr, hrd, &sc, b * BM, b);
+        else bwd_block<TE_ROWS, 1>(a, lds, hwr, hrd, &sc, a.nfull * BM + (b - a.nfull) * 16, b);
         if (!a.queue) break;
         if (threadIdx.x == 0) s_next = nx;
         __syncthreads();
@@ -1357,409 +1704,41 @@ __global__ __launch_bounds__(1024) void k_tgrad(TGradArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// dW = dZ X^T over all points (split-N): operands staged fp32 -> split bf16 planes in LDS, 16 points
-// (one bf16 k-step) per chunk, double-buffered; per-workgroup slabs reduced by k_dw_reduce (mlp.hip)
-// ------------------------------------------------------------------------------------------------
-constexpr int PC = 16;                 // points per chunk = one k-step
-constexpr int PITCH = 24;              // bf16 per LDS row: 16 + 8 pad (48 B: conflict-free b128 reads)
-constexpr int PLANE = WT * PITCH;      // bf16 per split plane
-constexpr int OPND = NSPLIT * PLANE;   // bf16 per operand
-constexpr int DW_LDS = 2 * 2 * OPND * 2;  // bytes: 2 buffers x (A, B)
-constexpr int DW_THREADS = 512;
-static_assert(DW_LDS <= 160 * 1024, "dW LDS");
-
-#define MFMA32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
-
-// the six split products into one 32x32 accumulator, smallest first
-__device__ inline void mma6_1(const AFrag &a, const AFrag &b, f32x16 &c) {
-    c = MFMA32(a.m, b.m, c);
-    c = MFMA32(a.h, b.l, c);
-    c = MFMA32(a.l, b.h, c);
-    c = MFMA32(a.h, b.m, c);
-    c = MFMA32(a.m, b.h, c);
-    c = MFMA32(a.h, b.h, c);
-}
-
-__device__ inline AFrag load_plane_frag(const __bf16 *op, int row, int h) {
-    const __bf16 *p = op + row * PITCH + 8 * h;
-    return AFrag{*reinterpret_cast<const bf16x8 *>(p), *reinterpret_cast<const bf16x8 *>(p + PLANE),
-                 *reinterpret_cast<const bf16x8 *>(p + 2 * PLANE)};
-}
-
-// one float4 (row, 4 points) -> the three planes
-__device__ inline void stage_split(__bf16 *op, int row, int col4, float4 v) {
-    const Split4 s = split4(v.x, v.y, v.z, v.w);
-    bf16x4 *p = reinterpret_cast<bf16x4 *>(op + row * PITCH + 4 * col4);
-    p[0] = s.h;
-    p[PLANE / 4] = s.m;
-    p[2 * PLANE / 4] = s.l;
-}
-
-__device__ inline float4 zsel4(float4 v, bool ok) {
-    return make_float4(ok ? v.x : 0.f, ok ? v.y : 0.f, ok ? v.z : 0.f, ok ? v.w : 0.f);
-}
-
-template <bool NARROW>
-__device__ __forceinline__ void dw_tile(const WJob &J, size_t Ns, const float *__restrict__ dz,
-                                        const float *__restrict__ saved, float *__restrict__ slabs, __bf16 *lds) {
-    const int split = blockIdx.x - J.block0;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wn = wave >> 2, wk = wave & 3;  // wide wave tile: rows [128 wn, +128), cols [64 wk, +64)
-    const int h = lane >> 5, i = lane & 31;
-    const int nch = (int)(Ns / PC);
-    const int per = div_up(nch, J.nsplit);
-    const int c0 = split * per;
-    const int c1 = min(nch, c0 + per);
-    // staging: float4 q = tid + 512 j (j < 2): row = q / 4 (0..255), points 4 (q % 4) .. +3
-    const int srow = tid >> 2, scol = tid & 3;
-    const float *baseA = dz + (size_t)J.zrow * Ns;
-    const float *baseB = saved + (size_t)J.xrow * Ns;
-    const bool okA0 = srow < J.nrows, okA1 = srow + 128 < J.nrows;
-    const bool okB0 = srow < J.krows, okB1 = srow + 128 < J.krows;
-    // 32-bit byte offsets from a uniform base; rows past the extent load row 0 (always valid) and are
-    // zeroed at the LDS store, so the loads stay in flight across the chunk's MFMAs
-    const uint32_t ns = (uint32_t)Ns;
-    const uint32_t uA0 = ((okA0 ? srow : 0) * ns + 4 * scol) * 4, uA1 = ((okA1 ? srow + 128 : 0) * ns + 4 * scol) * 4;
-    const uint32_t uB0 = ((okB0 ? srow : 0) * ns + 4 * scol) * 4, uB1 = ((okB1 ? srow + 128 : 0) * ns + 4 * scol) * 4;
-#define DW_LD(base, u, c) \
-    (*reinterpret_cast<const float4 *>(reinterpret_cast<const char *>(base) + (uint32_t)((u) + (uint32_t)(c) * (PC * 4u))))
-    struct Stage {
-        float4 a0, a1, b0, b1;
-    };
-    float bs0 = 0.f, bs1 = 0.f;  // bias row sums of the staged dZ rows
-    auto gload = [&](Stage &r, int c) {
-        r.a0 = DW_LD(baseA, uA0, c);
-        r.a1 = DW_LD(baseA, uA1, c);
-        r.b0 = DW_LD(baseB, uB0, c);
-        r.b1 = DW_LD(baseB, uB1, c);
-    };
-    auto lstore = [&](const Stage &r, int buf) {
-        __bf16 *A = lds + buf * 2 * OPND;
-        __bf16 *B = A + OPND;
-        const float4 a0 = zsel4(r.a0, okA0), a1 = zsel4(r.a1, okA1);
-        bs0 += (a0.x + a0.y) + (a0.z + a0.w);
-        bs1 += (a1.x + a1.y) + (a1.z + a1.w);
-        stage_split(A, srow, scol, a0);
-        stage_split(A, srow + 128, scol, a1);
-        stage_split(B, srow, scol, zsel4(r.b0, okB0));
-        stage_split(B, srow + 128, scol, zsel4(r.b1, okB1));
-    };
-#undef DW_LD
-    // this wave's active sub-tiles (wave-uniform). wide: rows 128 wn + 32 t, cols 64 wk + 32 u
-    // (acc[t][u]); narrow: rows 32 wave, cols 32 v (acc[v >> 1][v & 1], v < 4)
-    const int nact_r = NARROW ? (32 * wave < J.nrows ? 1 : 0) : min(4, max(0, div_up(J.nrows - 128 * wn, 32)));
-    const int nact_c = NARROW ? min(4, div_up(J.krows, 32)) : min(2, max(0, div_up(J.krows - 64 * wk, 32)));
-    const bool any = nact_r > 0 && nact_c > 0;
-    f32x16 acc[4][2];
-#pragma unroll
-    for (int t = 0; t < 4; t++)
-#pragma unroll
-        for (int u = 0; u < 2; u++)
-#pragma unroll
-            for (int r = 0; r < 16; r++) acc[t][u][r] = 0.f;
-    auto compute = [&](int buf) {
-        const __bf16 *A = lds + buf * 2 * OPND;
-        const __bf16 *B = A + OPND;
-        if (any && NARROW) {
-            const AFrag a0 = load_plane_frag(A, 32 * wave + i, h);
-#pragma unroll
-            for (int v = 0; v < 4; v++) {
-                if (v >= nact_c) continue;
-                const AFrag b = load_plane_frag(B, 32 * v + i, h);
-                mma6_1(a0, b, acc[v >> 1][v & 1]);
-            }
-        } else if (any) {
-            AFrag bb[2];
-#pragma unroll
-            for (int u = 0; u < 2; u++) bb[u] = load_plane_frag(B, 64 * wk + 32 * u + i, h);
-#pragma unroll
-            for (int t = 0; t < 4; t++) {
-                if (t >= nact_r) continue;
-                const AFrag at = load_plane_frag(A, 128 * wn + 32 * t + i, h);
-#pragma unroll
-                for (int u = 0; u < 2; u++) {
-                    if (u >= nact_c) continue;
-                    mma6_1(at, bb[u], acc[t][u]);
-                }
-            }
-        }
-    };
-    // Pipeline: LDS buffers alternate per chunk; two register stages keep the global loads two chunks
-    // ahead. Barriers wait for LDS only (lds_barrier): a __syncthreads() would also drain the
-    // prefetched global loads (vmcnt 0) every 48 MFMAs.
-    Stage R0, R1;
-    if (c0 < c1) gload(R0, c0);
-    if (c0 + 1 < c1) gload(R1, c0 + 1);
-    if (c0 < c1) lstore(R0, 0);
-    if (c0 + 2 < c1) gload(R0, c0 + 2);
-    lds_barrier();
-    for (int c = c0; c < c1; c += 2) {
-        // buffer 0 holds chunk c, R1 chunk c + 1, R0 chunk c + 2 (in flight)
-        compute(0);
-        if (c + 1 < c1) lstore(R1, 1);
-        if (c + 3 < c1) gload(R1, c + 3);
-        lds_barrier();
-        if (c + 1 >= c1) break;
-        compute(1);
-        if (c + 2 < c1) lstore(R0, 0);
-        if (c + 4 < c1) gload(R0, c + 4);
-        lds_barrier();
-    }
-    float *slab = slabs + (size_t)blockIdx.x * SLAB;
-    // bias row sums: the 4 lanes staging a row hold its partial sums (fixed xor-tree order)
-    bs0 += __shfl_xor(bs0, 1);
-    bs0 += __shfl_xor(bs0, 2);
-    bs1 += __shfl_xor(bs1, 1);
-    bs1 += __shfl_xor(bs1, 2);
-    if (scol == 0) {
-        slab[WT * WT + srow] = bs0;
-        slab[WT * WT + srow + 128] = bs1;
-    }
-    // rows past nrows / cols past krows hold zeros or partial garbage that k_dw_reduce never reads
-    if (NARROW) {
-#pragma unroll
-        for (int v = 0; v < 4; v++) {
-            const int nb = 32 * wave, kb = 32 * v;
-#pragma unroll
-            for (int r = 0; r < 16; r++) slab[(nb + TileAddr::row(r) + 4 * h) * WT + kb + i] = acc[v >> 1][v & 1][r];
-        }
-        return;
-    }
-#pragma unroll
-    for (int t = 0; t < 4; t++)
-#pragma unroll
-        for (int u = 0; u < 2; u++) {
-            const int nb = 128 * wn + 32 * t, kb = 64 * wk + 32 * u;
-#pragma unroll
-            for (int r = 0; r < 16; r++) slab[(nb + TileAddr::row(r) + 4 * h) * WT + kb + i] = acc[t][u][r];
-        }
-}
-
-__global__ __launch_bounds__(DW_THREADS) void k_dw(WJobs JT, size_t Ns, const float *__restrict__ dz,
-                                                   const float *__restrict__ saved, float *__restrict__ slabs) {
-    extern __shared__ bf16x8 dw_lds[];
-    // job of this workgroup: static-index selects over the kernel-argument table (no scratch copy)
-    WJob J = JT.j[0];
-#pragma unroll
-    for (int q = 1; q < MAXJ; q++)
-        if (q < JT.n && (int)blockIdx.x >= JT.j[q].block0) J = JT.j[q];
-    // the two wave layouts are separate code regions (one loop with a runtime switch spills)
-    if (J.narrow)
-        dw_tile<true>(J, Ns, dz, saved, slabs, reinterpret_cast<__bf16 *>(dw_lds));
-    else
-        dw_tile<false>(J, Ns, dz, saved, slabs, reinterpret_cast<__bf16 *>(dw_lds));
-}
-
-// ------------------------------------------------------------------------------------------------
-// dW = dZ X^T on split bf16 with LDS-DMA staging (k_dwg). The fp32 dZ / X rows stream global ->
-// LDS through global_load_lds_dwordx4 (no VGPR staging, no staging VALU, no lock-step store
-// phase): 32 points (two 16-point k-steps) per chunk, two buffers, ONE barrier per chunk, the next
-// chunk's DMA in flight during this chunk's MFMAs. Each wave splits its fp32 fragments in registers
-// right before its MFMAs. Same job plan, slab layout and k_dw_reduce as the fp32 k_dw.
-//   Numerics: each k-step's six split products go into a fresh accumulator T (C = 0) added to the
-// running sum in fp32 (RNE): tools/mfma_accum_probe.hip measured this as more accurate than the fp32
-// fma chain at K = 4096 (one running C loses the low bits of the small terms with a bias).
-//   LDS image per operand and buffer: 16-B units (4 points of one row) [s][rb][q][i]: k-step s (2),
-//   32-row block rb (8), point quad q (4), row i (32). One DMA wave-instruction fills the 1 KiB of
-//   (s, rb, q pair) lane-linearly (lane l -> q = 2 qp + (l >> 5), i = l & 31); a 32x32x16 fragment
-//   (lane (i, h): row i, points 8h..8h+7) is two conflict-free ds_read_b128 (units q = 2h, 2h + 1).
-// ------------------------------------------------------------------------------------------------
-constexpr int GPC = 32;                 // points per chunk
-constexpr int G_OPND = 2 * 8 * 4 * 32;  // 16-B units per operand and buffer
-constexpr int G_BUF = 2 * G_OPND;       // units per buffer (dZ, X)
-constexpr int G_LDS = 2 * G_BUF * 16;   // bytes (128 KiB)
-static_assert(G_LDS <= 160 * 1024, "dWg LDS");
-
-__device__ __forceinline__ constexpr int g_unit(int s, int rb, int q, int i) { return ((s * 8 + rb) * 4 + q) * 32 + i; }
-
-// 8 fp32 (one row, points 8h .. 8h + 7) -> the hi / mid / lo bf16 fragments
-__device__ __forceinline__ AFrag split8(const float4 &a, const float4 &b) {
-    uint32_t h[4], m[4], l[4];
-    split2(a.x, a.y, h[0], m[0], l[0]);
-    split2(a.z, a.w, h[1], m[1], l[1]);
-    split2(b.x, b.y, h[2], m[2], l[2]);
-    split2(b.z, b.w, h[3], m[3], l[3]);
-    return AFrag{__builtin_bit_cast(bf16x8, make_uint4(h[0], h[1], h[2], h[3])),
-                 __builtin_bit_cast(bf16x8, make_uint4(m[0], m[1], m[2], m[3])),
-                 __builtin_bit_cast(bf16x8, make_uint4(l[0], l[1], l[2], l[3]))};
-}
-
-__device__ __forceinline__ float sum8(const float4 &a, const float4 &b) {
-    return ((a.x + a.y) + (a.z + a.w)) + ((b.x + b.y) + (b.z + b.w));
-}
-
-// one k-step's six split products into a fresh T, then acc += T in fp32
-__device__ __forceinline__ void mma6_fresh(const AFrag &a, const AFrag &b, f32x16 &acc) {
-    f32x16 t = MFMA32(a.m, b.m, (f32x16)(0.f));
-    t = MFMA32(a.h, b.l, t);
-    t = MFMA32(a.l, b.h, t);
-    t = MFMA32(a.h, b.m, t);
-    t = MFMA32(a.m, b.h, t);
-    t = MFMA32(a.h, b.h, t);
-    acc += t;
-}
-
-typedef __attribute__((address_space(1))) void *gptr_t;
-typedef __attribute__((address_space(3))) void *lptr_t;
-
-template <bool NARROW>
-__device__ __forceinline__ void dwg_tile(const WJob &J, size_t Ns, const float *__restrict__ dz,
-                                         const float *__restrict__ saved, float *__restrict__ slabs, float4 *lds) {
-    const int split = blockIdx.x - J.block0;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wn = wave >> 2, wk = wave & 3;
-    const int h = lane >> 5, i = lane & 31;
-    const int nch = (int)(Ns / GPC);
-    const int per = div_up(nch, J.nsplit);
-    const int c0 = split * per;
-    const int c1 = min(nch, c0 + per);
-    // this wave's 8 DMA instructions per chunk: d = 8 wave + j -> operand d >> 5 (waves 0-3 dZ,
-    // 4-7 X), k-step, row block and quad pair of the 1 KiB they fill (all wave-uniform but the lane
-    // offset). Row blocks past the job's extent are not loaded; the rows of a partial block past it
-    // are in bounds (every job's rows rounded up to 32 lie inside saved / dZ, mlp_shared.h row maps)
-    // and only feed outputs k_dw_reduce never reads.
-    const int op = wave >> 2;
-    const float *obase = op ? saved + (size_t)J.xrow * Ns : dz + (size_t)J.zrow * Ns;
-    const int ext = op ? J.krows : J.nrows;
-    // buffer form: lane offset in one VGPR, row-block offset in an SGPR, chunk base in the
-    // descriptor (the host keeps 256 rows x Ns x 4 B below 2^31)
-    const uint32_t lane_off = (uint32_t)((i * Ns + 4 * h) * 4);
-    auto issue = [&](int c, int buf) {
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<float *>(obase + (size_t)c * GPC), 0, 0x7fffffff, 0x00020000);
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const int e = (8 * wave + j) & 31;
-            const int s = e >> 4, rb = (e >> 1) & 7, qp = e & 1;
-            if (rb * 32 < ext)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                    rs, (lptr_t)(lds + buf * G_BUF + op * G_OPND + g_unit(s, rb, 2 * qp, 0)), 16, lane_off,
-                    (uint32_t)((rb * 32 * Ns + s * 16 + 8 * qp) * 4), 0, 0);
-        }
-    };
-    const int nact_r = NARROW ? (32 * wave < J.nrows ? 1 : 0) : min(4, max(0, div_up(J.nrows - 128 * wn, 32)));
-    const int nact_c = NARROW ? min(4, div_up(J.krows, 32)) : min(2, max(0, div_up(J.krows - 64 * wk, 32)));
-    const bool any = nact_r > 0 && nact_c > 0;
-    f32x16 acc[4][2];
-#pragma unroll
-    for (int t = 0; t < 4; t++)
-#pragma unroll
-        for (int u = 0; u < 2; u++)
-#pragma unroll
-            for (int r = 0; r < 16; r++) acc[t][u][r] = 0.f;
-    float bs[4] = {0.f, 0.f, 0.f, 0.f};  // bias row sums of this lane's dZ rows (fixed order)
-    const bool bias_wave = NARROW || wk == 0;
-    if (c0 < c1) issue(c0, 0);
-    for (int c = c0; c < c1; c++) {
-        const int buf = (c - c0) & 1;
-        // this wave's DMAs of chunk c have landed; after the barrier everyone's have, and every wave
-        // is done reading the other buffer (chunk c - 1), which the next DMAs overwrite
-        __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) expcnt(7) lgkmcnt(0)
-        __builtin_amdgcn_s_barrier();
-        if (c + 1 < c1) issue(c + 1, buf ^ 1);
-        if (!any) continue;
-        const float4 *A = lds + buf * G_BUF;
-        const float4 *B = A + G_OPND;
-#pragma unroll
-        for (int s = 0; s < 2; s++) {
-            if (NARROW) {
-                const float4 a0 = A[g_unit(s, wave, 2 * h, i)], a1 = A[g_unit(s, wave, 2 * h + 1, i)];
-                bs[0] += sum8(a0, a1);
-                const AFrag at = split8(a0, a1);
-#pragma unroll
-                for (int v = 0; v < 4; v++) {
-                    if (v >= nact_c) continue;
-                    const AFrag b = split8(B[g_unit(s, v, 2 * h, i)], B[g_unit(s, v, 2 * h + 1, i)]);
-                    mma6_fresh(at, b, acc[v >> 1][v & 1]);
-                }
-            } else {
-                AFrag bb[2];
-#pragma unroll
-                for (int u = 0; u < 2; u++)
-                    if (u < nact_c) bb[u] = split8(B[g_unit(s, 2 * wk + u, 2 * h, i)], B[g_unit(s, 2 * wk + u, 2 * h + 1, i)]);
-#pragma unroll
-                for (int t = 0; t < 4; t++) {
-                    if (t >= nact_r) continue;
-                    const float4 a0 = A[g_unit(s, 4 * wn + t, 2 * h, i)], a1 = A[g_unit(s, 4 * wn + t, 2 * h + 1, i)];
-                    if (bias_wave) bs[t] += sum8(a0, a1);
-                    const AFrag at = split8(a0, a1);
-#pragma unroll
-                    for (int u = 0; u < 2; u++) {
-                        if (u >= nact_c) continue;
-                        mma6_fresh(at, bb[u], acc[t][u]);
-                    }
-                }
-            }
-        }
-    }
-    float *slab = slabs + (size_t)blockIdx.x * SLAB;
-    // rows past nrows / cols past krows hold garbage that k_dw_reduce never reads
-    if (NARROW) {
-        const float v0 = bs[0] + __shfl_xor(bs[0], 32);
-        if (h == 0) slab[WT * WT + 32 * wave + i] = v0;
-#pragma unroll
-        for (int v = 0; v < 4; v++) {
-            const int nb = 32 * wave, kb = 32 * v;
-#pragma unroll
-            for (int r = 0; r < 16; r++) slab[(nb + TileAddr::row(r) + 4 * h) * WT + kb + i] = acc[v >> 1][v & 1][r];
-        }
-        return;
-    }
-    if (bias_wave) {
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-            const float v = bs[t] + __shfl_xor(bs[t], 32);
-            if (h == 0) slab[WT * WT + 128 * wn + 32 * t + i] = v;
-        }
-    }
-#pragma unroll
-    for (int t = 0; t < 4; t++)
-#pragma unroll
-        for (int u = 0; u < 2; u++) {
-            const int nb = 128 * wn + 32 * t, kb = 64 * wk + 32 * u;
-#pragma unroll
-            for (int r = 0; r < 16; r++) slab[(nb + TileAddr::row(r) + 4 * h) * WT + kb + i] = acc[t][u][r];
-        }
-}
-
-__global__ __launch_bounds__(DW_THREADS) void k_dwg(WJobs JT, size_t Ns, const float *__restrict__ dz,
-                                                    const float *__restrict__ saved, float *__restrict__ slabs) {
-    extern __shared__ float4 dwg_lds[];
-    WJob J = JT.j[0];
-#pragma unroll
-    for (int q = 1; q < MAXJ; q++)
-        if (q < JT.n && (int)blockIdx.x >= JT.j[q].block0) J = JT.j[q];
-    if (J.narrow)
-        dwg_tile<true>(J, Ns, dz, saved, slabs, dwg_lds);
-    else
-        dwg_tile<false>(J, Ns, dz, saved, slabs, dwg_lds);
-}
-
-// ------------------------------------------------------------------------------------------------
-// dW = dZ X^T on split bf16 (k_dws, the default dW). Per job tile (<= 256 dZ rows x 256 X rows) and
-// 32-point chunk, each wave owns 32 rows of ONE operand ("private": loaded, split and kept as MFMA
-// fragments in its own registers) against all rows of the other ("shared": staged by the whole
-// workgroup, split once, through LDS):
-//   COL (krows = 256 jobs): private = X rows 32 w..+31 (B fragments), shared = dZ rows (A, NS tiles)
-//   ROW (krows <= 96 jobs): private = dZ rows 32 w..+31 (A fragments), shared = X rows (B, NS tiles)
+// dW = dZ X^T on split f16 (k_dws, the default dW). Per job tile (<= 256 dZ rows x 256 X rows) and
+// 32-point chunk, each wave owns 32 rows of ONE operand ("private": loaded, scaled, split and kept as
+// MFMA fragments in its own registers) against all rows of the other ("shared": staged by the whole
+// workgroup, scaled and split once, through LDS):
+//   COL (krows = 256 jobs): private = X rows 32 w..+31, shared = dZ rows (NS tiles)
+//   ROW (krows <= 96 jobs): private = dZ rows 32 w..+31, shared = X rows (NS tiles)
 // so every fp32 value is split exactly once per workgroup and only the shared operand makes the LDS
-// round trip (k_dwg split each fragment in every wave reading it; k_dw split once but through LDS
-// for both operands). Per chunk: split the private registers -> fragments | MFMAs on LDS buffer c & 1
-// with the next chunk's shared split (3 ds_write_b64 per float4) and loads interleaved | ONE barrier.
+// round trip. The private fragments are always the A operand and the shared ones B (the 32x32x16 A and
+// B lane maps are the same): a tile's MFMA output is [private row][shared row], lane i holding shared
+// row i. Per chunk: split the private registers -> fragments | MFMAs on LDS buffer c & 1 with the next
+// chunk's shared split (2 ds_write_b64 per float4) and loads interleaved | ONE barrier.
+//   Scales (power of two, as the forward): the private operand one per (wave, chunk) from the wave's
+// max over its 32 rows x 32 points; the shared operand one per (row, chunk) from the 8 lanes that stage
+// the row (3 DPP steps), kept in LDS beside the planes. Lane i of a tile's output then carries ONE
+// inverse scale (private x shared row i), applied when the chunk's fresh accumulator T joins the
+// running sum: acc = T * s + acc (one fma per element, where the bf16x6 split had one add).
 //   LDS: split planes in fragment order, unit (16 B) [split][k-step][32-row block][lane = 32 h + i]
-//   (row i, points 8h..8h+7): a fragment is one conflict-free ds_read_b128 per split; 2 x 48 KiB.
-//   Numerics: each tile's twelve products of a chunk (per k-step the five corrections, then hh) go
-//   into a fresh accumulator T, added to the running sum in fp32 (tools/mfma_accum_probe.hip: a
-//   long running MFMA C loses the low bits of small terms with a bias; within one chunk's T that
-//   loss stays below fp32's own rounding of T).
+//   (row i, points 8h..8h+7): a fragment is one conflict-free ds_read_b128 per split; 2 x 32 KiB.
+//   Numerics: each tile's six products of a chunk (per k-step the two corrections, then hh) go into a
+// fresh accumulator T, added to the running sum in fp32 (tools/mfma_accum_probe.hip: a long running
+// MFMA C loses the low bits of small terms with a bias; within one chunk's T that loss stays below
+// fp32's own rounding of T).
+//   Output: ROW jobs' tiles are [dZ row][X row] (the slab's own layout, stored as before); COL jobs'
+// are [X row][dZ row] and go through a per-wave LDS transpose so the slab stores stay coalesced.
 // Same job plan, slab layout and k_dw_reduce as the fp32 k_dw.
 // ------------------------------------------------------------------------------------------------
+constexpr int DW_THREADS = 512;
 constexpr int S_UNITS = NSPLIT * 2 * 8 * 64;  // 16-B units per chunk buffer
 constexpr int S_NBUF = 2;
-constexpr int S_LDS = S_NBUF * S_UNITS * 16;  // bytes (96 / 144 KiB)
-static_assert(S_LDS <= 160 * 1024, "dWs LDS");
+constexpr int S_RSC = WT;                     // shared-row inverse scales per buffer (floats)
+constexpr int S_LDS = S_NBUF * S_UNITS * 16 + S_NBUF * S_RSC * 4;  // bytes (66 KiB)
+constexpr int S_TRP = 32 * 33;                // per-wave transpose scratch (floats), after the loop
+static_assert(S_LDS <= 160 * 1024 && 8 * S_TRP * 4 <= S_LDS, "dWs LDS");
+
+#define MFMA32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_f16((a), (b), (c), 0, 0, 0)
 
 // unit of (split p, k-step ks, row block rb, point half hh, row i): each 32-unit half is rotated
 // by 4 ks + 2 hh, so the row-major staging stores (8 lanes per row: all (ks, hh, 8-byte half)
@@ -1769,27 +1748,50 @@ __device__ __forceinline__ constexpr int s_unit(int p, int ks, int rb, int hh, i
     return ((p * 2 + ks) * 8 + rb) * 64 + 32 * hh + ((i + 4 * ks + 2 * hh) & 31);
 }
 
-__device__ __forceinline__ AFrag s_frag(const bf16x8 *L, int ks, int rb, int lane) {
+__device__ __forceinline__ AFrag s_frag(const h16x8 *L, int ks, int rb, int lane) {
     const int hh = lane >> 5, i = lane & 31;
-    return AFrag{L[s_unit(0, ks, rb, hh, i)], L[s_unit(1, ks, rb, hh, i)], L[s_unit(2, ks, rb, hh, i)]};
+    return AFrag{L[s_unit(0, ks, rb, hh, i)], L[s_unit(1, ks, rb, hh, i)]};
 }
 
-// one k-step's six products into t (the five corrections first)
-__device__ __forceinline__ f32x16 mma6_into(const AFrag &a, const AFrag &b, f32x16 t) {
-    t = MFMA32(a.m, b.m, t);
-    t = MFMA32(a.h, b.l, t);
+// 8 fp32 (one row, points 8h .. 8h + 7) times S -> the hi / lo f16 fragments
+__device__ __forceinline__ AFrag split8(const float4 &a, const float4 &b, float S) {
+    uint32_t h[4], l[4];
+    hsplit2(a.x * S, a.y * S, h[0], l[0]);
+    hsplit2(a.z * S, a.w * S, h[1], l[1]);
+    hsplit2(b.x * S, b.y * S, h[2], l[2]);
+    hsplit2(b.z * S, b.w * S, h[3], l[3]);
+    return AFrag{__builtin_bit_cast(h16x8, make_uint4(h[0], h[1], h[2], h[3])),
+                 __builtin_bit_cast(h16x8, make_uint4(l[0], l[1], l[2], l[3]))};
+}
+
+__device__ __forceinline__ float sum8(const float4 &a, const float4 &b) {
+    return ((a.x + a.y) + (a.z + a.w)) + ((b.x + b.y) + (b.z + b.w));
+}
+
+__device__ __forceinline__ float absmax4(const float4 &v) {
+    return fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+}
+
+// one k-step's three products into t (the two corrections first)
+__device__ __forceinline__ f32x16 mma3_into(const AFrag &a, const AFrag &b, f32x16 t) {
     t = MFMA32(a.l, b.h, t);
-    t = MFMA32(a.h, b.m, t);
-    t = MFMA32(a.m, b.h, t);
+    t = MFMA32(a.h, b.l, t);
     return MFMA32(a.h, b.h, t);
 }
 
-// acc += t (v_pk_add_f32 or v_add_f32: measured alike here)
-__device__ __forceinline__ void add16(f32x16 &acc, const f32x16 &t) { acc += t; }
+// max over the 8 consecutive lanes (aligned groups) of non-negative floats, in every lane of the group:
+// quad_perm [1,0,3,2], [2,3,0,1], then row_half_mirror
+__device__ __forceinline__ float max8(float v) {
+    uint32_t x = __float_as_uint(v);
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xb1, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4e, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xf, 0xf, false));
+    return __uint_as_float(x);
+}
 
 template <bool COL, int NS>
 __device__ __forceinline__ void dws_run(const WJob &J, size_t Ns, const float *__restrict__ dz,
-                                        const float *__restrict__ saved, float *__restrict__ slabs, bf16x8 *lds) {
+                                        const float *__restrict__ saved, float *__restrict__ slabs, h16x8 *lds) {
     constexpr int SROWS = 32 * NS;                   // shared rows staged per chunk
     constexpr int NSF = (SROWS * 8 + 511) / 512;     // staged float4 per thread per chunk
     const int split = blockIdx.x - J.block0;
@@ -1811,12 +1813,11 @@ __device__ __forceinline__ void dws_run(const WJob &J, size_t Ns, const float *_
     // private: lane (i, h) holds row 32 w + i, points 8 h .. + 7 of each k-step (fragment layout)
     const int pvoff = ((32 * wave + i) * (int)Ns + 8 * h) * 4;
     float4 pr[4];  // [k-step][half]
-#define DWS_C(c) (c)
     auto pload = [&](int c) {
 #pragma unroll
         for (int q = 0; q < 4; q++)
             pr[q] = __builtin_bit_cast(float4,
-                                       __builtin_amdgcn_raw_buffer_load_b128(rsP, pvoff, DWS_C(c) * 128 + (q >> 1) * 64 + (q & 1) * 16, 0));
+                                       __builtin_amdgcn_raw_buffer_load_b128(rsP, pvoff, c * 128 + (q >> 1) * 64 + (q & 1) * 16, 0));
     };
     // shared staging: slot g = tid + 512 f -> row g >> 3, points 4 (g & 7) .. + 3 of the chunk (8
     // lanes read a row's 128 B)
@@ -1833,24 +1834,31 @@ __device__ __forceinline__ void dws_run(const WJob &J, size_t Ns, const float *_
             int row, q;
             if (sslot(f, row, q))
                 st[f] = __builtin_bit_cast(
-                    float4, __builtin_amdgcn_raw_buffer_load_b128(rsS, (row * (int)Ns + 4 * q) * 4, DWS_C(c) * 128, 0));
+                    float4, __builtin_amdgcn_raw_buffer_load_b128(rsS, (row * (int)Ns + 4 * q) * 4, c * 128, 0));
         }
     };
     float bsum[NSF] = {};  // COL: bias row sums of the staged dZ rows; ROW: bsum[0] of the private row
     char *lb = reinterpret_cast<char *>(lds);
+    float *rsc = reinterpret_cast<float *>(lb + S_NBUF * S_UNITS * 16);  // [buffer][row]
     // `live`: the staged chunk is a real one (the last chunk re-splits a stale copy into the buffer
     // nobody reads again; it must not count in the bias sums)
     auto sput = [&](int f, int buf, bool live) {
         int row, q;
-        if (!sslot(f, row, q)) return;
+        const bool ok = sslot(f, row, q);
         const float4 v = st[f];
+        // the row's scale: max over its 8 staging lanes (a partial last slot group lies in one wave, past
+        // the valid rows: its lanes see zeros, never a valid row's)
+        const Scale s = scale_for(max8(ok ? absmax4(v) : 0.f));
+        if (!ok) return;
         if (COL) bsum[f] += live ? (v.x + v.y) + (v.z + v.w) : 0.f;
-        const Split4 s = split4(v.x, v.y, v.z, v.w);
+        const Split4 sp = split4(v.x, v.y, v.z, v.w, s.s);
         char *p = lb + buf * (S_UNITS * 16) +
                   s_unit(0, q >> 2, row >> 5, (q >> 1) & 1, row & 31) * 16 + 8 * (q & 1);
-        *reinterpret_cast<bf16x4 *>(p) = s.h;
-        *reinterpret_cast<bf16x4 *>(p + 2 * 8 * 64 * 16) = s.m;
-        *reinterpret_cast<bf16x4 *>(p + 2 * 2 * 8 * 64 * 16) = s.l;
+        *reinterpret_cast<h16x4 *>(p) = sp.h;
+        *reinterpret_cast<h16x4 *>(p + 2 * 8 * 64 * 16) = sp.l;
+        // the row's 8 lanes store the same value (a `q == 0` branch here split the block and cost 72
+        // VGPRs of spills)
+        rsc[buf * S_RSC + row] = s.inv;
     };
     f32x16 acc[NS];
 #pragma unroll
@@ -1871,21 +1879,26 @@ __device__ __forceinline__ void dws_run(const WJob &J, size_t Ns, const float *_
     auto put_at = [](int f) { return (f * NH) / NSF; };
     auto chunk = [&](int c, auto BUFC) {
         constexpr int buf = decltype(BUFC)::value;
-        const bf16x8 *L = lds + buf * S_UNITS;
+        const h16x8 *L = lds + buf * S_UNITS;
         const bool more = c + 1 < c1;
         if (pact) {
-            // private fragments of this chunk, then the private loads of the next (in flight for
-            // the whole chunk)
-            AFrag pf0 = split8(pr[0], pr[1]), pf1 = split8(pr[2], pr[3]);
+            // private fragments of this chunk (scaled by the wave's max), then the private loads of
+            // the next (in flight for the whole chunk)
+            const float pm = wave_max(fmaxf(fmaxf(absmax4(pr[0]), absmax4(pr[1])), fmaxf(absmax4(pr[2]), absmax4(pr[3]))));
+            const Scale sp = scale_for(pm);
+            AFrag pf0 = split8(pr[0], pr[1], sp.s), pf1 = split8(pr[2], pr[3], sp.s);
             if (!COL) bsum[0] += sum8(pr[0], pr[1]) + sum8(pr[2], pr[3]);
             pload(min(c + 1, c1 - 1));
 #pragma unroll
             for (int s = 0; s < NS; s++) {
                 // the tile's two k-steps into a fresh accumulator, one shared fragment live at a time
+                const float si = sp.inv * rsc[buf * S_RSC + 32 * s + i];
                 const AFrag s0 = s_frag(L, 0, s, lane);
-                f32x16 T = COL ? mma6_into(s0, pf0, (f32x16)(0.f)) : mma6_into(pf0, s0, (f32x16)(0.f));
+                f32x16 T = mma3_into(pf0, s0, (f32x16)(0.f));
                 const AFrag s1 = s_frag(L, 1, s, lane);
-                add16(acc[s], COL ? mma6_into(s1, pf1, T) : mma6_into(pf1, s1, T));
+                T = mma3_into(pf1, s1, T);
+#pragma unroll
+                for (int r = 0; r < 16; r++) acc[s][r] = fmaf(T[r], si, acc[s][r]);
 #pragma unroll
                 for (int f = 0; f < NSF; f++)
                     if (put_at(f) == s) sput(f, buf ^ 1, more);
@@ -1921,17 +1934,36 @@ __device__ __forceinline__ void dws_run(const WJob &J, size_t Ns, const float *_
     }
     if (!pact) return;
     // rows past nrows / cols past krows hold zeros that k_dw_reduce never reads
+    if (!COL) {
+#pragma unroll
+        for (int s = 0; s < NS; s++) {
+            const int nb = 32 * wave, kb = 32 * s;
+#pragma unroll
+            for (int r = 0; r < 16; r++) slab[(nb + TileAddr::row(r) + 4 * h) * WT + kb + i] = acc[s][r];
+        }
+        return;
+    }
+    // COL: tile s is [X row 32 w + row(r) + 4 h][dZ row 32 s + i]; through this wave's LDS scratch so
+    // that 32 lanes store 32 consecutive X rows of one dZ row (the last chunk's barrier ended every
+    // wave's reads of the planes)
+    float *tp = reinterpret_cast<float *>(lds) + wave * S_TRP;
 #pragma unroll
     for (int s = 0; s < NS; s++) {
-        const int nb = COL ? 32 * s : 32 * wave, kb = COL ? 32 * wave : 32 * s;
 #pragma unroll
-        for (int r = 0; r < 16; r++) slab[(nb + TileAddr::row(r) + 4 * h) * WT + kb + i] = acc[s][r];
+        for (int r = 0; r < 16; r++) tp[i * 33 + TileAddr::row(r) + 4 * h] = acc[s][r];
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS writes before its reads
+#pragma unroll
+        for (int rr = 0; rr < 16; rr++) {
+            const int m = 2 * rr + h;  // dZ row 32 s + m, X rows 32 w + i
+            slab[(32 * s + m) * WT + 32 * wave + i] = tp[m * 33 + i];
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // the reads done before the next tile's writes
     }
 }
 
 __global__ __launch_bounds__(DW_THREADS) void k_dws(WJobs JT, size_t Ns, const float *__restrict__ dz,
                                                     const float *__restrict__ saved, float *__restrict__ slabs) {
-    extern __shared__ bf16x8 dws_lds[];
+    extern __shared__ h16x8 dws_lds[];
     WJob J = JT.j[0];
 #pragma unroll
     for (int q = 1; q < MAXJ; q++)
@@ -1981,6 +2013,7 @@ struct Plan : Params {
     int bT1 = -1, bT2 = -1, bL[8], bHd, wT1 = -1, wT2 = -1;     // fp32 offsets
     int w0te = -1, w5te = -1;                                    // fp32 t_emb columns of linear.0 / .5
     int nslots = 0, nf32 = 0;
+    std::vector<int> units;  // k_pack's workgroups: (first k-slot, k-slots) of every 16-row n-tile
     size_t img_floats() const { return (size_t)nslots * KSLOT * 4; }  // 16-B unit = 4 floats
     size_t total() const { return img_floats() + nf32; }
 };
@@ -2056,35 +2089,89 @@ Plan make_plan(int flags) {
         r0 += P.hrows[h];
     }
     P.nf32 = (P.nf32 + 3) & ~3;
+    // one pack workgroup per n-tile of every image region (its scale and row statistics span the tile's
+    // whole K): the region list is fixed by the flags
+    auto region = [&](int slot0, int ntiles, int nk) {
+        for (int t = 0; t < ntiles; t++) {
+            P.units.push_back(slot0 + t * nk);
+            P.units.push_back(nk);
+        }
+    };
+    if (F.blender) {
+        region(P.fT1, 16, 1);
+        region(P.fT2, 2, 8);
+        region(P.tT2, 16, 1);
+    }
+    for (int i = 0; i < 8; i++) {
+        region(P.fL[i], 16, layer_kpad_f(F, i) / 32);
+        region(P.tL[i], layer_kpad(i) / 16, 8);
+    }
+    region(P.fHd, 1, 8);
+    region(P.tHd, 16, 1);
     return P;
 }
 
-// Packing is one gather + split launch over map[i] = (parameter << 22) | element, or -1 for zero
-// padding: i < nslots * 512 are the A-image elements in [k-slot][lane][8] order (each split into
-// three bf16 planes of its k-slot), the rest the fp32 region. The map depends only on the flags
-// (built once on the host, cached on the device).
+// Packing is one gather + scale + split launch over map[i] = (parameter << 22) | element, or -1 for
+// zero padding: i < nslots * 512 are the A-image elements in [k-slot][lane][8] order, the rest the
+// fp32 region. The map depends only on the flags (built once on the host, cached on the device).
+// Workgroup b < nunits packs one 16-row n-tile (its k-slots slot0 .. slot0 + nk - 1): the tile's max
+// |w| sets its power-of-two scale S (scale_for), each element x is stored as hi = f16(S x) and lo =
+// f16(S x - hi) in the slot's first two planes, and the third plane of the tile's first slot holds
+// [1 / S, max over the tile's 16 rows of sum_k |w|] (the output-scale bounds of the forward / dX
+// kernels); the other workgroups copy the fp32 region.
 constexpr int PACK_MAXP = 32;
 constexpr int PACK_SHIFT = 22;
 struct PackPtrs {
     const float *p[PACK_MAXP];
 };
 
-__global__ __launch_bounds__(256) void k_pack(const int *__restrict__ map, PackPtrs src, __bf16 *__restrict__ img,
-                                              float *__restrict__ fp, int nimg, int total) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= total) return;
-    const int c = map[i];
-    const float v = c < 0 ? 0.f : src.p[c >> PACK_SHIFT][c & ((1 << PACK_SHIFT) - 1)];
-    if (i < nimg) {
-        const __bf16 hb = (__bf16)v;
-        const float r = v - (float)hb;
-        const __bf16 mb = (__bf16)r;
-        __bf16 *d = img + (size_t)(i >> 9) * 1536 + (i & 511);  // k-slot: 3 planes of 512 bf16
-        d[0] = hb;
-        d[512] = mb;
-        d[1024] = (__bf16)(r - (float)mb);
-    } else {
-        fp[i - nimg] = v;
+__global__ __launch_bounds__(512) void k_pack(const int *__restrict__ map, PackPtrs src, const int2 *__restrict__ units,
+                                              int nunits, _Float16 *__restrict__ img, float *__restrict__ fp, int nimg,
+                                              int nf32) {
+    __shared__ float s_rs[4][16];
+    __shared__ uint32_t s_max;
+    const int b = blockIdx.x, tid = threadIdx.x;
+    auto gather = [&](int i) {
+        const int c = map[i];
+        return c < 0 ? 0.f : src.p[c >> PACK_SHIFT][c & ((1 << PACK_SHIFT) - 1)];
+    };
+    if (b >= nunits) {
+        const int j = (b - nunits) * 512 + tid;
+        if (j < nf32) fp[j] = gather(nimg + j);
+        return;
+    }
+    const int2 u = units[b];  // (first k-slot, k-slots)
+    if (tid == 0) s_max = 0;
+    // element tid of a slot: lane l = tid >> 3 holds row l & 15 of the tile (v_mfma_f32_16x16x32_f16 A map)
+    float am = 0.f, rs = 0.f;
+    for (int k = 0; k < u.y; k++) {
+        const float v = fabsf(gather((u.x + k) * 512 + tid));
+        am = fmaxf(am, v);
+        rs += v;
+    }
+    rs += __shfl_xor(rs, 1);  // the 8 elements of a lane (tid bits 0-2): same row
+    rs += __shfl_xor(rs, 2);
+    rs += __shfl_xor(rs, 4);
+    __syncthreads();
+    am = wave_max(am);
+    if ((tid & 63) == 0) lds_fmax(&s_max, am);
+    if ((tid & 7) == 0) s_rs[tid >> 7][(tid >> 3) & 15] = rs;  // tid bits 7-8: the four k quarters
+    __syncthreads();
+    const Scale S = scale_for(__uint_as_float(s_max));
+    for (int k = 0; k < u.y; k++) {
+        const float x = gather((u.x + k) * 512 + tid) * S.s;
+        const _Float16 hi = (_Float16)x;
+        const _Float16 lo = (_Float16)(x - (float)hi);
+        _Float16 *d = img + (size_t)(u.x + k) * 1536 + tid;  // k-slot: hi, lo, scale plane of 512 f16
+        d[0] = hi;
+        d[512] = lo;
+    }
+    if (tid == 0) {
+        float m = 0.f;
+        for (int r = 0; r < 16; r++) m = fmaxf(m, (s_rs[0][r] + s_rs[1][r]) + (s_rs[2][r] + s_rs[3][r]));
+        float *t = reinterpret_cast<float *>(img + (size_t)u.x * 1536 + 1024);
+        t[0] = S.inv;
+        t[1] = m;
     }
 }
 
@@ -2119,6 +2206,7 @@ static std::vector<int> build_pack_map(const Plan &P) {
 
 static std::mutex g_map_mu;
 static std::map<std::pair<int, int>, int *> g_pack_maps;  // (device, flags) -> device map
+static std::map<std::pair<int, int>, int2 *> g_pack_units;  // (device, flags) -> n-tile table
 
 static int *pack_map_for(const Plan &P, int flags) {
     int dev = 0;
@@ -2134,6 +2222,23 @@ static int *pack_map_for(const Plan &P, int flags) {
         return nullptr;
     }
     g_pack_maps[{dev, flags}] = d;
+    return d;
+}
+
+static const int2 *pack_units_for(const Plan &P, int flags) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(g_map_mu);
+    auto it = g_pack_units.find({dev, flags});
+    if (it != g_pack_units.end()) return it->second;
+    int2 *d = nullptr;
+    const size_t bytes = P.units.size() * sizeof(int);
+    if (hipMalloc(&d, bytes) != hipSuccess) return nullptr;
+    if (hipMemcpy(d, P.units.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(d);
+        return nullptr;
+    }
+    g_pack_units[{dev, flags}] = d;
     return d;
 }
 
@@ -2156,8 +2261,7 @@ static WPlan split_wplan(const Flags &F, int target = 256) {
     }();
     return make_wplan(F, target, 1.5, 4.0, model ? nullptr : kDwsShapeCost);
 }
-static int dw_split(const Flags &F, size_t Ns, const float *dz, const float *saved, float *slabs, float *const *grads,
-                    hipStream_t stream);
+
 
 static size_t padded_points(int N) { return (size_t)div_up(N, BM) * BM; }
 
@@ -2261,19 +2365,16 @@ size_t saved_floats(int flags, int N) {
     return (size_t)F.nsaved * Ns + mask_words(F, Ns) + TC_FLOATS;
 }
 
-// dW arithmetic (DGS_MLP_SPLIT_DW): 3 (default) = the split-bf16 k_dws (private / shared operands,
-// every value split once), 2 = the split-bf16 k_dwg (LDS-DMA staged, per-wave splits), 1 = the
-// split-bf16 k_dw (VGPR staged, split phase), 0 = the fp32-input MFMA k_dw of mlp.hip, all on the
-// same [rows][Ns] arrays
+// dW arithmetic (DGS_MLP_SPLIT_DW): 3 (default) = the split-f16 k_dws (private / shared operands, every
+// value split once), 0 = the fp32-input MFMA k_dw of mlp.hip, both on the same [rows][Ns] arrays (the
+// bf16 k_dw / k_dwg variants, modes 1 and 2, were removed with the bf16x6 arithmetic in round 6)
 static int dw_mode() {
     static const int m = [] {
         const char *e = getenv("DGS_MLP_SPLIT_DW");
-        return (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 3;
+        return (e && e[0] == '0') ? 0 : 3;
     }();
     return m;
 }
-static int dw_glds(const Flags &F, size_t Ns, const float *dz, const float *saved, float *slabs, float *const *grads,
-                   hipStream_t stream);
 static int dw_split_once(const Flags &F, size_t Ns, const float *dz, const float *saved, float *slabs,
                          float *const *grads, hipStream_t stream);
 
@@ -2298,13 +2399,14 @@ int pack(int flags, const float *const *params, float *packed, hipStream_t strea
         src.p[k] = params[k];
     }
     const int *map = pack_map_for(P, flags);
-    if (!map) {
+    const int2 *units = pack_units_for(P, flags);
+    if (!map || !units) {
         set_error("dgs_deform_pack: could not allocate the pack map");
         return DGS_ERR_HIP;
     }
-    const int nimg = P.nslots * 512, total = nimg + P.nf32;
-    hipLaunchKernelGGL(k_pack, dim3(div_up(total, 256)), dim3(256), 0, stream, map, src,
-                       reinterpret_cast<__bf16 *>(packed), packed + P.img_floats(), nimg, total);
+    const int nimg = P.nslots * 512, nunits = (int)P.units.size() / 2;
+    hipLaunchKernelGGL(k_pack, dim3(nunits + div_up(P.nf32, 512)), dim3(512), 0, stream, map, src, units, nunits,
+                       reinterpret_cast<_Float16 *>(packed), packed + P.img_floats(), nimg, P.nf32);
     DGS_LAUNCH_CHECK("k_pack", false, stream);
     return DGS_OK;
 }
@@ -2364,7 +2466,7 @@ static void fwd_args(const Plan &P, int flags, int N, const float *xyz, const fl
     a.N = N;
     a.Ns = padded_points(N);
     a.xyz = xyz; a.t = t; a.out = out; a.saved = saved;
-    a.img = reinterpret_cast<const bf16x8 *>(packed);
+    a.img = reinterpret_cast<const h16x8 *>(packed);
     a.fp = packed + P.img_floats();
     a.mask = saved ? reinterpret_cast<uint32_t *>(saved + (size_t)P.F.nsaved * a.Ns) : nullptr;
     a.fT1 = P.fT1; a.fT2 = P.fT2; a.fHd = P.fHd;
@@ -2391,7 +2493,7 @@ int backward(int flags, int N, const float *packed, const float *saved, const fl
     float *slabs = scratch + (size_t)F.nz * Ns;
     BwdArgs b{};
     b.N = N; b.Ns = Ns; b.dout = dout; b.dz = dz;
-    b.img = reinterpret_cast<const bf16x8 *>(packed);
+    b.img = reinterpret_cast<const h16x8 *>(packed);
     b.mask = reinterpret_cast<const uint32_t *>(saved + (size_t)F.nsaved * Ns);
     b.tHd = P.tHd; b.tT2 = P.tT2;
     for (int i = 0; i < 8; i++) b.tL[i] = P.tL[i];
@@ -2422,16 +2524,8 @@ int backward(int flags, int N, const float *packed, const float *saved, const fl
     }
     DGS_LAUNCH_CHECK("k_bwd", false, stream);
     int rc;
-    if (F.uniform_t && (dw_mode() == 1 || dw_mode() == 2)) {  // A/B variants predate the folded t_emb jobs
-        set_error("dgs_deform_backward: DGS_MLP_SPLIT_DW=1/2 do not support a uniform t (folded t_emb)");
-        return DGS_ERR_ARGS;
-    }
     if (dw_mode() == 0)
         rc = mlp::dw_fp32(F, Ns, dz, saved, slabs, grads, stream);
-    else if (dw_mode() == 1)
-        rc = dw_split(F, Ns, dz, saved, slabs, grads, stream);
-    else if (dw_mode() == 2)
-        rc = dw_glds(F, Ns, dz, saved, slabs, grads, stream);
     else
         rc = dw_split_once(F, Ns, dz, saved, slabs, grads, stream);
     if (rc != DGS_OK || !F.uniform_t) return rc;
@@ -2449,19 +2543,6 @@ int backward(int flags, int N, const float *packed, const float *saved, const fl
     }
     DGS_LAUNCH_CHECK("k_tgrad", false, stream);
     return DGS_OK;
-}
-
-static int dw_split(const Flags &F, size_t Ns, const float *dz, const float *saved, float *slabs, float *const *grads,
-                    hipStream_t stream) {
-    const WPlan W = split_wplan(F);
-    {
-        // 144 KiB dynamic LDS: the attribute is per device, set once per (kernel, device)
-        if (int rc = ensure_dynamic_lds((const void *)k_dw, DW_LDS)) return rc;
-        ScopedTimer tm("mlp_dw", stream);
-        hipLaunchKernelGGL(k_dw, dim3(W.nblocks), dim3(DW_THREADS), DW_LDS, stream, W.jobs, Ns, dz, saved, slabs);
-    }
-    DGS_LAUNCH_CHECK("k_dw", false, stream);
-    return launch_dw_reduce(F, W, slabs, grads, stream);
 }
 
 static int dw_split_once(const Flags &F, size_t Ns, const float *dz, const float *saved, float *slabs,
@@ -2484,21 +2565,6 @@ static int dw_split_once(const Flags &F, size_t Ns, const float *dz, const float
         hipLaunchKernelGGL(k_dws, dim3(W.nblocks), dim3(DW_THREADS), S_LDS, stream, W.jobs, Ns, dz, saved, slabs);
     }
     DGS_LAUNCH_CHECK("k_dws", false, stream);
-    return launch_dw_reduce(F, W, slabs, grads, stream);
-}
-
-static int dw_glds(const Flags &F, size_t Ns, const float *dz, const float *saved, float *slabs, float *const *grads,
-                   hipStream_t stream) {
-    if ((size_t)WT * Ns * 4 >= 0x7fffffffull)  // buffer offsets of a 256-row tile must fit 31 bits
-        return mlp::dw_fp32(F, Ns, dz, saved, slabs, grads, stream);
-    const WPlan W = split_wplan(F);
-    {
-        // 128 KiB dynamic LDS: the attribute is per device, set once per (kernel, device)
-        if (int rc = ensure_dynamic_lds((const void *)k_dwg, G_LDS)) return rc;
-        ScopedTimer tm("mlp_dw", stream);
-        hipLaunchKernelGGL(k_dwg, dim3(W.nblocks), dim3(DW_THREADS), G_LDS, stream, W.jobs, Ns, dz, saved, slabs);
-    }
-    DGS_LAUNCH_CHECK("k_dwg", false, stream);
     return launch_dw_reduce(F, W, slabs, grads, stream);
 }
 

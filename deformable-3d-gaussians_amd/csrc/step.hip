@@ -66,7 +66,7 @@ extern "C" int dgs_train_step(const dgs_train_step_args *a, int *overflowed, int
             DGS_LAUNCH_CHECK("k_fill_scalar", false, stream);
             t = a->t_full;
         }
-        // pack + forward (the timenet inside the pack launch)
+        // pack + forward (k_pack, k_timenet, the forward: mlp_split.hip pack_forward)
         if (int rc = dgs_deform_pack_forward(flags, a->mlp_params, P, a->xyz, t, a->mlp_packed, a->mlp_out,
                                              a->mlp_saved, stream))
             return rc;

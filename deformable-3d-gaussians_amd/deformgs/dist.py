@@ -19,12 +19,15 @@ def init_from_env(backend=None):
     # DGS_DIST_BACKEND=gloo replaces RCCL (which refuses two ranks on one GPU)
     local = int(os.environ.get("DGS_DEVICE", local))
     backend = backend or os.environ.get("DGS_DIST_BACKEND") or None
+    from .train_step import reset_agreement
+    reset_agreement()  # a new group re-agrees on the native-vs-autograd path (train_step)
     if world > 1 and not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
             torch.cuda.set_device(local)
-            reserve_cus_for_collectives()
+            if os.environ.get("DGS_OVERLAP_RESERVE", "0") == "1":
+                reserve_cus_for_collectives()
             dist.init_process_group(backend, device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
@@ -39,7 +42,9 @@ def init_from_env(backend=None):
 # CUs it held) and +0.01-0.03 ms with 16 or 32 reserved for 16 or 32 stand-in workgroups, while the
 # reserve itself cost the step 0-2.5 % (tools/overlap_probe.py --sweep --wide,
 # profiles/r5c_overlap_sweep.jsonl; the collective queued after the network backward instead: +0.08-0.2
-# ms). RCCL itself cannot run on a one-GPU box, so its real workgroup count is capped, not measured.
+# ms). RCCL itself cannot run on a one-GPU box, so its real workgroup count and its bandwidth under the
+# channel cap are unmeasured: the reserve is OPT-IN (DGS_OVERLAP_RESERVE=1) until an 8-GPU run measures
+# it, so the default data-parallel step uses every CU and RCCL's own channel count.
 OVERLAP_CUS = 32
 
 

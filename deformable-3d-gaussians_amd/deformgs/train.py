@@ -44,7 +44,7 @@ from .dist import OverflowAgreement, OverlappedGradAllReduce, rank_identical_gen
 from .general import get_linear_noise_func
 from .loss import l1_loss, psnr, ssim
 from .renderer import render, set_fused
-from .train_step import optimizer_step, train_step
+from .train_step import optimizer_step, reset_agreement, train_step
 
 
 def build_viewpoint_stack(cameras, sequence_length):
@@ -108,6 +108,7 @@ def training(dataset, opt, pipe, testing_iterations, saving_iterations, scene, g
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
     set_fused(fused)
+    reset_agreement()  # this run agrees on its own native-vs-autograd path (train_step)
     try:
         torch_adam = None if fused else torch.optim.Adam
         gaussians.row_select = None if fused else (lambda mask, ts: [t[mask] for t in ts])

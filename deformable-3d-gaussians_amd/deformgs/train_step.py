@@ -111,20 +111,30 @@ def train_step(gaussians, deform, cam, gt_image, pipe, background, is_6dof=False
 _AGREED = {"key": None, "native": None}
 
 
+def reset_agreement():
+    """Forget the agreed native-vs-autograd choice: called when a process group or a training run
+    starts (dist.init_from_env, train.training), so a later run never reuses a decision taken under
+    another group or model."""
+    _AGREED["key"] = _AGREED["native"] = None
+
+
 def agreed_native_path(local, gaussians, deform, pipe, gt_image, is_6dof, group=None):
     """The native-vs-autograd choice of a data-parallel step, the same on every rank (the two paths
     issue different collectives: ranks split between them would hang in RCCL or fail in gloo).
 
     The ranks MIN-reduce their local `native_step.usable` flag whenever a RANK-INVARIANT key changes —
-    the Gaussian count, the image size, the network's configuration, the pipe / renderer switches —
-    so every rank issues that 1-int collective at the same step; between such changes the agreed
-    choice is reused with no collective. A rank that cannot take an agreed native path without a
-    key change (a condition only it sees, e.g. a misaligned parameter) raises instead of issuing
-    mismatched collectives; a rank that could but the others cannot simply takes the autograd path."""
+    the process group, the Gaussian count, the network's configuration, the pipe / renderer switches,
+    the SH layout — so every rank issues that 1-int collective at the same step; between such changes
+    the agreed choice is reused with no collective. The image size is NOT part of the key: each rank
+    renders its own camera, and the reference's readers allow a different width / height per camera
+    (scene/dataset_readers.py:113-114), so it can change on one rank and not on the others; usable()
+    does not depend on it. A rank that cannot take an agreed native path without a key change (a
+    condition only it sees, e.g. a misaligned parameter) raises; the other ranks then block in their next
+    collective until the backend's timeout (no process-group abort is attempted). A rank that could but
+    the others cannot simply takes the autograd path."""
     from .renderer import _FUSED, _HONOR_OVERRIDE, _SPLIT_SH
     net = deform.deform
-    H, W = (int(gt_image.shape[-2]), int(gt_image.shape[-1])) if gt_image.dim() >= 2 else (0, 0)
-    key = (int(gaussians._xyz.shape[0]), H, W, bool(is_6dof), getattr(net, "flags", None),
+    key = (id(group), int(gaussians._xyz.shape[0]), bool(is_6dof), getattr(net, "flags", None),
            bool(getattr(net, "exact_fp32", False)), native_step.enabled(), bool(_FUSED["on"]), bool(_SPLIT_SH),
            bool(_HONOR_OVERRIDE["on"]), bool(getattr(pipe, "compute_cov3D_python", False)),
            bool(getattr(pipe, "convert_SHs_python", False)), bool(getattr(pipe, "debug", False)),
@@ -137,7 +147,8 @@ def agreed_native_path(local, gaussians, deform, pipe, gt_image, is_6dof, group=
     if _AGREED["native"] and not local:
         raise RuntimeError(f"rank {dist.get_rank()}: the native training step is not usable on this rank while the "
                            "ranks agreed on it (a rank-local condition changed without a change of the Gaussian "
-                           "count / image size / configuration): the ranks' collectives would not match")
+                           "count / configuration): the ranks' collectives would not match; the other ranks "
+                           "block in their next collective until the backend's timeout")
     return _AGREED["native"]
 
 

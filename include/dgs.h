@@ -149,7 +149,8 @@ int dgs_raster_get_deterministic(void);
 /* Rect binning order: 1 (default; DGS_TILE_SORT=0 turns it off) = the Gaussians are binned in index order
  * and each tile's list is then sorted by (depth, index) in its own workgroup (k_tile_sort); 0 = a global
  * stable depth sort first (4 radix passes), lists placed in that order. The lists are identical either
- * way. The deterministic backward uses the global order (it re-walks the placement). Applies to forwards
+ * way. The deterministic backward keeps the per-tile sort: k_tile_sort also writes each sorted entry's
+ * index-order position, where the backward stores the pair's sums for k_rect_gather. Applies to forwards
  * issued after the call. */
 void dgs_debug_set_tile_sort(int on);
 int dgs_debug_get_tile_sort(void);
@@ -229,9 +230,8 @@ int dgs_deform_pack(int flags, const float *const *params, float *packed, void *
  * t: (N,1) per-point time. saved may be NULL for inference (no backward). */
 int dgs_deform_forward(int flags, int N, const float *xyz, const float *t, const float *packed,
                        float *out, float *saved, void *stream);
-/* dgs_deform_pack + dgs_deform_forward in one call (the training step's order): with a uniform t, the
- * blender network and saved activations the timenet runs inside the pack launch (one launch fewer);
- * results bitwise equal to the two calls. */
+/* dgs_deform_pack + dgs_deform_forward in one call (the training step's order): the same launches as the
+ * two calls (pack, then k_timenet and the forward), results bitwise equal. */
 int dgs_deform_pack_forward(int flags, const float *const *params, int N, const float *xyz, const float *t,
                             float *packed, float *out, float *saved, void *stream);
 /* dout: (N, n_out). grads: device pointers in the same order as params (overwritten).

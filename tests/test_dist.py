@@ -411,6 +411,14 @@ def _path_agreement_case(rank, world):
     ts.train_step(gs, deform, None, gt, types.SimpleNamespace(), None, deferred_count=False, allreduce=AR())
     out.append(list(calls))
     calls.clear()
+    # each rank renders its own camera, whose size may change on one rank only (the reference's
+    # readers allow a per-camera width / height): not a key change, so no lone 1-int collective that
+    # would pair with another rank's gradient all-reduce
+    gt_r = torch.zeros(3, 8, 8 + 4 * rank)
+    for _ in range(2):
+        ts.train_step(gs, deform, None, gt_r, types.SimpleNamespace(), None, deferred_count=False, allreduce=AR())
+    out.append(list(calls))
+    calls.clear()
     usable["v"] = rank == 0  # rank 1 loses the path without a key change: it raises
     try:
         ts.train_step(gs, deform, None, gt, types.SimpleNamespace(), None, deferred_count=False, allreduce=AR())
@@ -423,16 +431,21 @@ def _path_agreement_case(rank, world):
 def test_native_path_choice_is_agreed_across_ranks():
     out = _run(_path_agreement_case)
     for rank in (0, 1):
-        a, b, c, d = out[rank]
+        a, b, c, e, d = out[rank]
         assert a == ["autograd", "autograd"]
         assert b == ["autograd"]
         assert c == ["native"]
+        assert e == ["native", "native"]
         assert d == (["native"] if rank == 0 else "raised")
 
 
 def test_rccl_group_reserves_cus_for_the_collective(monkeypatch):
-    """Before an RCCL group: NCCL_MAX_NCHANNELS defaults to OVERLAP_CUS and the MLP kernels leave that
-    many CUs free (the library knob; a host-side setter, no GPU needed); explicit settings win."""
+    """reserve_cus_for_collectives (opt-in: DGS_OVERLAP_RESERVE=1 before an RCCL group): NCCL_MAX_NCHANNELS
+    defaults to OVERLAP_CUS and the MLP kernels leave that many CUs free (the library knob; a host-side
+    setter, no GPU needed); explicit settings win. By default nothing is reserved."""
+    import inspect
+    from deformgs import dist as dgs_dist
+    assert 'os.environ.get("DGS_OVERLAP_RESERVE", "0") == "1"' in inspect.getsource(dgs_dist.init_from_env)
     from deformgs import _lib
     from deformgs.dist import OVERLAP_CUS, reserve_cus_for_collectives
     lib = _lib.load()

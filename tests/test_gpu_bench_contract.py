@@ -41,3 +41,24 @@ def test_bench_line_contract():
     assert r["bound"] in ("hbm", "mfma") and r["unit"] in ("GB/s", "TFLOP/s")
     assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], rel=1e-6)
     assert 0.0 < r["frac"] < 1.0
+
+
+def test_bench_self_launches_two_ranks_gloo_rehearsal():
+    """`bench.py --gpus 2` invoked directly (no WORLD_SIZE) launches its own two ranks through
+    torch.distributed.run; on a one-GPU box both ranks share cuda:0 over gloo (DGS_DEVICE=0,
+    DGS_DIST_BACKEND=gloo: RCCL refuses two ranks on one GPU). Rank 0's single line reports n_gpus 2, the
+    backend and what every rank saw."""
+    env = dict(os.environ, DGS_DEVICE="0", DGS_DIST_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "1",
+           "--n", "20000", "--res", "256", "--no-cpu-baseline"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 2
+    assert d["dist"]["world_size"] == 2 and d["dist"]["backend"] == "gloo"
+    assert sorted(r["rank"] for r in d["dist"]["ranks"]) == [0, 1]
+    assert all(r["world_seen"] == 2 for r in d["dist"]["ranks"])
+    assert d["value"] == pytest.approx(2 * 1000.0 / d["ms_per_step"], rel=1e-6)

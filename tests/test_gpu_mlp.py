@@ -1,7 +1,8 @@
 """Fused HIP deformation MLP vs the reference's own outputs (tests/golden/mlp_*.npz) and the
 float64 numpy oracle (oracle/mlp_ref.py) at larger, ragged N, for both GEMM arithmetics: the default
-split-bf16 path (fp32 operands split exactly into hi/mid/lo bf16, six MFMA products per fp32
-product) and the exact fp32-input MFMA path (DGS_MLP_EXACT_FP32).
+split-f16 path (fp32 operands scaled by a power of two and split into hi / lo f16, three MFMA
+products per fp32 product; round 6, rounds 1-5 ran a six-product bf16 split) and the exact
+fp32-input MFMA path (DGS_MLP_EXACT_FP32).
 
 Tolerance (either path, vs a float64 oracle / the reference's fp32 CPU run): outputs
 |err| <= 2e-5 + 1e-4 |ref|; parameter gradients within 1e-4 relative to each tensor's max (or to
@@ -140,7 +141,7 @@ def test_expanded_time_input():
 @pytest.mark.parametrize("name,N", [("blender", 20000), ("nonblender", 20000), ("6dof", 20000), ("fork", 20000),
                                     ("blender", 100000)])
 def test_split_accuracy_matches_fp32(name, N):
-    """The split-bf16 GEMMs are as accurate as fp32 MFMA: max error vs the float64 oracle within 2x
+    """The split-f16 GEMMs are as accurate as fp32 MFMA: max error vs the float64 oracle within 2x
     the exact path's (every kernel output and every parameter gradient), at N = 20000 (ragged: 312.5
     blocks) and N = 100000. The upstream gradient is given on the kernel's raw outputs (for 6-DoF: w, v before
     exp_se3, whose 1/|w| amplifies any fp32 difference; that chain is checked by test_mlp_golden).
@@ -176,6 +177,94 @@ def test_split_accuracy_matches_fp32(name, N):
         errs[arith] = e
     for k in errs["exact"]:
         assert errs["split"][k] <= 2.0 * errs["exact"][k] + 1e-6, (k, errs["split"][k], errs["exact"][k])
+
+
+def _bench_regime():
+    """Inputs of bench.py's step at its own configuration (tests/test_gpu_step_parity.py bench-100k):
+    synth-100k (seed 0) at 800^2, blender network (mlp_weights seed 4, heads at 1/100), camera 1 (fid
+    1/30), target = that camera's initial render + N(0, 0.02), clamped. Returns (weights, xyz, t0, G)
+    with G = dL/d(raw network output), the upstream gradient the fused L1 + SSIM loss and the rasterizer
+    backward hand the network there: against a near-render target its per-point terms nearly cancel in
+    every dW sum, which is the regime the step-parity bar at bench size exercises."""
+    from deformgs.arguments import PipelineParams
+    from deformgs.deform_network import DeformNetworkBaseline
+    from deformgs.gaussian_model import GaussianModel
+    from deformgs.loss import l1_ssim_loss
+    from deformgs.renderer import render
+    from deformgs.synthetic import synth_camera, synth_gaussians
+    from weights import mlp_weights
+    dev = torch.device("cuda", 0)
+    N = 100_000
+    g = synth_gaussians(N, seed=0, device=dev)
+    gs = GaussianModel(3)
+    gs.from_tensors(g["xyz"], g["features_dc"], g["features_rest"], g["scaling"], g["rotation"], g["opacity"])
+    net = DeformNetworkBaseline(is_blender=True).cuda()
+    w = mlp_weights(mlp_ref.param_shapes(True, False), seed=4)
+    for k in w:
+        if k.startswith(("gaussian_warp", "gaussian_rotation", "gaussian_scaling")):
+            w[k] = (w[k] * 0.01).astype(np.float32)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in w.items()})
+    cam = synth_camera(800, 800, index=1, fid=1.0 / 30.0, device=dev)
+    pipe, bg = PipelineParams(), torch.zeros(3, device=dev)
+    x = gs.get_xyz.detach()
+    t = cam.fid.unsqueeze(0).expand(N, -1)
+    with torch.no_grad():
+        r0 = net.raw(x, t)
+        img0 = render(cam, gs, pipe, bg, r0[:, 0:3], r0[:, 3:7], r0[:, 7:10])["render"]
+        noise = torch.randn(img0.shape, generator=torch.Generator().manual_seed(101)).to(dev)
+        gt = (img0 + 0.02 * noise).clamp_(0.0, 1.0).contiguous()
+        del r0, img0
+    raw = net.raw(x, t)
+    raw.retain_grad()
+    img = render(cam, gs, pipe, bg, raw[:, 0:3], raw[:, 3:7], raw[:, 7:10])["render"]
+    loss, _, _ = l1_ssim_loss(img, gt)
+    loss.backward()
+    G = raw.grad.detach().double().cpu().numpy()
+    t0 = float(cam.fid.item())
+    del net, gs, raw, img
+    torch.cuda.empty_cache()
+    return w, x.cpu().numpy(), t0, G
+
+
+def test_split_accuracy_bench_regime():
+    """the default GEMM arithmetic against the fp32-MFMA path at the benchmarked
+    configuration. The network-output gradient of bench.py's own step (_bench_regime: a near-render
+    target, so every dW sum over the 100k points nearly cancels) is fed to both arithmetics on the
+    kernels the bench runs (stride-0 frame time: the folded-t_emb forward, the dX chain, k_dws / k_dw,
+    k_tgrad); every kernel output and every parameter gradient must be within 2x the fp32-MFMA path's
+    max error against the float64 oracle (plus 1e-12 absolute). Both errors are recorded
+    (gpurun_out/parity_stats.jsonl -> profiles/)."""
+    from helpers import write_stats
+    w, x, t0, G = _bench_regime()
+    N = x.shape[0]
+    out, c = mlp_ref.forward(w, x, np.full((N, 1), t0, np.float32), True, False)
+    ref_raw = np.concatenate([out["d_xyz"], out["d_rot"], out["d_scale"]], 1)
+    errs, scale = {}, {}
+    for arith in ARITH:
+        net = _net_from(w, ARITH[arith])
+        tt = torch.full((1, 1), t0, device="cuda").expand(N, -1)
+        raw = net.raw(torch.from_numpy(x).cuda(), tt)
+        masks = mlp_relu_masks(raw, N, True, ARITH[arith], th_saved=ARITH[arith])
+        e = {"out": float(np.abs(raw.detach().cpu().numpy() - ref_raw).max())}
+        (raw * torch.from_numpy(G).float().cuda()).sum().backward()
+        ref_g = mlp_ref.backward(w, c, out, _raw_grads(G, False, False), True, False, relu_masks=masks)
+        for k, p in net.named_parameters():
+            if k in ref_g:
+                e[k] = float(np.abs(p.grad.cpu().numpy() - ref_g[k]).max())
+                scale[k] = float(np.abs(ref_g[k]).max())
+        errs[arith] = e
+        del net, raw
+    write_stats("mlp_split_accuracy_bench_regime", {"split": errs["split"], "exact": errs["exact"],
+                                                     "ref_max": scale})
+    for k in errs["exact"]:
+        assert errs["split"][k] <= 2.0 * errs["exact"][k] + 1e-12, (k, errs["split"][k], errs["exact"][k])
+
+
+def _net_from(w, exact):
+    from deformgs.deform_network import DeformNetworkBaseline
+    net = DeformNetworkBaseline(is_blender=True, exact_fp32=exact).cuda()
+    net.load_state_dict({k: torch.from_numpy(a) for k, a in w.items()})
+    return net
 
 
 def _raw_grads(G, d6, fork):
@@ -231,7 +320,8 @@ def test_uniform_t_flag(name, N):
 def test_tail_blocks_bitwise_equal_64_point_blocks(tmp_path):
     """The fused forward / dX kernels run the sparse last round of 64-point blocks as 16-point
     blocks (mlp_split.hip block_split); every output and parameter gradient must equal the all-64-
-    point decomposition (DGS_MLP_NO_TAIL=1, read once per process) bit for bit."""
+    point decomposition (DGS_MLP_NO_TAIL=1, read once per process) bit for bit. (Round 6: every
+    operand scale of the split-f16 GEMMs is per 16-point column tile, so this still holds.)"""
     import os
     import subprocess
     import sys
