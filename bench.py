@@ -47,11 +47,17 @@ MLP_DX_MAC = 461312             # W^T products whose input gradient is needed (h
 MLP_DW_MAC = 493568             # every trunk + head weight once, t_emb columns from gb (x) te
 
 
+ARGV_ENV = "DGS_BENCH_ARGV"  # the parent's arguments for the launched ranks (JSON list)
+
+
 def launcher_cmd(argv, nproc, port):
-    """The child command that runs this bench as `nproc` ranks on one node (no GPU call in the parent):
-    torch.distributed.run on 127.0.0.1 with the same arguments."""
-    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
-            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    """(command, extra environment) that run this bench as `nproc` ranks on one node (no GPU call in the
+    parent): torch.distributed.run on 127.0.0.1. The bench arguments travel in DGS_BENCH_ARGV, not on the
+    command line: torch.distributed.run's parser matches option prefixes even after the script name
+    (`--n` is ambiguous with its --nnodes / --nproc-per-node / --node-rank)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)]
+    return cmd, {ARGV_ENV: json.dumps(list(argv))}
 
 
 def _free_port():
@@ -67,9 +73,9 @@ def maybe_launch(args, argv):
     if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
         return None
     import subprocess
-    cmd = launcher_cmd(argv, args.gpus, _free_port())
-    print("[bench] launching " + " ".join(cmd), file=sys.stderr, flush=True)
-    return subprocess.call(cmd)
+    cmd, extra = launcher_cmd(argv, args.gpus, _free_port())
+    print("[bench] launching " + " ".join(cmd) + " with " + str(extra), file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=dict(os.environ, **extra))
 
 
 def parse(argv=None):
@@ -225,7 +231,8 @@ def cpu_baseline(N, res, steps, warmup=3):
 
 
 def main():
-    args = parse()
+    # a launched rank takes the parent's arguments from DGS_BENCH_ARGV (launcher_cmd)
+    args = parse(json.loads(os.environ[ARGV_ENV]) if "WORLD_SIZE" in os.environ and ARGV_ENV in os.environ else None)
     rc = maybe_launch(args, sys.argv[1:])
     if rc is not None:
         sys.exit(rc)
