@@ -45,6 +45,16 @@ HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak (spec)
 MLP_FWD_MAC = 493568            # every trunk + head weight once, t_emb columns folded
 MLP_DX_MAC = 461312             # W^T products whose input gradient is needed (heads, L7..L1 hidden rows)
 MLP_DW_MAC = 493568             # every trunk + head weight once, t_emb columns from gb (x) te
+# Algorithmic HBM bytes per point of the MLP kernels (blender network, one frame time):
+#   k_fwd8: the saved activations it writes for dW (x_emb 64 + H0..H7 2048 rows, fp32) + the relu' bits
+#           of the 2048 trunk rows + xyz in + the 10 outputs
+#   k_bwd:  the dZ rows it writes (8 x 256 + the 32 dOut rows, fp32) + the relu' bits + dOut in
+#   k_dws:  every row the dW jobs read once (X: 2 x 64 x_emb + H0..H6 + H4 again + H7 = 2432 rows; dZ:
+#           8 x 256 + dZ5 again + 32 = 2336 rows), plus the per-workgroup slabs (constant per launch)
+MLP_FWD_BYTES = 4 * 2112 + 2048 / 8 + 12 + 40
+MLP_BWD_BYTES = 4 * 2080 + 2048 / 8 + 40
+MLP_DW_BYTES = 4 * (2432 + 2336)
+MLP_DW_SLAB_BYTES = 256 * (256 * 256 + 256) * 4
 
 
 ARGV_ENV = "DGS_BENCH_ARGV"  # the parent's arguments for the launched ranks (JSON list)
@@ -113,6 +123,18 @@ def mfma_peak(name):
     if exact:
         return FP32_MFMA_PEAK_TFLOPS, "fp32 MFMA (v_mfma_f32_32x32x2_f32)"
     return SPLIT_MFMA_PEAK_TFLOPS, "f16 MFMA peak / 3 (scaled hi/lo f16 split, three products per fp32 product)"
+
+
+def mlp_bytes(name, N):
+    """Algorithmic HBM bytes per launch of an MLP kernel class (padded points: 64-point blocks)."""
+    Ns = -(-N // 64) * 64
+    if name == "mlp_fwd":
+        return MLP_FWD_BYTES * Ns
+    if name == "mlp_bwd":
+        return MLP_BWD_BYTES * Ns
+    if name == "mlp_dw":
+        return MLP_DW_BYTES * Ns + MLP_DW_SLAB_BYTES
+    return None
 
 
 def kernel_algorithmic(name, N, P, HW, cap=None, T=None):
@@ -389,11 +411,25 @@ def main():
         name, ms, n, (amount, unit, bound) = best
         avg_s = ms / 1000.0 / n
         if bound == "mfma":
-            achieved = amount / avg_s / 1e12
+            # the MLP kernels move ~1-2 GB per launch beside their FLOPs: their roofline is the larger of
+            # the MFMA time and the HBM time of their algorithmic bytes (attainable = min(peak, AI x BW));
+            # frac = that ideal time / the measured launch
             peak, arith = mfma_peak(name)
-            roofline = {"bound": "mfma", "kernel": name, "achieved": achieved, "peak": peak, "peak_basis": arith,
-                        "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
-                        "avg_launch_ms": avg_s * 1e3, "launches": n}
+            nbytes = mlp_bytes(name, N)
+            t_flop = amount / (peak * 1e12)
+            t_hbm = nbytes / (HBM_PEAK_GBS * 1e9) if nbytes else 0.0
+            if t_hbm > t_flop:
+                roofline = {"bound": "hbm", "kernel": name, "achieved": nbytes / avg_s / 1e9, "peak": HBM_PEAK_GBS,
+                            "unit": "GB/s", "frac": t_hbm / avg_s, "traffic": None, "algorithmic_bytes": nbytes,
+                            "mfma": {"achieved_tflops": amount / avg_s / 1e12, "peak_tflops": peak,
+                                     "peak_basis": arith, "frac": t_flop / avg_s},
+                            "avg_launch_ms": avg_s * 1e3, "launches": n}
+            else:
+                roofline = {"bound": "mfma", "kernel": name, "achieved": amount / avg_s / 1e12, "peak": peak,
+                            "peak_basis": arith, "unit": "TFLOP/s", "frac": t_flop / avg_s, "traffic": None,
+                            "hbm": {"algorithmic_bytes": nbytes, "achieved_gbs": (nbytes or 0) / avg_s / 1e9,
+                                    "frac": t_hbm / avg_s},
+                            "avg_launch_ms": avg_s * 1e3, "launches": n}
         else:
             achieved = amount / avg_s / 1e9
             roofline = {"bound": "hbm", "kernel": name, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

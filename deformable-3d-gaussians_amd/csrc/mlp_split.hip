@@ -190,7 +190,7 @@ __device__ __forceinline__ void lds_fmax(uint32_t *p, float v) {
 //  bsync[i][q]: block-wide maxima gathered behind a workgroup barrier (staging, narrow timenet tiles)
 //  bmax[L]: max |bias| of trunk layer L (8: heads), from the launch-constant bias table
 //  wstat[L]: max row abs sum of the layer's A image (k_pack's tile statistics; [8]: heads^T)
-struct ScaleLDS {
+struct alignas(16) ScaleLDS {
     float ksc[12][4];
     float amax[2][16][4];
     float ain[2][4];
@@ -201,11 +201,16 @@ struct ScaleLDS {
 // block-sync slots
 constexpr int BS_XE = 0, BS_TE = 1, BS_TIN = 2, BS_TH = 3, BS_TET = 4, BS_G = 5, BS_GTE = 6;
 
-__device__ inline float amax_of(const ScaleLDS *sc, int par, int nw, int q) {
-    float m = 0.f;
-    for (int w = 0; w < nw; w++) m = fmaxf(m, sc->amax[par][w][q]);
+// max over the nw writer waves of their published maxima, all four column tiles (one 16-B read per wave)
+__device__ inline float4 amax_of4(const ScaleLDS *sc, int par, int nw) {
+    float4 m = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int w = 0; w < nw; w++) {
+        const float4 v = *reinterpret_cast<const float4 *>(sc->amax[par][w]);
+        m = make_float4(fmaxf(m.x, v.x), fmaxf(m.y, v.y), fmaxf(m.z, v.z), fmaxf(m.w, v.w));
+    }
     return m;
 }
+__device__ __forceinline__ float f4get(const float4 &v, int q) { return q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w; }
 
 // ------------------------------------------------------------------------------------------------
 // GEMM pieces. 16x16x32 lane maps (cdna_hip_programming.md §3): lane l (kq = l >> 4, col = l & 15)
@@ -1019,11 +1024,11 @@ __device__ __forceinline__ void fwd_block(const FwdArgs &a, h16x8 *lds, uint32_t
         // same on every wave)
         float so[NQB], my[NQB] = {};
         const float ws = __uint_as_float(sc->wstat[L]), bm = __uint_as_float(sc->bmax[L]);
+        const float4 am = L > 0 ? amax_of4(sc, (L - 1) & 1, NWAVE) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
         for (int q = 0; q < NQB; q++) {
-            float ain = L == 0 || L == 5 ? sc->ain[0][q] : 0.f;
+            float ain = fmaxf(L == 0 || L == 5 ? sc->ain[0][q] : 0.f, f4get(am, q));
             if (!fold && (L == 0 || L == 5)) ain = fmaxf(ain, sc->ain[1][q]);
-            if (L > 0) ain = fmaxf(ain, amax_of(sc, (L - 1) & 1, NWAVE, q));
             so[q] = fmaf(ws, ain, bm);
         }
         col_absmax(c, my);
@@ -1222,12 +1227,9 @@ __device__ __forceinline__ void fwd_block8(const FwdArgs &a, h16x8 *lds, uint32_
         // same on every wave)
         float so[NQB];
         const float ws = __uint_as_float(sc->wstat[L]), bm = __uint_as_float(sc->bmax[L]);
+        const float4 am = L > 0 ? amax_of4(sc, (L - 1) & 1, NW8) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-        for (int q = 0; q < NQB; q++) {
-            float ain = L == 0 || L == 5 ? sc->ain[0][q] : 0.f;
-            if (L > 0) ain = fmaxf(ain, amax_of(sc, (L - 1) & 1, NW8, q));
-            so[q] = fmaf(ws, ain, bm);
-        }
+        for (int q = 0; q < NQB; q++) so[q] = fmaf(ws, fmaxf(L == 0 || L == 5 ? sc->ain[0][q] : 0.f, f4get(am, q)), bm);
         col_wave_max(my);
         // this wave's rows are H k-step w: all 8 waves must have read it (and its scales) in this layer
         if (L > 0) lds_wait_ge(hrd + w, (uint32_t)NW8 * L, lds_peek(hrd + w));
@@ -1367,8 +1369,9 @@ __device__ inline void stage_dout(const BwdArgs &a, h16x8 *lds, ScaleLDS *sc, fl
 // only zeroes), the same on every wave
 template <int NQB>
 __device__ inline void chain_scales(const ScaleLDS *sc, float ws, int par, int nw, float (&so)[NQB]) {
+    const float4 am = par < 0 ? *reinterpret_cast<const float4 *>(sc->ain[0]) : amax_of4(sc, par, nw);
 #pragma unroll
-    for (int q = 0; q < NQB; q++) so[q] = ws * (par < 0 ? sc->ain[0][q] : amax_of(sc, par, nw, q));
+    for (int q = 0; q < NQB; q++) so[q] = ws * f4get(am, q);
 }
 
 // TE_ROWS: per-point dL/dt_emb (blender, t not frame-uniform); the other instantiation carries no
@@ -2510,11 +2513,12 @@ int backward(int flags, int N, const float *packed, const float *saved, const fl
             hipLaunchKernelGGL(k_bwd<true>, dim3(grid), dim3(NTHR), 0, stream, b);
         else
         {
-            // DGS_MLP_BWD8=1: the 8-wave k_bwd8 (bitwise equal; A/B r5u: neutral, so the 16-wave kernel
-            // stays the default)
+            // the 8-wave k_bwd8 (bitwise equal to the 16-wave kernel): neutral on the bf16x6 split (r5u),
+            // +0.5 % steps/s on the f16 split (mlp_bwd 0.333 -> 0.325 ms, profiles/r6f_mlp_variants_ab.txt);
+            // DGS_MLP_BWD8=0 keeps the 16-wave k_bwd
             static const bool bwd8 = [] {
                 const char *e = getenv("DGS_MLP_BWD8");
-                return e && e[0] == '1';
+                return !(e && e[0] == '0');
             }();
             if (bwd8)
                 hipLaunchKernelGGL(k_bwd8, dim3(grid), dim3(NTHR8), 0, stream, b);
