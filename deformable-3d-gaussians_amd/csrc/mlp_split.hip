@@ -1851,7 +1851,11 @@ __device__ __forceinline__ void dws_run(const WJob &J, size_t Ns, const float *_
         const float4 v = st[f];
         // the row's scale: max over its 8 staging lanes (a partial last slot group lies in one wave, past
         // the valid rows: its lanes see zeros, never a valid row's)
+#ifdef DGS_DIAG_DWS_NOSCALE  // diagnostic (wrong results): constant scales, no per-chunk maxima
+        const Scale s = Scale{1024.f, 1.f / 1024.f};
+#else
         const Scale s = scale_for(max8(ok ? absmax4(v) : 0.f));
+#endif
         if (!ok) return;
         if (COL) bsum[f] += live ? (v.x + v.y) + (v.z + v.w) : 0.f;
         const Split4 sp = split4(v.x, v.y, v.z, v.w, s.s);
@@ -1887,8 +1891,12 @@ __device__ __forceinline__ void dws_run(const WJob &J, size_t Ns, const float *_
         if (pact) {
             // private fragments of this chunk (scaled by the wave's max), then the private loads of
             // the next (in flight for the whole chunk)
+#ifdef DGS_DIAG_DWS_NOSCALE
+            const Scale sp = Scale{1024.f, 1.f / 1024.f};
+#else
             const float pm = wave_max(fmaxf(fmaxf(absmax4(pr[0]), absmax4(pr[1])), fmaxf(absmax4(pr[2]), absmax4(pr[3]))));
             const Scale sp = scale_for(pm);
+#endif
             AFrag pf0 = split8(pr[0], pr[1], sp.s), pf1 = split8(pr[2], pr[3], sp.s);
             if (!COL) bsum[0] += sum8(pr[0], pr[1]) + sum8(pr[2], pr[3]);
             pload(min(c + 1, c1 - 1));
@@ -1897,11 +1905,18 @@ __device__ __forceinline__ void dws_run(const WJob &J, size_t Ns, const float *_
                 // the tile's two k-steps into a fresh accumulator, one shared fragment live at a time
                 const float si = sp.inv * rsc[buf * S_RSC + 32 * s + i];
                 const AFrag s0 = s_frag(L, 0, s, lane);
+#ifdef DGS_DIAG_DWS_NOFOLD  // diagnostic (wrong results): the MFMAs accumulate into acc directly
+                acc[s] = mma3_into(pf0, s0, acc[s]);
+                const AFrag s1 = s_frag(L, 1, s, lane);
+                acc[s] = mma3_into(pf1, s1, acc[s]);
+                (void)si;
+#else
                 f32x16 T = mma3_into(pf0, s0, (f32x16)(0.f));
                 const AFrag s1 = s_frag(L, 1, s, lane);
                 T = mma3_into(pf1, s1, T);
 #pragma unroll
                 for (int r = 0; r < 16; r++) acc[s][r] = fmaf(T[r], si, acc[s][r]);
+#endif
 #pragma unroll
                 for (int f = 0; f < NSF; f++)
                     if (put_at(f) == s) sput(f, buf ^ 1, more);
