@@ -449,7 +449,7 @@ def main():
     step_s = elapsed / args.steps
     if roofline is not None:
         # SURVEY.md 8d's step-level figure: (MLP FLOPs / MFMA peak + raster bytes / HBM peak) / step time,
-        # on both MFMA bases (the split-bf16 GEMMs' ceiling and the native fp32 MFMA peak)
+        # on both MFMA bases (the split-f16 GEMMs' ceiling and the native fp32 MFMA peak)
         mlp_flop = 2.0 * (MLP_FWD_MAC + MLP_DX_MAC + MLP_DW_MAC) * N
         raster_bytes = 1000.0 * N + 132.0 * P_pairs + 48.0 * HW
         roofline["step"] = {

@@ -18,7 +18,7 @@ from . import _lib
 FLAG_BLENDER = 1
 FLAG_6DOF = 2
 FLAG_NO_ROTSCALE = 4
-FLAG_EXACT_FP32 = 8  # v_mfma_f32_32x32x2_f32 kernels instead of the split-bf16 (bf16x6) default
+FLAG_EXACT_FP32 = 8  # v_mfma_f32_32x32x2_f32 kernels instead of the split-f16 (f16x3) default
 FLAG_UNIFORM_T = 16  # every point carries t[0] (set when t is one value or a stride-0 expand)
 
 
@@ -141,7 +141,7 @@ class _DeformBase(nn.Module):
         self.gaussian_scaling = nn.Linear(W, 3)
         self.flags = (FLAG_BLENDER if is_blender else 0) | (FLAG_6DOF if is_6dof else 0) | (
             0 if self._rotscale else FLAG_NO_ROTSCALE)
-        # GEMM arithmetic: fp32 on bf16 MFMA over an exact hi/mid/lo split (default) or fp32-input MFMA;
+        # GEMM arithmetic: fp32 on f16 MFMA over a scaled hi/lo split (default) or fp32-input MFMA;
         # both are fp32-accurate (include/dgs.h), the flag is not part of the state_dict
         self.exact_fp32 = _exact_default() if exact_fp32 is None else bool(exact_fp32)
 

@@ -200,15 +200,16 @@ void dgs_timing_sample(int period);
 long long dgs_timing_launches(const char *name);
 
 /* ---- deformation MLP (utils/time_utils.py:56-201), fused PE + 8x256 MLP ----
- * Default: fp32 GEMMs on bf16 MFMA over an exact hi/mid/lo operand split (six products per fp32
- * product, dropped terms < 2^-23 relative: fp32 accuracy). DGS_MLP_EXACT_FP32 selects the
+ * Default: fp32 GEMMs on f16 MFMA over a scaled two-piece operand split (x * 2^e = hi + lo, both f16;
+ * three products hh + hl + lh per fp32 product, dropped ll <= 2^-22 relative; every output and
+ * gradient held to 2x the fp32-MFMA path's error, mlp_split.hip). DGS_MLP_EXACT_FP32 selects the
  * v_mfma_f32_32x32x2_f32 kernels (bit-identical to fp32 fma chains). The flag changes the packed /
  * saved / scratch layouts: pass the same flags to every call of one forward/backward. */
 enum {
     DGS_MLP_BLENDER = 1,   /* timenet on (t: L=6 -> 256 -> 30); else raw t PE (L=10, 21 ch) */
     DGS_MLP_6DOF = 2,      /* heads branch_w(3), branch_v(3) instead of gaussian_warp(3) */
     DGS_MLP_NO_ROTSCALE = 4, /* DeformNetwork fork variant: rotation/scaling heads unused */
-    DGS_MLP_EXACT_FP32 = 8, /* fp32-input MFMA path instead of the split-bf16 path */
+    DGS_MLP_EXACT_FP32 = 8, /* fp32-input MFMA path instead of the split-f16 path */
     DGS_MLP_UNIFORM_T = 16  /* caller guarantees t[i] == t[0] for every point (one frame time, as
                                train_baseline.py:107-110 feeds it): the timenet runs once per launch,
                                t_emb is folded into the linear.0 / linear.5 biases (outputs equal the
