@@ -56,6 +56,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <cassert>
 
 #include <algorithm>
 #include <cmath>
@@ -85,6 +86,7 @@ constexpr int NQ = 4;             // 16-point column tiles per workgroup
 constexpr int NWAVE = 16;         // one 16-row n-tile of a 256-wide layer per wave
 constexpr int NTHR = NWAVE * 64;
 constexpr int NSPLIT = 2;         // hi, lo
+constexpr int PACK_MAXK = 11;     // k-slots of the widest A-image n-tile (linear.5's forward image: 352 / 32)
 constexpr int UG = NSPLIT * BM;   // 16-B units per 8-feature group (all splits, all points)
 constexpr int KSLOT = 3 * 64;     // units per (n-tile, k-step) of an A image: hi, lo, inverse scale
 constexpr int KG = 4;             // 8-feature groups per k-step (32 features)
@@ -2110,6 +2112,7 @@ Plan make_plan(int flags) {
     // one pack workgroup per n-tile of every image region (its scale and row statistics span the tile's
     // whole K): the region list is fixed by the flags
     auto region = [&](int slot0, int ntiles, int nk) {
+        assert(nk <= PACK_MAXK);
         for (int t = 0; t < ntiles; t++) {
             P.units.push_back(slot0 + t * nk);
             P.units.push_back(nk);
@@ -2158,14 +2161,18 @@ __global__ __launch_bounds__(512) void k_pack(const int *__restrict__ map, PackP
         if (j < nf32) fp[j] = gather(nimg + j);
         return;
     }
-    const int2 u = units[b];  // (first k-slot, k-slots)
+    const int2 u = units[b];  // (first k-slot, k-slots <= PACK_MAXK)
     if (tid == 0) s_max = 0;
-    // element tid of a slot: lane l = tid >> 3 holds row l & 15 of the tile (v_mfma_f32_16x16x32_f16 A map)
+    // element tid of a slot: lane l = tid >> 3 holds row l & 15 of the tile (v_mfma_f32_16x16x32_f16 A map);
+    // the tile's values stay in registers between the statistics and the split: one gather each, all
+    // in flight at once (the rolled loops made 2 x k-slots dependent map -> parameter round trips)
+    float v[PACK_MAXK];
     float am = 0.f, rs = 0.f;
-    for (int k = 0; k < u.y; k++) {
-        const float v = fabsf(gather((u.x + k) * 512 + tid));
-        am = fmaxf(am, v);
-        rs += v;
+#pragma unroll
+    for (int k = 0; k < PACK_MAXK; k++) {
+        v[k] = k < u.y ? gather((u.x + k) * 512 + tid) : 0.f;
+        am = fmaxf(am, fabsf(v[k]));
+        rs += fabsf(v[k]);
     }
     rs += __shfl_xor(rs, 1);  // the 8 elements of a lane (tid bits 0-2): same row
     rs += __shfl_xor(rs, 2);
@@ -2176,8 +2183,10 @@ __global__ __launch_bounds__(512) void k_pack(const int *__restrict__ map, PackP
     if ((tid & 7) == 0) s_rs[tid >> 7][(tid >> 3) & 15] = rs;  // tid bits 7-8: the four k quarters
     __syncthreads();
     const Scale S = scale_for(__uint_as_float(s_max));
-    for (int k = 0; k < u.y; k++) {
-        const float x = gather((u.x + k) * 512 + tid) * S.s;
+#pragma unroll
+    for (int k = 0; k < PACK_MAXK; k++) {
+        if (k >= u.y) break;
+        const float x = v[k] * S.s;
         const _Float16 hi = (_Float16)x;
         const _Float16 lo = (_Float16)(x - (float)hi);
         _Float16 *d = img + (size_t)(u.x + k) * 1536 + tid;  // k-slot: hi, lo, scale plane of 512 f16
