@@ -1744,6 +1744,11 @@ constexpr int S_TRP = 32 * 33;                // per-wave transpose scratch (flo
 static_assert(S_LDS <= 160 * 1024 && 8 * S_TRP * 4 <= S_LDS, "dWs LDS");
 
 #define MFMA32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_f16((a), (b), (c), 0, 0, 0)
+#ifdef DGS_DIAG_DWS_L2  // diagnostic (wrong results): every chunk re-reads the split's first chunk (L2-resident)
+#define DWS_DIAG_C(c) (c0)
+#else
+#define DWS_DIAG_C(c) (c)
+#endif
 
 // unit of (split p, k-step ks, row block rb, point half hh, row i): each 32-unit half is rotated
 // by 4 ks + 2 hh, so the row-major staging stores (8 lanes per row: all (ks, hh, 8-byte half)
@@ -1822,7 +1827,7 @@ __device__ __forceinline__ void dws_run(const WJob &J, size_t Ns, const float *_
 #pragma unroll
         for (int q = 0; q < 4; q++)
             pr[q] = __builtin_bit_cast(float4,
-                                       __builtin_amdgcn_raw_buffer_load_b128(rsP, pvoff, c * 128 + (q >> 1) * 64 + (q & 1) * 16, 0));
+                                       __builtin_amdgcn_raw_buffer_load_b128(rsP, pvoff, DWS_DIAG_C(c) * 128 + (q >> 1) * 64 + (q & 1) * 16, 0));
     };
     // shared staging: slot g = tid + 512 f -> row g >> 3, points 4 (g & 7) .. + 3 of the chunk (8
     // lanes read a row's 128 B)
@@ -1839,7 +1844,7 @@ __device__ __forceinline__ void dws_run(const WJob &J, size_t Ns, const float *_
             int row, q;
             if (sslot(f, row, q))
                 st[f] = __builtin_bit_cast(
-                    float4, __builtin_amdgcn_raw_buffer_load_b128(rsS, (row * (int)Ns + 4 * q) * 4, c * 128, 0));
+                    float4, __builtin_amdgcn_raw_buffer_load_b128(rsS, (row * (int)Ns + 4 * q) * 4, DWS_DIAG_C(c) * 128, 0));
         }
     };
     float bsum[NSF] = {};  // COL: bias row sums of the staged dZ rows; ROW: bsum[0] of the private row
