@@ -257,7 +257,19 @@ __device__ unsigned long long *dgs_mlps_prof;
         if (L == 3 && (threadIdx.x & 63) == 0 && p0 == (int)blockIdx.x * BM)                           \
             dgs_mlps_prof[blockIdx.x * 64 + (k) + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memtime();  \
     } while (0)
+// k_fwd8 (8 waves): layer DGS_PROF_LAYER of the workgroup's first block, stamp k + wave
+#ifndef DGS_PROF_LAYER
+#define DGS_PROF_LAYER 3
+#endif
+#define DGS_WSTAMP8(k, L)                                                                              \
+    do {                                                                                               \
+        if (L == DGS_PROF_LAYER && (threadIdx.x & 63) == 0 && p0 == (int)blockIdx.x * BM)              \
+            dgs_mlps_prof[blockIdx.x * 64 + (k) + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memtime();  \
+    } while (0)
 #else
+#define DGS_WSTAMP8(k, L) \
+    do {                  \
+    } while (0)
 #define DGS_WSTAMP(k, L) \
     do {                 \
     } while (0)
@@ -1160,6 +1172,7 @@ __device__ __forceinline__ void fwd_block8(const FwdArgs &a, h16x8 *lds, uint32_
                                                   (16 * (L >> 1) + nt) * 256, 0);
         }
     };
+    DGS_STAMP(0);
     if (tid < 8) {
         hwr[tid] = 0;
         hrd[tid] = 0;
@@ -1202,6 +1215,7 @@ __device__ __forceinline__ void fwd_block8(const FwdArgs &a, h16x8 *lds, uint32_
         put_unit8(lds, g, m, v, scale_for(fmaxf(1.f, __uint_as_float(sc->bsync[BS_XE][qof(m)]))).s);
     }
     lds_barrier();
+    DGS_STAMP(1);
     f32x4 c[2][NQB];
     float ib[NQB];
 #pragma unroll 1
@@ -1213,9 +1227,11 @@ __device__ __forceinline__ void fwd_block8(const FwdArgs &a, h16x8 *lds, uint32_
         const h16x8 *Aw = a.img + (size_t)(a.fL[L] + 2 * w * nk) * KSLOT;
         const int astride = nk * KSLOT;
         const HGate hg{hwr, hrd, L == 5 ? 2 : 0, 1u * L, true, lane};
+        DGS_WSTAMP8(24, L);
         if (L == 0) gemm2<2, NQB>(Aw, astride, lds, g0, 0, lane, c, ib, sc->ksc);
         else if (L == 5) gemm2<10, NQB, NoPre, HGate, 2, 1u << 2>(Aw, astride, lds, g0, 0, lane, c, ib, sc->ksc, NoPre(), hg);
         else gemm2<8, NQB>(Aw, astride, lds, g0, 0, lane, c, ib, sc->ksc, NoPre(), hg);
+        DGS_WSTAMP8(32, L);
         float my[NQB] = {};
 #pragma unroll
         for (int t = 0; t < 2; t++) {
@@ -1234,7 +1250,9 @@ __device__ __forceinline__ void fwd_block8(const FwdArgs &a, h16x8 *lds, uint32_
         for (int q = 0; q < NQB; q++) so[q] = fmaf(ws, fmaxf(L == 0 || L == 5 ? sc->ain[0][q] : 0.f, f4get(am, q)), bm);
         col_wave_max(my);
         // this wave's rows are H k-step w: all 8 waves must have read it (and its scales) in this layer
+        DGS_WSTAMP8(40, L);
         if (L > 0) lds_wait_ge(hrd + w, (uint32_t)NW8 * L, lds_peek(hrd + w));
+        DGS_WSTAMP8(48, L);
 #pragma unroll
         for (int q = 0; q < NQB; q++) {
             const Scale s = scale_for(so[q]);
@@ -1246,7 +1264,9 @@ __device__ __forceinline__ void fwd_block8(const FwdArgs &a, h16x8 *lds, uint32_
             for (int t = 0; t < 2; t++) acc_to_lds(c[t][q], lds, G_H, 2 * w + t, q, lane, s.s);
         }
         lds_signal(hwr + w, lane);
+        DGS_WSTAMP8(56, L);
     }
+    DGS_STAMP(20);
     // heads on the last NQB waves (one column tile each), once all 8 layers' writers have signalled
     const int hq = w - (NW8 - NQB);
     if (hq >= 0) {
