@@ -1238,7 +1238,9 @@ __device__ __forceinline__ void fwd_block8(const FwdArgs &a, h16x8 *lds, uint32_
             const int nt = 2 * w + t;
             bias_relu(c[t], a_inv(Aw + t * astride), ib, sb[64 * L + 4 * nt + kq], true);
             trunk_mask(relu_bits(c[t]), L, nt);
+#ifndef DGS_DIAG_NOSAVE  // diagnostic only (wrong backward): the trunk's saved-activation stores skipped
             tile16(a.saved, Ns, s_h(L) + 16 * nt, p0, lane).store(c[t]);
+#endif
             col_absmax(c[t], my);
         }
         // the layer's output scales: max_rows sum |W_L| x max |input| + max |b_L| per column tile (the
@@ -1564,7 +1566,9 @@ __device__ __forceinline__ void bwd_block8(const BwdArgs &a, h16x8 *lds, uint32_
         for (int t = 0; t < 2; t++) {
             scale_tiles(c[t], a_inv(Aw + t * astride), ib);
             mask_apply(c[t], mk[t]);
+#ifndef DGS_DIAG_NOSAVE  // diagnostic only (wrong dW): the dZ chain's stores skipped
             tile16(a.dz, Ns, zrow + 16 * (2 * w + t), p0, lane).store(c[t]);
+#endif
             col_absmax(c[t], my);
         }
         float so[NQB];
