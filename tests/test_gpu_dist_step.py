@@ -7,7 +7,8 @@ post-Adam parameters are bitwise identical on both ranks. "overflow": rank 1's s
 capacity is forced to overflow: on the autograd path BOTH ranks must redo (the agreement), on the native
 path (NativeStep.step_data_parallel) rank 1 redoes alone, its count being known before any collective;
 the result is unchanged either way.
-RCCL itself is unmeasured on hardware here (one GPU); gloo carries the same collectives.
+RCCL refuses two ranks on one GPU, so these carry the collectives over gloo; RCCL itself runs with a
+one-rank group in test_rccl_group_runs_the_data_parallel_step.
 """
 import os
 import socket
@@ -127,3 +128,48 @@ def test_two_rank_loop_stays_replicated_through_densification(tmp_path, variant)
         assert torch.equal(x, y), f"end: parameter {i} differs between ranks"
     # the ranks rendered different frames: their local losses differ (the test is not vacuous)
     assert r0["loss"] != r1["loss"]
+
+
+@pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")
+@pytest.mark.parametrize("reserve", [False, True])
+def test_rccl_group_runs_the_data_parallel_step(tmp_path, reserve):
+    """RCCL itself on the box's one GPU (tests/rccl1_worker.py): a "nccl" process group of one rank,
+    AVG / SUM / MAX and an async all-reduce on a side stream leave the values bitwise unchanged, and the
+    data-parallel step's RCCL-only branches (native step_data_parallel, the autograd path's overlapped
+    reducer, the device-side path agreement; reserve: the opt-in CU reserve and channel cap) run and give
+    the gradients of an un-reduced step (blend atomics: 1e-4 relative + 1e-6 of the tensor's max)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
+               LOCAL_RANK="0")
+    for k in ("NCCL_MAX_NCHANNELS", "DGS_MLP_RESERVE_CUS", "DGS_NATIVE_STEP"):
+        env.pop(k, None)
+    p = subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "rccl1_worker.py"), str(tmp_path)]
+                         + (["reserve"] if reserve else []), env=env, cwd=ROOT)
+    try:
+        rc = p.wait(timeout=100)
+    except subprocess.TimeoutExpired:
+        p.kill()
+        rc = -9
+    assert rc == 0, rc
+    r = torch.load(tmp_path / "rccl.pt", weights_only=True)
+    assert r["backend"] == "nccl" and r["avg"], r
+    assert all(r["ops"].values()), r["ops"]
+    assert r["nchannels"] == ("32" if reserve else None)
+    assert r["reserved_cus"] == (32 if reserve else 0)
+    steps = r["steps"]
+    for path in ("native", "autograd"):
+        local, red = steps[f"{path}-local"], steps[f"{path}-rccl"]
+        assert local["native"] == red["native"] == (path == "native")
+        assert not local["redone"] and not red["redone"]
+        # the local steps issue no collective; the reduced ones go through the RCCL branches: native =
+        # two step_data_parallel calls, each with async Gaussian + network all-reduces (warm) after
+        # the path agreement (one sync MIN); autograd = the hooks' async early reduce + the late one
+        assert local["calls"] == {"allreduce_async": 0, "allreduce_sync": 0, "dp_steps": 0}, local["calls"]
+        c = red["calls"]
+        if path == "native":
+            assert c["dp_steps"] == 2 and c["allreduce_async"] == 4 and c["allreduce_sync"] == 1, c
+        else:
+            assert c["dp_steps"] == 0 and c["allreduce_async"] == 2 and c["allreduce_sync"] >= 2, c
+        assert abs(local["loss"] - red["loss"]) <= 1e-6 * abs(local["loss"])
+        for i, (a, want) in enumerate(zip(red["grads"], local["grads"])):
+            tol = 1e-6 * float(want.abs().max()) + 1e-4 * want.abs()
+            assert bool(((a - want).abs() <= tol).all()), (path, i, float((a - want).abs().max()))
