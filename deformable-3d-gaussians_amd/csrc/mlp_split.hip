@@ -1845,13 +1845,19 @@ __device__ __forceinline__ void dws_run(const WJob &J, size_t Ns, const float *_
         const_cast<float *>(COL ? xb : zb), 0, (int)((COL ? J.krows : J.nrows) * Ns * 4), 0x00020000);
     const bool pact = 32 * wave < (COL ? J.krows : J.nrows);  // this wave has private rows (uniform)
     // private: lane (i, h) holds row 32 w + i, points 8 h .. + 7 of each k-step (fragment layout)
+#ifdef DGS_DIAG_DWS_TILED  // diagnostic (wrong results): chunk-major addressing [chunk][row][32 points]
+    const int pvoff = ((32 * wave + i) * 32 + 8 * h) * 4;
+    const int pcst = (COL ? J.krows : J.nrows) * 128, scst = (COL ? J.nrows : J.krows) * 128;
+#else
     const int pvoff = ((32 * wave + i) * (int)Ns + 8 * h) * 4;
+    constexpr int pcst = 128, scst = 128;
+#endif
     float4 pr[4];  // [k-step][half]
     auto pload = [&](int c) {
 #pragma unroll
         for (int q = 0; q < 4; q++)
             pr[q] = __builtin_bit_cast(float4,
-                                       __builtin_amdgcn_raw_buffer_load_b128(rsP, pvoff, DWS_DIAG_C(c) * 128 + (q >> 1) * 64 + (q & 1) * 16, 0));
+                                       __builtin_amdgcn_raw_buffer_load_b128(rsP, pvoff, DWS_DIAG_C(c) * pcst + (q >> 1) * 64 + (q & 1) * 16, 0));
     };
     // shared staging: slot g = tid + 512 f -> row g >> 3, points 4 (g & 7) .. + 3 of the chunk (8
     // lanes read a row's 128 B)
@@ -1868,7 +1874,11 @@ __device__ __forceinline__ void dws_run(const WJob &J, size_t Ns, const float *_
             int row, q;
             if (sslot(f, row, q))
                 st[f] = __builtin_bit_cast(
-                    float4, __builtin_amdgcn_raw_buffer_load_b128(rsS, (row * (int)Ns + 4 * q) * 4, DWS_DIAG_C(c) * 128, 0));
+#ifdef DGS_DIAG_DWS_TILED
+                    float4, __builtin_amdgcn_raw_buffer_load_b128(rsS, (row * 32 + 4 * q) * 4, DWS_DIAG_C(c) * scst, 0));
+#else
+                    float4, __builtin_amdgcn_raw_buffer_load_b128(rsS, (row * (int)Ns + 4 * q) * 4, DWS_DIAG_C(c) * scst, 0));
+#endif
         }
     };
     float bsum[NSF] = {};  // COL: bias row sums of the staged dZ rows; ROW: bsum[0] of the private row
