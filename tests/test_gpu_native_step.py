@@ -6,7 +6,8 @@ must be bitwise equal; gradients go through the blend backward's float atomics (
 they are compared to 1e-4 relative + 1e-6 of each tensor's max. Variants: the blender network
 (configs 1-3), the 6-DoF screw head (config 4), the non-blender network with an ast_noise frame-time
 offset (config 5), a warm-up iteration (no deformation network), and a forced overflow of the deferred
-pair count (redone synchronously by train_step)."""
+pair count (redone synchronously by train_step). Edge cases: nothing rendered (every Gaussian behind the
+camera) and a single Gaussian."""
 import numpy as np
 import pytest
 import torch
@@ -94,6 +95,75 @@ def test_native_step_matches_autograd_step(name, N, res, is_blender, is_6dof, as
         torch.testing.assert_close(p.grad, want, rtol=1e-4, atol=1e-6 * max(float(want.abs().max()), 1e-30),
                                    msg=lambda m: f"param {i}: {m}")
     assert _lib.load().dgs_debug_guard_expiries() == 0
+
+
+@pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")
+@pytest.mark.parametrize("deferred", [False, True])
+def test_native_step_nothing_rendered(deferred):
+    """Every Gaussian behind the camera (num_rendered = 0: empty tile lists, no pair to sort, blend or
+    replay): the native step and the autograd step give the background image, the same loss, radii 0,
+    nothing visible, and all-zero gradients for every Gaussian and network parameter."""
+    from deformgs.arguments import PipelineParams
+    from deformgs.synthetic import synth_camera
+    from deformgs.train_step import drop_grads, forward_backward, train_step
+    dev = torch.device("cuda", 0)
+    gs, deform = _model(3000, True, False, seed=2)
+    cam = synth_camera(96, 80, index=1, fid=0.2, device=dev)
+    with torch.no_grad():
+        gs._xyz.copy_(cam.camera_center[None] * 1.5 + 0.01 * gs._xyz)
+    gt = torch.rand((3, 80, 96), generator=torch.Generator().manual_seed(3)).to(dev)
+    pipe, bg = PipelineParams(), torch.tensor([0.3, 0.2, 0.1], device=dev)
+    loss_a, pkg_a = forward_backward(gs, deform, cam, gt, pipe, bg)
+    torch.cuda.synchronize()
+    assert int(pkg_a["render"].grad_fn.num_rendered) == 0
+    ref = [None if p.grad is None else p.grad.clone() for p in _params(gs, deform)]
+    drop_grads(gs, deform)
+    loss_n, pkg_n, redone = train_step(gs, deform, cam, gt, pipe, bg, False, deferred_count=deferred)
+    torch.cuda.synchronize()
+    assert getattr(gs, "_dgs_native", None) is not None and not redone
+    assert pkg_n["num_rendered"] == 0
+    assert float(loss_n) == float(loss_a)
+    want = bg[:, None, None].expand(3, 80, 96)
+    assert torch.equal(pkg_n["render"], want) and torch.equal(pkg_a["render"].detach(), want)
+    assert int(pkg_n["radii"].abs().sum()) == 0 and not bool(pkg_n["visibility_filter"].any())
+    for i, (p, r) in enumerate(zip(_params(gs, deform), ref)):
+        assert p.grad is not None and r is not None, i
+        assert float(p.grad.abs().max()) == 0.0 and float(r.abs().max()) == 0.0, i
+
+
+@pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")
+def test_native_step_single_gaussian():
+    """N = 1 (one 16-point tail block of the network kernels, one short tile list per covered tile): one
+    Gaussian at the scene origin, in view; the native step equals the autograd step (image and loss
+    bitwise, gradients to the atomics' 1e-4)."""
+    from deformgs.arguments import PipelineParams
+    from deformgs.synthetic import synth_camera
+    from deformgs.train_step import drop_grads, forward_backward, train_step
+    dev = torch.device("cuda", 0)
+    gs, deform = _model(1, True, False, seed=4)
+    with torch.no_grad():
+        gs._xyz.zero_()
+        gs._scaling.fill_(-2.0)
+        gs._opacity.fill_(1.0)
+    cam = synth_camera(96, 80, index=2, fid=0.6, device=dev)
+    gt = torch.rand((3, 80, 96), generator=torch.Generator().manual_seed(8)).to(dev)
+    pipe, bg = PipelineParams(), torch.zeros(3, device=dev)
+    loss_a, pkg_a = forward_backward(gs, deform, cam, gt, pipe, bg)
+    torch.cuda.synchronize()
+    nr = int(pkg_a["render"].grad_fn.num_rendered)
+    image = pkg_a["render"].detach().clone()
+    ref = [p.grad.clone() for p in _params(gs, deform)]
+    drop_grads(gs, deform)
+    loss_n, pkg_n, redone = train_step(gs, deform, cam, gt, pipe, bg, False)
+    torch.cuda.synchronize()
+    assert getattr(gs, "_dgs_native", None) is not None and not redone
+    assert pkg_n["num_rendered"] == nr > 0
+    assert float(loss_n) == float(loss_a) and torch.equal(pkg_n["render"], image)
+    assert float(image.abs().max()) > 0  # the Gaussian is drawn
+    for i, (p, want) in enumerate(zip(_params(gs, deform), ref)):
+        torch.testing.assert_close(p.grad, want, rtol=1e-4, atol=1e-6 * max(float(want.abs().max()), 1e-30),
+                                   msg=lambda m: f"param {i}: {m}")
+    assert float(gs._xyz.grad.abs().max()) > 0
 
 
 @pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")
