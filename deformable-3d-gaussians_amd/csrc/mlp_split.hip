@@ -2612,10 +2612,15 @@ int backward(int flags, int N, const float *packed, const float *saved, const fl
     return DGS_OK;
 }
 
+// dW launches handed to the fp32 k_dw because a 256-row operand exceeds k_dws's 32-bit byte offsets
+// (N > ~2.1 M points; dgs_debug_dw_fallbacks)
+static std::atomic<long long> g_dw_fallbacks{0};
 static int dw_split_once(const Flags &F, size_t Ns, const float *dz, const float *saved, float *slabs,
                          float *const *grads, hipStream_t stream) {
-    if ((size_t)WT * Ns * 4 >= 0x7fffffffull)  // 32-bit byte offsets of a 256-row operand
+    if ((size_t)WT * Ns * 4 >= 0x7fffffffull) {  // 32-bit byte offsets of a 256-row operand
+        g_dw_fallbacks.fetch_add(1);
         return mlp::dw_fp32(F, Ns, dz, saved, slabs, grads, stream);
+    }
     const WPlan W = split_wplan(F, std::max(32, 256 - reserved_cus()));
     for (int q = 0; q < W.jobs.n; q++) {  // the shapes k_dws instantiates
         const WJob &j = W.jobs.j[q];
@@ -2671,6 +2676,8 @@ extern "C" int dgs_debug_clock(int k, int n, unsigned long long *out) {
 
 extern "C" void dgs_mlp_set_reserved_cus(int k) { mlps::g_reserve_cus.store(k < 0 ? 0 : k > 64 ? 64 : k); }
 extern "C" int dgs_mlp_reserved_cus(void) { return mlps::reserved_cus(); }
+
+extern "C" long long dgs_debug_dw_fallbacks(void) { return mlps::g_dw_fallbacks.load(); }
 
 extern "C" long long dgs_debug_guard_expiries(void) {
     uint32_t v = 0;

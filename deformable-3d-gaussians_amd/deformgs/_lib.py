@@ -58,6 +58,7 @@ _SIGS = {
     "dgs_raster_set_deferred_count": ([I], None),
     "dgs_raster_set_exact_scale_grad": ([I], None),
     "dgs_debug_guard_expiries": ([], ctypes.c_longlong),
+    "dgs_debug_dw_fallbacks": ([], ctypes.c_longlong),
     "dgs_debug_sort_pairs": ([P, P, P, P, I, I, I, P], I),
     "dgs_raster_deferred_overflows": ([], ctypes.c_longlong),
     "dgs_debug_set_binning": ([I], None),

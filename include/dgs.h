@@ -169,6 +169,10 @@ void dgs_raster_set_exact_scale_grad(int on);
  * current device since process start: must be 0; a non-zero count means MLP outputs / gradients of
  * some launch are invalid (GPU tests assert it stays 0). -1 if the counter could not be read. */
 long long dgs_debug_guard_expiries(void);
+/* dW launches of the split-f16 path handed to the fp32 k_dw since process start: a 256-row dZ / saved
+ * operand spans >= 2^31 bytes (N > ~2.1 M points), past k_dws's 32-bit buffer offsets (the fp32 k_dw
+ * takes up to ~8.4 M). Same results to fp32 summation order (tests/test_gpu_mlp.py linearity test). */
+long long dgs_debug_dw_fallbacks(void);
 /* CUs the deformation-MLP kernels leave free for concurrent work on other streams (the data-parallel
  * step's gradient all-reduce under the network backward): the persistent k_fwd / k_bwd
  * grids launch (CUs - k) workgroups and k_dws's plan spans (256 - k). 0..64; default

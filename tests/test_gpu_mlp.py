@@ -337,3 +337,40 @@ def test_tail_blocks_bitwise_equal_64_point_blocks(tmp_path):
     assert set(a.files) == set(b.files) and len(a.files) > 0
     for k in a.files:
         np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+
+
+def test_dw_linearity_past_32bit_operand_offsets():
+    """Maximum size: at N = 2,150,016 points one 256-row dW operand spans more than 2^31 bytes, so the
+    split k_dws (32-bit buffer offsets) hands the dW to the fp32 fallback (mlp_split.hip dw_split_once ->
+    mlp::dw_fp32). Size-independent check of that path: the forward is per point (per 16-point column
+    tile scales: a half split on a tile boundary computes bitwise the same rows), and every parameter
+    gradient is a sum over points, so the full launch must equal the two halves' (each below the limit,
+    on k_dws) to fp32 summation error: 1e-4 of each tensor's max."""
+    net, _ = _net("blender", 11)
+    N = 2_150_016
+    gen = torch.Generator(device="cpu").manual_seed(21)
+    x = (torch.rand((N, 3), generator=gen) * 2 - 1).cuda()
+    G = torch.randn((N, 10), generator=gen).cuda()
+    t = torch.full((1, 1), 0.37, device="cuda")
+
+    def run(xs, gs):
+        net.zero_grad(set_to_none=True)
+        raw = net.raw(xs, t.expand(xs.shape[0], -1))
+        (raw * gs).sum().backward()
+        torch.cuda.synchronize()
+        return raw.detach(), {k: p.grad.detach().clone() for k, p in net.named_parameters()}
+
+    from deformgs import _lib
+    lib = _lib.load()
+    f0 = lib.dgs_debug_dw_fallbacks()
+    raw_full, g_full = run(x, G)
+    assert lib.dgs_debug_dw_fallbacks() == f0 + 1, "the full launch must take the fp32 dW fallback"
+    h = N // 2
+    raw_a, g_a = run(x[:h].contiguous(), G[:h].contiguous())
+    raw_b, g_b = run(x[h:].contiguous(), G[h:].contiguous())
+    assert lib.dgs_debug_dw_fallbacks() == f0 + 1, "the halves run k_dws"
+    assert torch.equal(raw_full, torch.cat([raw_a, raw_b]))
+    for k, gf in g_full.items():
+        want = g_a[k] + g_b[k]
+        tol = 1e-4 * float(want.abs().max())
+        assert float((gf - want).abs().max()) <= tol, (k, float((gf - want).abs().max()), tol)
