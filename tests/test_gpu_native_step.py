@@ -50,6 +50,7 @@ CASES = [
     ("6dof", 12000, 320, True, True, 0.0, True),
     ("nonblender-noise", 12000, 320, False, False, -0.021, True),
     ("warmup", 8000, 256, True, False, 0.0, False),
+    ("blender-1M", 1_000_000, 800, True, False, 0.0, True),  # 10x the bench's Gaussians, ~10 M pairs
 ]
 
 
