@@ -458,12 +458,13 @@ def main():
             "frac_fp32_basis": (mlp_flop / (FP32_MFMA_PEAK_TFLOPS * 1e12) + raster_bytes / (HBM_PEAK_GBS * 1e9)) / step_s,
             "note": "kernel frac is vs the split-f16 ceiling (2.5 PF f16 / 3); vs the 157.3 TF fp32 MFMA peak the "
                     "split kernels can exceed 1 (three f16 products per fp32 product at 16x the fp32 rate)"}
+    scene = "synth-100k" if N == 100_000 else f"synth-{N // 1000}k (the synth-100k protocol at {N} Gaussians)"
     result = {
         "metric": f"train iters/s (deform+raster fwd+bwd), {N // 1000}k Gaussians @ {R}x{R}",
         "value": value, "unit": "iters/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "fp32", "data": "synthetic (synth-100k, random-init weights, targets = initial renders + noise)",
-        "config": {"workload": f"synth-100k: {N} Gaussians, {R}x{R}, blender DeformNetworkBaseline"
+        "vs_baseline": None, "dtype": "fp32", "data": f"synthetic ({scene}, random-init weights, targets = initial renders + noise)",
+        "config": {"workload": f"{scene}: {N} Gaussians, {R}x{R}, blender DeformNetworkBaseline"
                    + (" (6-DoF screw head)" if six else "") + ", SH3"
                    + (" (raw-init heads)" if args.raw_init else " (heads at 1/100 init: steady-state deltas)"),
                    "global_batch": world, "includes_adam": not args.no_adam, "pairs_per_render": P_pairs,
