@@ -165,6 +165,9 @@ VARIANTS = [
     ("blender-cfg3", 55000, 800, True, False, 0.0),
     ("6dof-cfg4", 78600, 800, True, True, 0.0),
     ("nonblender-cfg5", 55000, 800, False, False, 0.0137),
+    # a ragged, non-square frame (W x H = 537 x 301: partial blend tiles on two edges, partial SSIM tiles,
+    # the network's 16-point tail blocks at N = 12003)
+    ("blender-ragged", 12003, (537, 301), True, False, 0.0),
     # the configuration bench.py times: synth-100k (seed 0) at 800^2, blender network, heads at 1/100,
     # one of its cameras, its target (that camera's initial render + N(0, 0.02), clamped)
     ("bench-100k", 100_000, 800, True, False, 0.0),
@@ -191,6 +194,7 @@ def test_training_step_vs_oracle_chain(name, N, res, is_blender, is_6dof, ast_no
     from weights import mlp_weights
     dev = torch.device("cuda", 0)
     bench = name == "bench-100k"
+    W, H = res if isinstance(res, tuple) else (res, res)
     g = synth_gaussians(N, seed=0 if bench else 2, device=dev)
     gs = GaussianModel(3)
     gs.from_tensors(g["xyz"], g["features_dc"], g["features_rest"], g["scaling"], g["rotation"], g["opacity"])
@@ -212,8 +216,8 @@ def test_training_step_vs_oracle_chain(name, N, res, is_blender, is_6dof, ast_no
             gt = (img0 + 0.02 * noise).clamp_(0.0, 1.0).contiguous()
             del d, img0
     else:
-        cam = synth_camera(res, res, index=1, fid=0.37, device=dev)
-        gt = torch.rand((3, res, res), generator=torch.Generator().manual_seed(9)).to(dev)
+        cam = synth_camera(W, H, index=1, fid=0.37, device=dev)
+        gt = torch.rand((3, H, W), generator=torch.Generator().manual_seed(9)).to(dev)
     noise = torch.full((1, 1), ast_noise, device=dev) if ast_noise else 0.0
     # the frame time the network sees: fp32 fid + fp32 noise (train_step adds them on the device)
     t_value = float((cam.fid.unsqueeze(0) + (noise if ast_noise else 0.0)).reshape(-1)[0].item())
@@ -243,7 +247,7 @@ def test_training_step_vs_oracle_chain(name, N, res, is_blender, is_6dof, ast_no
                                      deferred_count=True)
         assert not deferred_overflowed()
     torch.cuda.synchronize()
-    want_loss, want, o, c = _oracle_step(w, g, cam, gt, N, res, res, masks, is_blender, is_6dof, t_value)
+    want_loss, want, o, c = _oracle_step(w, g, cam, gt, N, H, W, masks, is_blender, is_6dof, t_value)
     # the loss bar: 2e-6 relative plus twice the reference's own fp32 rounding of the loss on this image
     # (its fp32 L1 + SSIM of the oracle's image vs the float64 value): against a target close to the
     # render (bench-100k) the SSIM variances E[I^2] - mu^2 cancel, and any fp32 evaluation, the
