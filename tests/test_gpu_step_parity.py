@@ -168,6 +168,8 @@ VARIANTS = [
     # a ragged, non-square frame (W x H = 537 x 301: partial blend tiles on two edges, partial SSIM tiles,
     # the network's 16-point tail blocks at N = 12003)
     ("blender-ragged", 12003, (537, 301), True, False, 0.0),
+    ("6dof-ragged", 9001, (333, 250), True, True, 0.0),
+    ("nonblender-ragged", 7777, (250, 347), False, False, -0.0091),
     # the configuration bench.py times: synth-100k (seed 0) at 800^2, blender network, heads at 1/100,
     # one of its cameras, its target (that camera's initial render + N(0, 0.02), clamped)
     ("bench-100k", 100_000, 800, True, False, 0.0),
